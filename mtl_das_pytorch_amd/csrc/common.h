@@ -1,0 +1,151 @@
+// Common device helpers for the gfx950 (MI355X / CDNA4) kernels of mtl_das_pytorch_amd.
+//
+// Conventions used by every kernel in this directory:
+//   * activations are NHWC, addressed as rows of pixels with a row pitch `ld` (elements), so a
+//     channel slice of a concatenation buffer is just (base + channel_offset, ld = total_channels);
+//   * MFMA operands are bf16, accumulation and every reduction is fp32;
+//   * gradient buffers of activations are fp32 and written exactly once (no read-modify-write);
+//     a consumer that needs the sum of several gradient sources takes a GradSrcs list;
+//   * per-channel BN statistics are accumulated into NREP replicas (blockIdx % NREP) to spread
+//     atomic contention over the 8 XCD L2s; consumers sum the replicas;
+//   * wave size is 64; blocks are 256 threads (4 waves).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define DEV __device__ __forceinline__
+
+namespace mda {
+
+constexpr int NREP = 8;  // BN-statistic replicas
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t bf16_t;  // raw bf16 storage
+
+DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+// round-to-nearest-even; NaN-preserving via the hardware conversion
+DEV bf16_t f2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return *reinterpret_cast<bf16_t*>(&h);
+}
+
+DEV void load8(const bf16_t* p, float* v) {
+  uint4 u = *reinterpret_cast<const uint4*>(p);
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+DEV void store8(bf16_t* p, const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+DEV void load8f(const float* p, float* v) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+DEV void store8f(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Parameter structs (passed by value as kernel arguments)
+// ---------------------------------------------------------------------------------------------
+
+// A bf16 NHWC source made of up to two channel segments (e.g. cat[F_shared, B_task]).
+// Segment s covers channels [s ? C0 : 0, s ? C0 + C1 : C0). `gs` = element stride per group
+// (grid.z); 0 means the segment is shared by every group.
+struct Src2 {
+  const bf16_t* p[2];
+  int64_t gs[2];
+  int ld[2];
+  int C0, C1;
+};
+
+// Up to 6 fp32 gradient sources summed on load (deterministic gradient accumulation).
+struct GradSrcs {
+  const float* p[6];
+  int64_t gs[6];
+  int ld[6];
+  int n;
+};
+
+DEV void gsum8(const GradSrcs& g, int z, int64_t pix, int c, float* v) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  for (int s = 0; s < g.n; ++s) {
+    float t[8];
+    load8f(g.p[s] + g.gs[s] * z + pix * g.ld[s] + c, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += t[j];
+  }
+}
+
+// Per-BN-layer state. Everything is indexed by group z with the given strides (0 = shared).
+struct BNArgs {
+  const float* stats;    // [G][NREP][2][C] sums of y and y^2 (training) -- zeroed every step
+  const float* gamma;    // [C] (+ z * pstride)
+  const float* beta;
+  float* run_mean;       // running stats (+ z * pstride)
+  float* run_var;
+  int64_t* nbt;          // num_batches_tracked (+ z)
+  int64_t pstride;       // element stride of gamma/beta/running stats between groups
+  int C;
+  int count;             // number of elements per channel reduced into stats (B*H*W)
+  float eps, momentum;
+  int training;          // 1: batch statistics (and update running), 0: running statistics
+};
+
+// Computes per-channel scale/shift into LDS: out = y * scale + shift == gamma * (y - mean) / std + beta
+// Also returns mean and invstd arrays when requested (needed by backward kernels).
+DEV void bn_prepare(const BNArgs& a, int z, float* s_scale, float* s_shift, float* s_mean, float* s_invstd,
+                    bool update_running) {
+  const float* st = a.stats + (int64_t)z * NREP * 2 * a.C;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    float mean, var;
+    if (a.training) {
+      float s = 0.f, ss = 0.f;
+#pragma unroll
+      for (int r = 0; r < NREP; ++r) { s += st[r * 2 * a.C + c]; ss += st[r * 2 * a.C + a.C + c]; }
+      float inv_n = 1.f / (float)a.count;
+      mean = s * inv_n;
+      var = fmaxf(ss * inv_n - mean * mean, 0.f);
+      if (update_running) {
+        float unb = a.count > 1 ? var * (float)a.count / (float)(a.count - 1) : var;
+        float* rm = a.run_mean + a.pstride * z;
+        float* rv = a.run_var + a.pstride * z;
+        rm[c] = (1.f - a.momentum) * rm[c] + a.momentum * mean;
+        rv[c] = (1.f - a.momentum) * rv[c] + a.momentum * unb;
+      }
+    } else {
+      mean = a.run_mean[a.pstride * z + c];
+      var = a.run_var[a.pstride * z + c];
+    }
+    float inv = rsqrtf(var + a.eps);
+    float g = a.gamma[a.pstride * z + c], b = a.beta[a.pstride * z + c];
+    s_scale[c] = g * inv;
+    s_shift[c] = b - mean * g * inv;
+    if (s_mean) s_mean[c] = mean;
+    if (s_invstd) s_invstd[c] = inv;
+  }
+  if (update_running && a.training && threadIdx.x == 0 && a.nbt) a.nbt[z] += 1;
+}
+
+}  // namespace mda
