@@ -1,0 +1,234 @@
+// pybind11 bindings of the HIP kernel library (module `_mda_hip`).
+//
+// The Python side (mtl_das_pytorch_amd/ops/hip.py) passes raw device pointers (tensor.data_ptr()),
+// the current HIP stream handle (torch.cuda.current_stream().cuda_stream) and plain dicts of kernel
+// arguments; no PyTorch C++ headers are needed, so the library builds in seconds with hipcc and shares
+// the HIP runtime (libamdhip64.so.7) that torch has already loaded into the process.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace py = pybind11;
+using namespace mda;
+
+namespace {
+
+int64_t I(const py::dict& d, const char* k, int64_t dflt = 0) {
+  if (!d.contains(k)) return dflt;
+  py::object o = d[k];
+  if (o.is_none()) return dflt;
+  return o.cast<int64_t>();
+}
+double F(const py::dict& d, const char* k, double dflt = 0.0) {
+  if (!d.contains(k)) return dflt;
+  py::object o = d[k];
+  if (o.is_none()) return dflt;
+  return o.cast<double>();
+}
+template <typename T>
+T* P(const py::dict& d, const char* k) {
+  return reinterpret_cast<T*>(static_cast<intptr_t>(I(d, k, 0)));
+}
+hipStream_t S(int64_t s) { return reinterpret_cast<hipStream_t>(static_cast<intptr_t>(s)); }
+
+void check(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string("mtl_das_pytorch_amd HIP launch failed: ") + what + " rc=" + std::to_string(rc));
+}
+
+Src2 parse_src(const py::dict& d) {
+  Src2 s{};
+  s.p[0] = P<const bf16_t>(d, "p0");
+  s.p[1] = P<const bf16_t>(d, "p1");
+  s.gs[0] = I(d, "gs0");
+  s.gs[1] = I(d, "gs1");
+  s.ld[0] = (int)I(d, "ld0");
+  s.ld[1] = (int)I(d, "ld1", s.ld[0]);
+  s.C0 = (int)I(d, "C0");
+  s.C1 = (int)I(d, "C1");
+  return s;
+}
+
+GradSrcs parse_grads(const py::list& l) {
+  GradSrcs g{};
+  if (l.size() > 6) throw std::runtime_error("at most 6 gradient sources");
+  g.n = (int)l.size();
+  for (int i = 0; i < g.n; ++i) {
+    py::tuple t = l[i].cast<py::tuple>();
+    g.p[i] = reinterpret_cast<const float*>(static_cast<intptr_t>(t[0].cast<int64_t>()));
+    g.gs[i] = t[1].cast<int64_t>();
+    g.ld[i] = t[2].cast<int>();
+  }
+  return g;
+}
+
+BNArgs parse_bn(const py::dict& d) {
+  BNArgs b{};
+  b.stats = P<const float>(d, "stats");
+  b.gamma = P<const float>(d, "gamma");
+  b.beta = P<const float>(d, "beta");
+  b.run_mean = P<float>(d, "run_mean");
+  b.run_var = P<float>(d, "run_var");
+  b.nbt = P<int64_t>(d, "nbt");
+  b.pstride = I(d, "pstride");
+  b.C = (int)I(d, "C");
+  b.count = (int)I(d, "count");
+  b.eps = (float)F(d, "eps", 1e-5);
+  b.momentum = (float)F(d, "momentum", 0.1);
+  b.training = (int)I(d, "training", 1);
+  return b;
+}
+
+void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
+  ConvArgs a{};
+  a.src = parse_src(d["src"].cast<py::dict>());
+  a.w = P<const bf16_t>(d, "w");
+  a.wgs = I(d, "wgs");
+  a.bias = P<const float>(d, "bias");
+  a.bgs = I(d, "bgs");
+  a.out = P<void>(d, "out");
+  a.ogs = I(d, "ogs");
+  a.ldo = (int)I(d, "ldo");
+  a.stats = P<float>(d, "stats");
+  a.B = (int)I(d, "B"); a.Hs = (int)I(d, "Hs"); a.Ws = (int)I(d, "Ws"); a.Ho = (int)I(d, "Ho"); a.Wo = (int)I(d, "Wo");
+  a.N = (int)I(d, "N"); a.Npad = (int)I(d, "Npad"); a.Cs = (int)I(d, "Cs");
+  a.KH = (int)I(d, "KH"); a.KW = (int)I(d, "KW"); a.sh = (int)I(d, "sh"); a.sw = (int)I(d, "sw");
+  a.ph = (int)I(d, "ph"); a.pw = (int)I(d, "pw"); a.Kpad = (int)I(d, "Kpad");
+  if (a.Cs % 8 || a.N % 4 || a.Kpad % 32 || a.src.C0 + a.src.C1 != a.Cs) throw std::runtime_error("conv: bad geometry");
+  check(launch_conv(mode, a, G, cfg, S(stream)), "conv");
+}
+
+void wgrad(int cfg, int G, int64_t stream, py::dict d) {
+  WgradArgs a{};
+  a.src = parse_src(d["src"].cast<py::dict>());
+  a.dy = P<const bf16_t>(d, "dy");
+  a.dgs = I(d, "dgs");
+  a.ldd = (int)I(d, "ldd");
+  a.slab = P<float>(d, "slab");
+  a.splits = (int)I(d, "splits"); a.m_per_split = (int)I(d, "m_per_split");
+  a.B = (int)I(d, "B"); a.Hi = (int)I(d, "Hi"); a.Wi = (int)I(d, "Wi"); a.Ho = (int)I(d, "Ho"); a.Wo = (int)I(d, "Wo");
+  a.Co = (int)I(d, "Co"); a.Npad = (int)I(d, "Npad"); a.Cs = (int)I(d, "Cs");
+  a.KH = (int)I(d, "KH"); a.KW = (int)I(d, "KW"); a.sh = (int)I(d, "sh"); a.sw = (int)I(d, "sw");
+  a.ph = (int)I(d, "ph"); a.pw = (int)I(d, "pw"); a.Kpad = (int)I(d, "Kpad");
+  if (a.Cs % 8 || a.Co % 8 || a.Kpad % 64) throw std::runtime_error("wgrad: bad geometry");
+  check(launch_wgrad(a, G, cfg, S(stream)), "wgrad");
+}
+
+void wgrad_finalize(int64_t descs, int nd, int64_t nblocks, double scale, int64_t stream) {
+  check(launch_wgrad_finalize(reinterpret_cast<const WgFinDesc*>(static_cast<intptr_t>(descs)), nd, nblocks,
+                              (float)scale, S(stream)), "wgrad_finalize");
+}
+
+TailArgs parse_tail(const py::dict& d) {
+  TailArgs a{};
+  a.y = P<const bf16_t>(d, "y"); a.ygs = I(d, "ygs"); a.ldy = (int)I(d, "ldy");
+  a.bn = parse_bn(d["bn"].cast<py::dict>());
+  a.r = P<const bf16_t>(d, "r"); a.rgs = I(d, "rgs"); a.ldr = (int)I(d, "ldr");
+  if (d.contains("bn2") && !d["bn2"].is_none()) { a.bn2 = parse_bn(d["bn2"].cast<py::dict>()); a.r_bn = 1; }
+  a.out = P<bf16_t>(d, "out"); a.ogs = I(d, "ogs"); a.ldo = (int)I(d, "ldo");
+  a.B = (int)I(d, "B"); a.H = (int)I(d, "H"); a.W = (int)I(d, "W"); a.C = (int)I(d, "C");
+  if (d.contains("g")) a.g = parse_grads(d["g"].cast<py::list>());
+  a.ws = P<float>(d, "ws"); a.ws2 = P<float>(d, "ws2");
+  a.side = P<float>(d, "side"); a.sgs = I(d, "sgs"); a.lds = (int)I(d, "lds");
+  a.dy = P<bf16_t>(d, "dy"); a.dgs = I(d, "dgs"); a.ldd = (int)I(d, "ldd");
+  a.dy2 = P<bf16_t>(d, "dy2"); a.d2gs = I(d, "d2gs"); a.ldd2 = (int)I(d, "ldd2");
+  a.dgamma = P<float>(d, "dgamma"); a.dbeta = P<float>(d, "dbeta");
+  a.dgamma2 = P<float>(d, "dgamma2"); a.dbeta2 = P<float>(d, "dbeta2");
+  a.pgs = I(d, "pgs");
+  if (a.C % 8 || a.C > 2048) throw std::runtime_error("tail: C must be a multiple of 8 and <= 2048");
+  return a;
+}
+
+void tail_fwd(int kind, int G, int blocks, int64_t stream, py::dict d) {
+  check(launch_tail_fwd(kind, parse_tail(d), G, blocks, S(stream)), "tail_fwd");
+}
+void tail_bwd(int kind, int G, int blocks, int64_t stream, py::dict d) {
+  check(launch_tail_bwd(kind, parse_tail(d), G, blocks, S(stream)), "tail_bwd");
+}
+
+void mtl_head(int64_t stream, py::dict d) {
+  HeadArgs a{};
+  a.feat = P<const bf16_t>(d, "feat"); a.fgs = I(d, "fgs"); a.ldf = (int)I(d, "ldf");
+  a.labels = P<const int64_t>(d, "labels"); a.lab_stride = (int)I(d, "lab_stride"); a.lab_off = (int)I(d, "lab_off");
+  a.T = (int)I(d, "T"); a.B = (int)I(d, "B"); a.HW = (int)I(d, "HW"); a.C = (int)I(d, "C");
+  py::list ncls = d["ncls"].cast<py::list>(), w = d["w"].cast<py::list>();
+  if (a.T > 4 || (int)ncls.size() != a.T || (int)w.size() != a.T) throw std::runtime_error("mtl_head: bad task list");
+  for (int t = 0; t < a.T; ++t) { a.ncls[t] = ncls[t].cast<int>(); a.w[t] = w[t].cast<float>(); if (a.ncls[t] > 16) throw std::runtime_error("ncls > 16"); }
+  a.logp = P<float>(d, "logp"); a.dfeat = P<float>(d, "dfeat"); a.dgs = I(d, "dgs");
+  a.metrics = P<float>(d, "metrics"); a.confusion = P<int>(d, "confusion");
+  a.nvalid = P<const int64_t>(d, "nvalid");
+  check(launch_mtl_head(a, S(stream)), "mtl_head");
+}
+
+void cls_head(int64_t stream, py::dict d) {
+  ClsArgs a{};
+  a.x = P<const bf16_t>(d, "x"); a.ldx = (int)I(d, "ldx");
+  a.W = P<const float>(d, "W"); a.bias = P<const float>(d, "bias");
+  a.labels = P<const int64_t>(d, "labels");
+  a.B = (int)I(d, "B"); a.HW = (int)I(d, "HW"); a.C = (int)I(d, "C"); a.N = (int)I(d, "N");
+  a.p_drop = (float)F(d, "p_drop");
+  a.seed = P<const int64_t>(d, "seed");
+  a.feat = P<float>(d, "feat"); a.logits = P<float>(d, "logits"); a.dlogits = P<float>(d, "dlogits");
+  a.dx = P<float>(d, "dx"); a.metrics = P<float>(d, "metrics"); a.confusion = P<int>(d, "confusion");
+  a.dW = P<float>(d, "dW"); a.db = P<float>(d, "db");
+  a.nvalid = P<const int64_t>(d, "nvalid");
+  check(launch_cls_head(a, P<int64_t>(d, "seed"), S(stream)), "cls_head");
+}
+
+void gather_batch(int64_t X, int64_t idx, int64_t lab, int lab_w, int64_t out, int64_t lab_out, int B, int Cin, int H,
+                  int W, int64_t stream) {
+  check(launch_gather_batch(reinterpret_cast<const float*>(X), reinterpret_cast<const int64_t*>(idx),
+                            reinterpret_cast<const int64_t*>(lab), lab_w, reinterpret_cast<bf16_t*>(out),
+                            reinterpret_cast<int64_t*>(lab_out), B, Cin, H, W, S(stream)), "gather_batch");
+}
+
+void pool3(int is_max, int backward, int64_t stream, py::dict d) {
+  PoolArgs a{};
+  a.x = P<const bf16_t>(d, "x"); a.ldx = (int)I(d, "ldx");
+  a.y = P<bf16_t>(d, "y"); a.ldy = (int)I(d, "ldy");
+  a.g = P<const float>(d, "g"); a.ldg = (int)I(d, "ldg");
+  a.dx = P<float>(d, "dx"); a.lddx = (int)I(d, "lddx");
+  a.B = (int)I(d, "B"); a.H = (int)I(d, "H"); a.W = (int)I(d, "W"); a.C = (int)I(d, "C");
+  a.Ho = (int)I(d, "Ho"); a.Wo = (int)I(d, "Wo");
+  if (a.C % 8) throw std::runtime_error("pool3: C % 8");
+  check(launch_pool3(is_max, backward, a, S(stream)), "pool3");
+}
+
+void grad_sum(py::list g, int64_t out, int ldo, int64_t M, int C, int64_t stream) {
+  check(launch_grad_sum(parse_grads(g), reinterpret_cast<float*>(out), ldo, M, C, S(stream)), "grad_sum");
+}
+
+void adam_pack(int64_t stream, py::dict d) {
+  AdamArgs a{};
+  a.p = P<float>(d, "p"); a.g = P<const float>(d, "g"); a.m = P<float>(d, "m"); a.v = P<float>(d, "v");
+  a.lr = P<const float>(d, "lr"); a.step = P<const float>(d, "step");
+  a.b1 = (float)F(d, "b1", 0.9); a.b2 = (float)F(d, "b2", 0.999); a.eps = (float)F(d, "eps", 1e-8);
+  a.wd = (float)F(d, "wd", 0.0); a.grad_scale = (float)F(d, "grad_scale", 1.0);
+  a.update = (int)I(d, "update", 1);
+  check(launch_adam_pack(a, P<const OptSeg>(d, "segs"), (int)I(d, "nsegs"), I(d, "nblocks"), S(stream)), "adam_pack");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_mda_hip, m) {
+  m.doc() = "gfx950 HIP kernels of mtl_das_pytorch_amd";
+  m.attr("NREP") = NREP;
+  m.attr("SIZEOF_WGFIN") = (int)sizeof(WgFinDesc);
+  m.attr("SIZEOF_OPTSEG") = (int)sizeof(OptSeg);
+  m.def("conv", &conv);
+  m.def("wgrad", &wgrad);
+  m.def("wgrad_finalize", &wgrad_finalize);
+  m.def("tail_fwd", &tail_fwd);
+  m.def("tail_bwd", &tail_bwd);
+  m.def("mtl_head", &mtl_head);
+  m.def("cls_head", &cls_head);
+  m.def("gather_batch", &gather_batch);
+  m.def("pool3", &pool3);
+  m.def("grad_sum", &grad_sum);
+  m.def("adam_pack", &adam_pack);
+  m.def("hip_device_sync", []() { return (int)hipDeviceSynchronize(); });
+}

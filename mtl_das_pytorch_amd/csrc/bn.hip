@@ -1,0 +1,392 @@
+// Fused training-mode BatchNorm tails (forward) and BatchNorm backward for NHWC bf16 activations.
+//
+// Forward "tails" consume the pre-BN conv output y (whose per-channel sums were accumulated by the
+// conv epilogue) and fuse everything that follows a BN in the reference models:
+//   ACT_NONE / ACT_RELU / ACT_SIGMOID  BN -> act                  (modelA conv1, resblock left.1-2,
+//                                                                 att gen .1-.2, Inception BasicConv2d)
+//   SIGMUL     sigmoid(BN(y)) * F      attention mask applied to the shared feature
+//                                       (modelA_MTL.py:42-50 + :144,151,157,163)
+//   ADD_RELU   relu(BN(y) + BN2(y2))  or relu(BN(y) + x): ResBlock tail (modelA_MTL.py:27-32)
+//   POOL_RELU  maxpool2x2_ceil(relu(BN(y))) written straight into the upper half of the next level's
+//              concat input (modelA_MTL.py:101-116, 145-159) -- no torch.cat, no pool indices stored.
+// Block 0 of each group also updates running_mean / running_var (momentum, unbiased variance) and
+// num_batches_tracked, matching nn.BatchNorm2d in train mode.
+//
+// Backward is two launches per fused op: `reduce` recomputes dz (the gradient w.r.t. the BN output)
+// from the saved bf16 y and the upstream fp32 gradients, and accumulates sum(dz), sum(dz * xhat);
+// `apply` recomputes dz and writes dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)) as the bf16
+// operand of the conv dgrad/wgrad, and block 0 stores d(gamma), d(beta) into the flat gradient buffer.
+// Side outputs (written once, fp32): SIGMUL -> g*sigmoid (gradient of the shared feature F),
+// ADD_RELU with identity shortcut -> dz (gradient of the block input through the shortcut).
+#include "kernels.h"
+
+namespace mda {
+
+
+
+// thread -> (channel group, pixel lane) mapping shared by every kernel here
+struct Lanes {
+  int CG, PL, cg, pl;
+  bool active;
+  DEV Lanes(int C) {
+    CG = C >> 3;
+    PL = 256 / CG;
+    cg = threadIdx.x % CG;
+    pl = threadIdx.x / CG;
+    active = pl < PL;
+  }
+};
+
+template <int KIND>
+__global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
+  extern __shared__ float sm[];
+  float* s_sc = sm;
+  float* s_sh = sm + a.C;
+  float* s_sc2 = sm + 2 * a.C;
+  float* s_sh2 = sm + 3 * a.C;
+  const int z = blockIdx.z;
+  const bool upd = blockIdx.x == 0;
+  bn_prepare(a.bn, z, s_sc, s_sh, nullptr, nullptr, upd);
+  if (KIND == ADD_RELU && a.r_bn) bn_prepare(a.bn2, z, s_sc2, s_sh2, nullptr, nullptr, upd);
+  __syncthreads();
+  Lanes L(a.C);
+  if (!L.active) return;
+  const int c = L.cg * 8;
+  const bf16_t* yz = a.y + a.ygs * z;
+  bf16_t* oz = a.out + a.ogs * z;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = s_sc[c + j]; sh[j] = s_sh[c + j]; }
+
+  if (KIND == POOL_RELU) {
+    const int Hp = (a.H + 1) >> 1, Wp = (a.W + 1) >> 1;
+    const int Mp = a.B * Hp * Wp;
+    for (int p = blockIdx.x * L.PL + L.pl; p < Mp; p += gridDim.x * L.PL) {
+      int b = p / (Hp * Wp), r = p - b * Hp * Wp;
+      int hp = r / Wp, wp = r - hp * Wp;
+      float mx[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mx[j] = 0.f;  // relu output >= 0, window never empty
+      for (int dh = 0; dh < 2; ++dh) {
+        int h = 2 * hp + dh;
+        if (h >= a.H) break;
+        for (int dw = 0; dw < 2; ++dw) {
+          int w = 2 * wp + dw;
+          if (w >= a.W) break;
+          float v[8];
+          load8(yz + ((int64_t)(b * a.H + h) * a.W + w) * a.ldy + c, v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) mx[j] = fmaxf(mx[j], v[j] * sc[j] + sh[j]);
+        }
+      }
+      store8(oz + (int64_t)p * a.ldo + c, mx);
+    }
+    return;
+  }
+
+  float sc2[8], sh2[8];
+  if (KIND == ADD_RELU && a.r_bn) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc2[j] = s_sc2[c + j]; sh2[j] = s_sh2[c + j]; }
+  }
+  const bf16_t* rz = a.r ? a.r + a.rgs * z : nullptr;
+  const int M = a.B * a.H * a.W;
+  for (int p = blockIdx.x * L.PL + L.pl; p < M; p += gridDim.x * L.PL) {
+    float v[8];
+    load8(yz + (int64_t)p * a.ldy + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
+    if (KIND == ACT_RELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+    } else if (KIND == ACT_SIGMOID) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = sigmoidf_(v[j]);
+    } else if (KIND == SIGMUL) {
+      float f[8];
+      load8(rz + (int64_t)p * a.ldr + c, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = sigmoidf_(v[j]) * f[j];
+    } else if (KIND == ADD_RELU) {
+      float f[8];
+      load8(rz + (int64_t)p * a.ldr + c, f);
+      if (a.r_bn) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = f[j] * sc2[j] + sh2[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] + f[j], 0.f);
+    }
+    store8(oz + (int64_t)p * a.ldo + c, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------------
+struct BwdCtx {
+  float sc[8], sh[8], mean[8], inv[8];
+  float sc2[8], sh2[8], mean2[8], inv2[8];
+};
+
+// dz for the 8 channels [c, c+8) at pre-pool pixel p; also returns xhat (and xhat2 for ADD_RELU+BN2)
+// and the side output value.
+template <int KIND>
+DEV void compute_dz(const TailArgs& a, const BwdCtx& X, int z, int p, int c, float* dz, float* xh, float* xh2,
+                    float* side) {
+  const bf16_t* yz = a.y + a.ygs * z;
+  float y[8];
+  load8(yz + (int64_t)p * a.ldy + c, y);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) xh[j] = (y[j] - X.mean[j]) * X.inv[j];
+  if (KIND == POOL_RELU) {
+    const int HW = a.H * a.W;
+    int b = p / HW, r = p - b * HW;
+    int h = r / a.W, w = r - h * a.W;
+    const int Hp = (a.H + 1) >> 1, Wp = (a.W + 1) >> 1;
+    const int hp = h >> 1, wp = w >> 1;
+    float g[8];
+    gsum8(a.g, z, (int64_t)(b * Hp + hp) * Wp + wp, c, g);
+    // window argmax (first max in row-major scan, as torch max_pool2d) of relu(BN(y))
+    float mx[8];
+    int am[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mx[j] = -1.f; am[j] = -1; }
+    for (int dh = 0; dh < 2; ++dh) {
+      int hh = 2 * hp + dh;
+      if (hh >= a.H) break;
+      for (int dw = 0; dw < 2; ++dw) {
+        int ww = 2 * wp + dw;
+        if (ww >= a.W) break;
+        float v[8];
+        load8(yz + ((int64_t)(b * a.H + hh) * a.W + ww) * a.ldy + c, v);
+        int id = dh * 2 + dw;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = fmaxf(v[j] * X.sc[j] + X.sh[j], 0.f);
+          if (t > mx[j]) { mx[j] = t; am[j] = id; }
+        }
+      }
+    }
+    const int me = (h - 2 * hp) * 2 + (w - 2 * wp);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dz[j] = (am[j] == me && mx[j] > 0.f) ? g[j] : 0.f;
+    return;
+  }
+  float g[8];
+  gsum8(a.g, z, p, c, g);
+  if (KIND == ACT_NONE) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dz[j] = g[j];
+  } else if (KIND == ACT_RELU) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dz[j] = (y[j] * X.sc[j] + X.sh[j]) > 0.f ? g[j] : 0.f;
+  } else if (KIND == ACT_SIGMOID) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { float s = sigmoidf_(y[j] * X.sc[j] + X.sh[j]); dz[j] = g[j] * s * (1.f - s); }
+  } else if (KIND == SIGMUL) {
+    float f[8];
+    load8(a.r + a.rgs * z + (int64_t)p * a.ldr + c, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = sigmoidf_(y[j] * X.sc[j] + X.sh[j]);
+      dz[j] = g[j] * f[j] * s * (1.f - s);
+      side[j] = g[j] * s;
+    }
+  } else if (KIND == ADD_RELU) {
+    float f[8];
+    load8(a.r + a.rgs * z + (int64_t)p * a.ldr + c, f);
+    if (a.r_bn) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xh2[j] = (f[j] - X.mean2[j]) * X.inv2[j];
+        f[j] = f[j] * X.sc2[j] + X.sh2[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dz[j] = (y[j] * X.sc[j] + X.sh[j] + f[j]) > 0.f ? g[j] : 0.f;
+      side[j] = dz[j];
+    }
+  }
+}
+
+template <int KIND>
+DEV void load_ctx(const TailArgs& a, BwdCtx& X, const float* s_sc, const float* s_sh, const float* s_mean,
+                  const float* s_inv, int c) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    X.sc[j] = s_sc[c + j]; X.sh[j] = s_sh[c + j]; X.mean[j] = s_mean[c + j]; X.inv[j] = s_inv[c + j];
+  }
+  if (KIND == ADD_RELU && a.r_bn) {
+    const int C = a.C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      X.sc2[j] = s_sc[4 * C + c + j]; X.sh2[j] = s_sh[4 * C + c + j];
+      X.mean2[j] = s_mean[4 * C + c + j]; X.inv2[j] = s_inv[4 * C + c + j];
+    }
+  }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void tail_bwd_reduce_kernel(TailArgs a) {
+  extern __shared__ float sm[];
+  const int C = a.C;
+  // [0..4C): sc, sh, mean, inv of BN1; [4C..8C): BN2; then partial sums [PL][3][C]
+  float* s_sc = sm; float* s_sh = sm + C; float* s_mean = sm + 2 * C; float* s_inv = sm + 3 * C;
+  float* s_part = sm + 8 * C;
+  const int z = blockIdx.z;
+  bn_prepare(a.bn, z, s_sc, s_sh, s_mean, s_inv, false);
+  const bool two = (KIND == ADD_RELU && a.r_bn);
+  if (two) bn_prepare(a.bn2, z, s_sc + 4 * C, s_sh + 4 * C, s_mean + 4 * C, s_inv + 4 * C, false);
+  __syncthreads();
+  Lanes L(C);
+  const int c = L.cg * 8;
+  float sdz[8], sdx[8], sdx2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sdz[j] = 0.f; sdx[j] = 0.f; sdx2[j] = 0.f; }
+  if (L.active) {
+    BwdCtx X;
+    load_ctx<KIND>(a, X, s_sc, s_sh, s_mean, s_inv, c);
+    const int M = a.B * a.H * a.W;
+    for (int p = blockIdx.x * L.PL + L.pl; p < M; p += gridDim.x * L.PL) {
+      float dz[8], xh[8], xh2[8], side[8];
+      compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sdz[j] += dz[j];
+        sdx[j] += dz[j] * xh[j];
+        if (two) sdx2[j] += dz[j] * xh2[j];
+      }
+      if ((KIND == SIGMUL || (KIND == ADD_RELU && !a.r_bn)) && a.side)
+        store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
+    }
+  }
+  // block reduction over pixel lanes
+  const int PL = L.PL;
+  if (L.active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s_part[(L.pl * 3 + 0) * C + c + j] = sdz[j];
+      s_part[(L.pl * 3 + 1) * C + c + j] = sdx[j];
+      if (two) s_part[(L.pl * 3 + 2) * C + c + j] = sdx2[j];
+    }
+  }
+  __syncthreads();
+  const int rep = blockIdx.x % NREP;
+  for (int ch = threadIdx.x; ch < C; ch += blockDim.x) {
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+    for (int q = 0; q < PL; ++q) {
+      t0 += s_part[(q * 3 + 0) * C + ch];
+      t1 += s_part[(q * 3 + 1) * C + ch];
+      if (two) t2 += s_part[(q * 3 + 2) * C + ch];
+    }
+    float* w = a.ws + ((int64_t)z * NREP + rep) * 2 * C;
+    atomicAdd(w + ch, t0);
+    atomicAdd(w + C + ch, t1);
+    if (two) {
+      float* w2 = a.ws2 + ((int64_t)z * NREP + rep) * 2 * C;
+      atomicAdd(w2 + ch, t0);
+      atomicAdd(w2 + C + ch, t2);
+    }
+  }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void tail_bwd_apply_kernel(TailArgs a) {
+  extern __shared__ float sm[];
+  const int C = a.C;
+  float* s_sc = sm; float* s_sh = sm + C; float* s_mean = sm + 2 * C; float* s_inv = sm + 3 * C;
+  // coefficient arrays: dy = A*dz + Bc*y + Cc  (BN1 at [8C..11C), BN2 at [11C..14C))
+  float* s_A = sm + 8 * C; float* s_B = sm + 9 * C; float* s_Cc = sm + 10 * C;
+  const int z = blockIdx.z;
+  const bool two = (KIND == ADD_RELU && a.r_bn);
+  bn_prepare(a.bn, z, s_sc, s_sh, s_mean, s_inv, false);
+  if (two) bn_prepare(a.bn2, z, s_sc + 4 * C, s_sh + 4 * C, s_mean + 4 * C, s_inv + 4 * C, false);
+  __syncthreads();
+  const float inv_n = 1.f / (float)a.bn.count;
+  for (int ch = threadIdx.x; ch < C; ch += blockDim.x) {
+    for (int k = 0; k < (two ? 2 : 1); ++k) {
+      const float* w = (k == 0 ? a.ws : a.ws2) + (int64_t)z * NREP * 2 * C;
+      float sdz = 0.f, sdx = 0.f;
+#pragma unroll
+      for (int r = 0; r < NREP; ++r) { sdz += w[r * 2 * C + ch]; sdx += w[r * 2 * C + C + ch]; }
+      const float g = (k == 0 ? a.bn.gamma[a.bn.pstride * z + ch] : a.bn2.gamma[a.bn2.pstride * z + ch]);
+      const float inv = s_inv[4 * C * k + ch], mu = s_mean[4 * C * k + ch];
+      const float mdz = sdz * inv_n, mdx = sdx * inv_n;
+      s_A[3 * C * k + ch] = g * inv;
+      s_B[3 * C * k + ch] = -g * inv * inv * mdx;
+      s_Cc[3 * C * k + ch] = g * inv * (mu * inv * mdx - mdz);
+      if (blockIdx.x == 0) {
+        float* dg = (k == 0 ? a.dgamma : a.dgamma2);
+        float* db = (k == 0 ? a.dbeta : a.dbeta2);
+        if (dg) dg[a.pgs * z + ch] = sdx;
+        if (db) db[a.pgs * z + ch] = sdz;
+      }
+    }
+  }
+  __syncthreads();
+  Lanes L(C);
+  if (!L.active) return;
+  const int c = L.cg * 8;
+  BwdCtx X;
+  load_ctx<KIND>(a, X, s_sc, s_sh, s_mean, s_inv, c);
+  float A1[8], B1[8], C1[8], A2[8], B2[8], C2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    A1[j] = s_A[c + j]; B1[j] = s_B[c + j]; C1[j] = s_Cc[c + j];
+    if (two) { A2[j] = s_A[3 * C + c + j]; B2[j] = s_B[3 * C + c + j]; C2[j] = s_Cc[3 * C + c + j]; }
+  }
+  const int M = a.B * a.H * a.W;
+  const bf16_t* yz = a.y + a.ygs * z;
+  for (int p = blockIdx.x * L.PL + L.pl; p < M; p += gridDim.x * L.PL) {
+    float dz[8], xh[8], xh2[8], side[8];
+    compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
+    float y[8], o[8];
+    load8(yz + (int64_t)p * a.ldy + c, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = A1[j] * dz[j] + B1[j] * y[j] + C1[j];
+    store8(a.dy + a.dgs * z + (int64_t)p * a.ldd + c, o);
+    if (two) {
+      float y2[8];
+      load8(a.r + a.rgs * z + (int64_t)p * a.ldr + c, y2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = A2[j] * dz[j] + B2[j] * y2[j] + C2[j];
+      store8(a.dy2 + a.d2gs * z + (int64_t)p * a.ldd2 + c, o);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st) {
+  size_t lds = (size_t)4 * a.C * sizeof(float);
+  dim3 grid(blocks, 1, G);
+  switch (kind) {
+#define K(X) case X: hipLaunchKernelGGL(tail_fwd_kernel<X>, grid, dim3(256), lds, st, a); break;
+    K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(ADD_RELU) K(POOL_RELU)
+#undef K
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st) {
+  const int CG = a.C / 8;
+  const int PL = 256 / CG;
+  size_t lds_r = (size_t)(8 * a.C + 3 * PL * a.C) * sizeof(float);
+  size_t lds_a = (size_t)(14 * a.C) * sizeof(float);
+  dim3 grid(blocks, 1, G);
+  switch (kind) {
+#define K(X)                                                                                 \
+  case X:                                                                                    \
+    hipLaunchKernelGGL(tail_bwd_reduce_kernel<X>, grid, dim3(256), lds_r, st, a);            \
+    hipLaunchKernelGGL(tail_bwd_apply_kernel<X>, grid, dim3(256), lds_a, st, a);             \
+    break;
+    K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(ADD_RELU) K(POOL_RELU)
+#undef K
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace mda

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <algorithm>
 
 #define DEV __device__ __forceinline__
 

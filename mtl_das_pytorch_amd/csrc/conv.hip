@@ -1,0 +1,363 @@
+// Implicit-GEMM convolutions on gfx950 MFMA (v_mfma_f32_16x16x32_bf16), NHWC bf16, fp32 accumulate.
+//
+// Replaces the reference's implicit cuDNN convolutions (every nn.Conv2d of model/modelA_MTL.py,
+// model/modelB_singleTask.py and the Inception blocks of model/modelC_multiClassifier.py) and their
+// autograd backward (convolution_backward: grad_input + grad_weight).
+//
+//  conv_igemm<FWD>   out[m, n] = sum_k W[n, k] * im2col(x)[k, m]      m = (b, oh, ow), n = cout,
+//                    k = (kh, kw, cin).  Epilogue: + bias, bf16 store, per-channel BN partial sums
+//                    (sum y, sum y^2) into NREP replicas -- the training-mode BN reduction is fused
+//                    into the producing conv.
+//  conv_igemm<DGRAD> dx[m, n] = sum_k Wt[n, k] * gather(dy)[k, m]      m = (b, ih, iw), n = cin,
+//                    k = (kh, kw, cout); strided convs gather only the taps with (ih+p-kh) % s == 0.
+//                    fp32 output (gradient buffers are fp32 and written exactly once).
+//  conv_wgrad        dW[n, k] = sum_m dy[m, n] * im2col(x)[m, k]; both operands are staged in LDS
+//                    pixel-major (natural NHWC rows, 16-B writes) and read as MFMA operands with the
+//                    gfx950 transpose read ds_read_b64_tr_b16.  Split over m; fp32 partial slabs are
+//                    summed (deterministically) by wgrad_finalize into the flat fp32 gradient buffer in
+//                    the reference's NCHW weight layout.
+//
+// MFMA orientation: the weight tile is the A operand (rows = output channels) and the im2col tile
+// the B operand (cols = pixels), so each lane's accumulator holds 4 consecutive channels of one
+// pixel -> 8-byte (bf16) / 16-byte (fp32) NHWC stores, 16 lanes covering 16 consecutive pixels.
+//
+// The K dimension is walked in steps of 32 = four 8-channel groups; a per-block LDS table maps each
+// k-group to (segment, kh, kw, channel) so two-segment inputs (cat[F_shared, B_task]) need no concat.
+#include "kernels.h"
+
+namespace mda {
+
+
+
+DEV int encode_kg(int i, int Ktot, int Cs8, int KW, int C0) {
+  if (i * 8 >= Ktot) return 0;
+  int tap = i / Cs8, c = (i - tap * Cs8) * 8;
+  int kh = tap / KW, kw = tap - kh * KW;
+  int seg = c >= C0;
+  if (seg) c -= C0;
+  return c | (kw << 14) | (kh << 21) | (seg << 28) | (1 << 29);
+}
+
+template <int MODE, int WN, int WM, int WAVES_N, int WAVES_M>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
+  extern __shared__ int s_tab[];
+  constexpr int FN = WN / 16, FM = WM / 16;
+  constexpr int BN_T = WN * WAVES_N, BM_T = WM * WAVES_M;
+  const int z = blockIdx.z;
+  const int nkg = a.Kpad >> 3;
+  const int Ktot = a.KH * a.KW * a.Cs;
+  for (int i = threadIdx.x; i < nkg; i += 256) s_tab[i] = encode_kg(i, Ktot, a.Cs >> 3, a.KW, a.src.C0);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wn = wid % WAVES_N, wm = wid / WAVES_N;
+  const int n_base = blockIdx.y * BN_T + wn * WN;
+  const int m_base = blockIdx.x * BM_T + wm * WM;
+  const int HWo = a.Ho * a.Wo;
+  const int M = a.B * HWo;
+  const int l16 = lane & 15, kgl = lane >> 4;
+
+  int pb[FM], py[FM], px[FM];
+  bool pv[FM];
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    int m = m_base + f * 16 + l16;
+    pv[f] = m < M;
+    int mm = pv[f] ? m : 0;
+    int b = mm / HWo, r = mm - b * HWo;
+    int oh = r / a.Wo, ow = r - oh * a.Wo;
+    pb[f] = b;
+    if (MODE == MODE_FWD) { py[f] = oh * a.sh - a.ph; px[f] = ow * a.sw - a.pw; }
+    else { py[f] = oh + a.ph; px[f] = ow + a.pw; }
+  }
+  const bf16_t* base0 = a.src.p[0] + a.src.gs[0] * z;
+  const bf16_t* base1 = a.src.p[1] ? a.src.p[1] + a.src.gs[1] * z : base0;
+  const int ld0 = a.src.ld[0], ld1 = a.src.ld[1];
+  const bf16_t* wz = a.w + a.wgs * z;
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int f = 0; f < FM; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int nks = a.Kpad >> 5;
+  for (int ks = 0; ks < nks; ++ks) {
+    const int e = s_tab[ks * 4 + kgl];
+    const bool valid = (e >> 29) & 1;
+    const int seg = (e >> 28) & 1;
+    const int kh = (e >> 21) & 127, kw = (e >> 14) & 127, c = e & 16383;
+    const bf16_t* sb = seg ? base1 : base0;
+    const int sld = seg ? ld1 : ld0;
+    bf16x8 bfr[FM];
+#pragma unroll
+    for (int f = 0; f < FM; ++f) {
+      int ih, iw;
+      bool ok;
+      if (MODE == MODE_FWD) {
+        ih = py[f] + kh; iw = px[f] + kw;
+        ok = valid && pv[f] && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+      } else {
+        int nh = py[f] - kh, nw = px[f] - kw;
+        ok = valid && pv[f] && nh >= 0 && nw >= 0;
+        if (a.sh == 2) { ok = ok && !(nh & 1); ih = nh >> 1; } else if (a.sh == 1) { ih = nh; } else { ok = ok && (nh % a.sh == 0); ih = nh / a.sh; }
+        if (a.sw == 2) { ok = ok && !(nw & 1); iw = nw >> 1; } else if (a.sw == 1) { iw = nw; } else { ok = ok && (nw % a.sw == 0); iw = nw / a.sw; }
+        ok = ok && ih < a.Hs && iw < a.Ws;
+      }
+      bfr[f] = ok ? *reinterpret_cast<const bf16x8*>(sb + ((int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw) * sld + c) : zero8;
+    }
+    bf16x8 afr[FN];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      int n = n_base + i * 16 + l16;
+      afr[i] = n < a.Npad ? *reinterpret_cast<const bf16x8*>(wz + (int64_t)n * a.Kpad + ks * 32 + kgl * 8) : zero8;
+    }
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int f = 0; f < FM; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], bfr[f], acc[i][f], 0, 0, 0);
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const int rep = blockIdx.x % NREP;
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int n0 = n_base + i * 16 + 4 * kgl;
+    const bool nok = n0 < a.N;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (MODE == MODE_FWD && a.bias && nok) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[r] = a.bias[a.bgs * z + n0 + r];
+    }
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < FM; ++f) {
+      const int m = m_base + f * 16 + l16;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] + bias[r];
+      if (nok && pv[f]) {
+        if (MODE == MODE_FWD) {
+          bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
+          uint2 w;
+          w.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          w.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *reinterpret_cast<uint2*>(o) = w;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { s[r] += v[r]; ss[r] += v[r] * v[r]; }
+        } else {
+          float* o = reinterpret_cast<float*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
+          *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+    if (MODE == MODE_FWD && a.stats) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s[r] += __shfl_xor(s[r], o, 64);
+          ss[r] += __shfl_xor(ss[r], o, 64);
+        }
+      }
+      if (l16 == 0 && nok) {
+        float* st = a.stats + ((int64_t)z * NREP + rep) * 2 * a.N;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          atomicAdd(st + n0 + r, s[r]);
+          atomicAdd(st + a.N + n0 + r, ss[r]);
+        }
+      }
+    }
+  }
+}
+
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
+  // Block of rows r..r+7 (two 4-row transposed reads), 16 columns col0..col0+15.
+  // Lane 4q+p of each 16-lane group supplies &row[q][col0 + 4p]; lane i receives column col0+i.
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const bf16_t* a0 = lds_row0 + q * ld_elems + col0 + 4 * p;
+  const bf16_t* a1 = a0 + 4 * ld_elems;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a1));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// Block: 256 threads, output tile TN (rows = cout) x TK (cols = k), MCH pixels staged per iteration.
+template <int TN, int TK, int MCH>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+  constexpr int PAD = 8;  // rows stay 16-byte aligned (ds_write_b128 staging, 8-byte tr-read addresses)
+  constexpr int LDY = TN + PAD, LDX = TK + PAD;
+  __shared__ __attribute__((aligned(16))) bf16_t s_dy[MCH * LDY];
+  __shared__ __attribute__((aligned(16))) bf16_t s_x[MCH * LDX];
+  __shared__ int s_tab[TK / 8];
+  constexpr int FN = TN / 16, FK = TK / 16, NFR = FN * FK;
+  constexpr int FPW = (NFR + 3) / 4;  // fragments per wave
+
+  const int z = blockIdx.z;
+  const int split = blockIdx.y;
+  const int ntk = a.Kpad / TK;
+  const int tn = blockIdx.x / ntk, tk = blockIdx.x - tn * ntk;
+  const int n0 = tn * TN, k0 = tk * TK;
+  const int Ktot = a.KH * a.KW * a.Cs;
+  if (threadIdx.x < TK / 8) s_tab[threadIdx.x] = encode_kg(k0 / 8 + threadIdx.x, Ktot, a.Cs >> 3, a.KW, a.src.C0);
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int HWo = a.Ho * a.Wo;
+  const int M = a.B * HWo;
+  const int mbeg = split * a.m_per_split;
+  const int mend = min(M, mbeg + a.m_per_split);
+  const bf16_t* base0 = a.src.p[0] + a.src.gs[0] * z;
+  const bf16_t* base1 = a.src.p[1] ? a.src.p[1] + a.src.gs[1] * z : base0;
+  const bf16_t* dyz = a.dy + a.dgs * z;
+
+  f32x4 acc[FPW];
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  for (int mc = mbeg; mc < mend; mc += MCH) {
+    // stage dy tile [MCH][TN]
+    constexpr int VY = MCH * (TN / 8);
+    for (int v = threadIdx.x; v < VY; v += 256) {
+      int p = v / (TN / 8), cg = v - p * (TN / 8);
+      int m = mc + p, n = n0 + cg * 8;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (m < mend && n < a.Co) val = *reinterpret_cast<const uint4*>(dyz + (int64_t)m * a.ldd + n);
+      *reinterpret_cast<uint4*>(&s_dy[p * LDY + cg * 8]) = val;
+    }
+    // stage im2col tile [MCH][TK]
+    constexpr int VX = MCH * (TK / 8);
+    for (int v = threadIdx.x; v < VX; v += 256) {
+      int p = v / (TK / 8), g = v - p * (TK / 8);
+      int m = mc + p;
+      int e = s_tab[g];
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (m < mend && ((e >> 29) & 1)) {
+        int b = m / HWo, r = m - b * HWo;
+        int oh = r / a.Wo, ow = r - oh * a.Wo;
+        int ih = oh * a.sh - a.ph + ((e >> 21) & 127);
+        int iw = ow * a.sw - a.pw + ((e >> 14) & 127);
+        if (ih >= 0 && ih < a.Hi && iw >= 0 && iw < a.Wi) {
+          int seg = (e >> 28) & 1;
+          const bf16_t* sb = seg ? base1 : base0;
+          val = *reinterpret_cast<const uint4*>(sb + ((int64_t)(b * a.Hi + ih) * a.Wi + iw) * a.src.ld[seg] + (e & 16383));
+        }
+      }
+      *reinterpret_cast<uint4*>(&s_x[p * LDX + g * 8]) = val;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < MCH / 32; ++kk) {
+      const int prow = kk * 32 + 8 * (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < FPW; ++j) {
+        const int fr = wid + 4 * j;
+        if (fr < NFR) {
+          const int fi = fr / FK, fk = fr - fi * FK;
+          bf16x8 av = tr_read8(&s_dy[prow * LDY], LDY, fi * 16, lane);
+          bf16x8 bv = tr_read8(&s_x[prow * LDX], LDX, fk * 16, lane);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* slab = a.slab + (((int64_t)z * a.splits + split) * a.Npad) * a.Kpad;
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) {
+    const int fr = wid + 4 * j;
+    if (fr < NFR) {
+      const int fi = fr / FK, fk = fr - fi * FK;
+      const int row = n0 + fi * 16 + 4 * (lane >> 4);
+      const int col = k0 + fk * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (row + r < a.Npad) slab[(int64_t)(row + r) * a.Kpad + col] = acc[j][r];
+    }
+  }
+}
+
+
+__global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale) {
+  int lo = 0, hi = nd - 1;  // last descriptor with block0 <= blockIdx.x
+  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (descs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
+  const WgFinDesc& D = descs[lo];
+  int64_t e = ((int64_t)blockIdx.x - D.block0) * 256 + threadIdx.x;
+  if (e >= D.elems) return;
+  const int64_t per = (int64_t)D.Co * D.Ci * D.KH * D.KW;
+  int g = (int)(e / per);
+  int64_t r = e - g * per;
+  int kw = r % D.KW; r /= D.KW;
+  int kh = r % D.KH; r /= D.KH;
+  int ci = r % D.Ci;
+  int co = (int)(r / D.Ci);
+  int k = (kh * D.KW + kw) * D.Cs + ci;
+  const float* s = D.slab + (((int64_t)g * D.splits) * D.Npad + co) * D.Kpad + k;
+  const int64_t sstride = (int64_t)D.Npad * D.Kpad;
+  float acc = 0.f;
+  for (int sp = 0; sp < D.splits; ++sp) acc += s[sp * sstride];
+  D.grad[g * D.ggs + (((int64_t)co * D.Ci + ci) * D.KH + kh) * D.KW + kw] = acc * scale;
+}
+
+// ------------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------------
+template <int MODE>
+static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
+  const int M = a.B * a.Ho * a.Wo;
+  const size_t lds = (size_t)(a.Kpad / 8) * sizeof(int);
+#define LAUNCH_CFG(WN, WM, WAN, WAM)                                                               \
+  {                                                                                                \
+    dim3 grid((M + WM * WAM - 1) / (WM * WAM), (a.N + WN * WAN - 1) / (WN * WAN), G);               \
+    hipLaunchKernelGGL((conv_igemm_kernel<MODE, WN, WM, WAN, WAM>), grid, dim3(256), lds, st, a);  \
+    break;                                                                                         \
+  }
+  switch (cfg) {
+    case 0: LAUNCH_CFG(16, 64, 1, 4)   // N <= 16
+    case 1: LAUNCH_CFG(32, 32, 1, 4)   // N <= 32
+    case 2: LAUNCH_CFG(32, 32, 2, 2)   // N <= 64
+    case 3: LAUNCH_CFG(64, 32, 2, 2)   // N <= 128 and wide layers
+    case 4: LAUNCH_CFG(32, 16, 2, 2)   // small-M layers: more blocks
+    default: return -1;
+  }
+#undef LAUNCH_CFG
+  return (int)hipGetLastError();
+}
+
+int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
+  return mode == MODE_FWD ? launch_conv_cfg<MODE_FWD>(a, G, cfg, st) : launch_conv_cfg<MODE_DGRAD>(a, G, cfg, st);
+}
+
+int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st) {
+  const int ntn = (a.Npad + 15) / 16;
+#define LAUNCH_WG(TN, TK, MCH)                                                                      \
+  {                                                                                                 \
+    dim3 grid(((a.Npad + TN - 1) / TN) * (a.Kpad / TK), a.splits, G);                               \
+    hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, a);                \
+    break;                                                                                          \
+  }
+  (void)ntn;
+  switch (cfg) {
+    case 0: LAUNCH_WG(16, 32, 128)
+    case 1: LAUNCH_WG(32, 32, 128)
+    case 2: LAUNCH_WG(32, 64, 64)
+    case 3: LAUNCH_WG(64, 64, 64)
+    default: return -1;
+  }
+#undef LAUNCH_WG
+  return (int)hipGetLastError();
+}
+
+int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, d_descs, nd, scale);
+  return (int)hipGetLastError();
+}
+
+}  // namespace mda

@@ -1,0 +1,201 @@
+// Fused task heads + losses + on-device metrics.
+//
+// mtl_head: one launch for all tasks of Models A/B (reference modelA_MTL.py:165-172 and the loss /
+//   metric code of utils.py:272-292,359-380):  GAP over HxW -> AvgPool1d over groups of C/ncls channels
+//   -> log_softmax -> NLL (mean over batch) weighted per task; writes log-probabilities, the gradient
+//   w.r.t. the task features (broadcast back through the pools) and accumulates loss sums, correct
+//   counts, |pred - label| (distance MAE in metres) and the confusion matrix with atomics, so the hot
+//   loop never synchronises with the host (the reference does 4 .item() syncs per batch).
+//
+// cls_head (+ cls_wgrad): Model C's GAP -> Dropout(0.5) -> Linear(2048, 32) -> CrossEntropy
+//   (modelC_multiClassifier.py:146-152, utils.py:746-771) with the joint label decoded on device into
+//   (distance, event) = (j % 16, j / 16) for the metrics (replaces the per-sample Python loop).
+#include "kernels.h"
+
+namespace mda {
+
+
+__global__ __launch_bounds__(256) void mtl_head_kernel(HeadArgs a) {
+  __shared__ float s_gap[4][256];  // up to 4 tasks x 256 channels
+  __shared__ float s_part[256];
+  __shared__ float s_logit[16], s_prob[16];
+  const int b = blockIdx.x;
+  const bool valid = a.nvalid == nullptr || b < *a.nvalid;
+  for (int t = 0; t < a.T; ++t) {
+    const bf16_t* f = a.feat + a.fgs * t + (int64_t)b * a.HW * a.ldf;
+    // GAP: thread -> (channel, pixel-lane)
+    const int lanes = 256 / a.C;  // C in {.., 64, 128, 256}
+    const int c = threadIdx.x % a.C, pl = threadIdx.x / a.C;
+    float s = 0.f;
+    if (pl < lanes)
+      for (int p = pl; p < a.HW; p += lanes) s += bf2f(f[(int64_t)p * a.ldf + c]);
+    s_part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x < a.C) {
+      float acc = 0.f;
+      for (int q = 0; q < lanes; ++q) acc += s_part[q * a.C + threadIdx.x];
+      s_gap[t][threadIdx.x] = acc / (float)a.HW;
+    }
+    __syncthreads();
+    const int K = a.ncls[t], gsz = a.C / K;
+    if (threadIdx.x < K) {
+      float acc = 0.f;
+      for (int q = 0; q < gsz; ++q) acc += s_gap[t][threadIdx.x * gsz + q];
+      s_logit[threadIdx.x] = acc / (float)gsz;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float mx = -INFINITY;
+      int am = 0;
+      for (int k = 0; k < K; ++k) if (s_logit[k] > mx) { mx = s_logit[k]; am = k; }
+      float se = 0.f;
+      for (int k = 0; k < K; ++k) se += __expf(s_logit[k] - mx);
+      const float lse = mx + __logf(se);
+      const int lab = (int)a.labels[(int64_t)b * a.lab_stride + a.lab_off + t];
+      for (int k = 0; k < K; ++k) {
+        float lp = s_logit[k] - lse;
+        a.logp[((int64_t)t * a.B + b) * 16 + k] = lp;
+        s_prob[k] = __expf(lp);
+      }
+      const float loss = lse - s_logit[lab];
+      float* mt = a.metrics + t * 4;
+      if (valid) {
+        atomicAdd(mt + 0, loss);
+        atomicAdd(mt + 1, am == lab ? 1.f : 0.f);
+        atomicAdd(mt + 2, 1.f);
+        atomicAdd(mt + 3, fabsf((float)(am - lab)));
+        atomicAdd(a.confusion + (t * 16 + lab) * 16 + am, 1);
+      }
+      s_prob[lab] -= 1.f;  // softmax - onehot
+    }
+    __syncthreads();
+    if (a.dfeat) {
+      // d loss_t / d feat[p][c] = w_t * (p_j - y_j) / B / gsz / HW for channel c in group j
+      float* d = a.dfeat + a.dgs * t + (int64_t)b * a.HW * a.C;
+      const float scale = a.w[t] / ((float)a.B * gsz * a.HW);
+      const int n = a.HW * a.C;
+      for (int i = threadIdx.x; i < n; i += 256) {
+        const int ch = i % a.C;
+        d[i] = s_prob[ch / gsz] * scale;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+int launch_mtl_head(const HeadArgs& a, hipStream_t st) {
+  if (a.C > 256 || 256 % a.C) return -2;
+  hipLaunchKernelGGL(mtl_head_kernel, dim3(a.B), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Model C classifier head
+// ------------------------------------------------------------------------------------------------
+DEV uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  // a few rounds of a counter-based mixer (splitmix/murmur finaliser style)
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
+  h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
+  return h;
+}
+
+
+__global__ __launch_bounds__(256) void cls_head_kernel(ClsArgs a) {
+  extern __shared__ float sm[];
+  float* s_feat = sm;            // [C]
+  float* s_mask = sm + a.C;      // [C]
+  __shared__ float s_logit[64];
+  const int b = blockIdx.x;
+  const uint32_t seed = a.seed ? (uint32_t)(*a.seed) : 0u;
+  const float keep_scale = a.p_drop > 0.f ? 1.f / (1.f - a.p_drop) : 1.f;
+  for (int c = threadIdx.x; c < a.C; c += 256) {
+    float s = 0.f;
+    for (int p = 0; p < a.HW; ++p) s += bf2f(a.x[((int64_t)b * a.HW + p) * a.ldx + c]);
+    s /= (float)a.HW;
+    float m = 1.f;
+    if (a.p_drop > 0.f) {
+      float u = (hash3(seed, (uint32_t)b, (uint32_t)c) >> 8) * (1.f / 16777216.f);
+      m = u >= a.p_drop ? keep_scale : 0.f;
+    }
+    s_mask[c] = m;
+    s_feat[c] = s * m;
+    a.feat[(int64_t)b * a.C + c] = s * m;
+  }
+  __syncthreads();
+  // logits: one wave per output class group
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int n = wid; n < a.N; n += 4) {
+    float acc = 0.f;
+    for (int c = lane; c < a.C; c += 64) acc += a.W[(int64_t)n * a.C + c] * s_feat[c];
+    acc = wave_sum(acc);
+    if (lane == 0) s_logit[n] = acc + a.bias[n];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float mx = -INFINITY;
+    int am = 0;
+    for (int n = 0; n < a.N; ++n) if (s_logit[n] > mx) { mx = s_logit[n]; am = n; }
+    float se = 0.f;
+    for (int n = 0; n < a.N; ++n) se += __expf(s_logit[n] - mx);
+    const float lse = mx + __logf(se);
+    const int lab = (int)a.labels[b];
+    for (int n = 0; n < a.N; ++n) a.logits[(int64_t)b * a.N + n] = s_logit[n];
+    const float loss = lse - s_logit[lab];
+    const int pd = am % 16, pe = am / 16, ld_ = lab % 16, le = lab / 16;
+    const bool valid = a.nvalid == nullptr || b < *a.nvalid;
+    if (valid) {
+    atomicAdd(a.metrics + 0, loss);
+    atomicAdd(a.metrics + 1, am == lab ? 1.f : 0.f);
+    atomicAdd(a.metrics + 2, 1.f);
+    atomicAdd(a.metrics + 4 + 1, pd == ld_ ? 1.f : 0.f);
+    atomicAdd(a.metrics + 4 + 2, 1.f);
+    atomicAdd(a.metrics + 4 + 3, fabsf((float)(pd - ld_)));
+    atomicAdd(a.metrics + 8 + 1, pe == le ? 1.f : 0.f);
+    atomicAdd(a.metrics + 8 + 2, 1.f);
+    atomicAdd(a.confusion + ld_ * 16 + pd, 1);
+    atomicAdd(a.confusion + 256 + le * 16 + pe, 1);
+    }
+    if (a.dlogits) {
+      for (int n = 0; n < a.N; ++n)
+        a.dlogits[(int64_t)b * a.N + n] = (__expf(s_logit[n] - lse) - (n == lab ? 1.f : 0.f)) / (float)a.B;
+    }
+  }
+  if (!a.dx) return;
+  __syncthreads();
+  // dx[b][p][c] = (sum_n dlogits[n] W[n][c]) * mask[c] / HW
+  for (int c = threadIdx.x; c < a.C; c += 256) {
+    float acc = 0.f;
+    for (int n = 0; n < a.N; ++n) acc += a.dlogits[(int64_t)b * a.N + n] * a.W[(int64_t)n * a.C + c];
+    acc *= s_mask[c] / (float)a.HW;
+    for (int p = 0; p < a.HW; ++p) a.dx[((int64_t)b * a.HW + p) * a.C + c] = acc;
+  }
+}
+
+// dW[n][c] = sum_b dlogits[b][n] * feat[b][c];  db[n] = sum_b dlogits[b][n]; advances the dropout seed.
+__global__ __launch_bounds__(256) void cls_wgrad_kernel(ClsArgs a, int64_t* seed) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < (int64_t)a.N * a.C) {
+    const int n = (int)(i / a.C), c = (int)(i - (int64_t)n * a.C);
+    float acc = 0.f;
+    for (int b = 0; b < a.B; ++b) acc += a.dlogits[(int64_t)b * a.N + n] * a.feat[(int64_t)b * a.C + c];
+    a.dW[i] = acc;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < a.N) {
+    float acc = 0.f;
+    for (int b = 0; b < a.B; ++b) acc += a.dlogits[(int64_t)b * a.N + threadIdx.x];
+    a.db[threadIdx.x] = acc;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && seed) *seed += 1;
+}
+
+int launch_cls_head(const ClsArgs& a, int64_t* seed_mut, hipStream_t st) {
+  if (a.N > 64) return -2;
+  hipLaunchKernelGGL(cls_head_kernel, dim3(a.B), dim3(256), (size_t)2 * a.C * sizeof(float), st, a);
+  int rc = (int)hipGetLastError();
+  if (rc || !a.dx) return rc;
+  const int64_t n = (int64_t)a.N * a.C;
+  hipLaunchKernelGGL(cls_wgrad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, seed_mut);
+  return (int)hipGetLastError();
+}
+
+}  // namespace mda

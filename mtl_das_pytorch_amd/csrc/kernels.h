@@ -1,0 +1,141 @@
+// Kernel argument structs and host launch entry points of the mtl_das_pytorch_amd HIP library.
+// Every launcher enqueues on the given stream (PyTorch's current stream, so HIP-graph capture works)
+// and returns hipGetLastError() (negative = rejected arguments).
+#pragma once
+#include "common.h"
+
+namespace mda {
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+
+struct ConvArgs {
+  Src2 src;
+  const bf16_t* w;  // packed [Npad][Kpad] (+ z * wgs)
+  int64_t wgs;
+  const float* bias;  // FWD only, may be null
+  int64_t bgs;
+  void* out;  // FWD: bf16, DGRAD: fp32; [M][ldo] (+ z * ogs)
+  int64_t ogs;
+  int ldo;
+  float* stats;  // FWD: [G][NREP][2][N] (may be null)
+  int B, Hs, Ws, Ho, Wo;
+  int N, Npad, Cs;
+  int KH, KW, sh, sw, ph, pw;
+  int Kpad;
+};
+
+// ------------------------------------------------------------------------------------------------
+// Weight gradient
+// ------------------------------------------------------------------------------------------------
+struct WgradArgs {
+  Src2 src;          // forward input (bf16)
+  const bf16_t* dy;  // [M][ldd] (+ z * dgs)
+  int64_t dgs;
+  int ldd;
+  float* slab;       // [G][splits][Npad][Kpad]
+  int splits, m_per_split;
+  int B, Hi, Wi, Ho, Wo;
+  int Co, Npad, Cs;
+  int KH, KW, sh, sw, ph, pw;
+  int Kpad;
+};
+
+// Sums the split-M partial slabs of many convolutions and scatters them into the flat fp32 gradient
+// buffer in the reference weight layout [Cout][Cin][KH][KW] (deterministic, one launch per backward).
+struct WgFinDesc {
+  const float* slab;  // [G][splits][Npad][Kpad]
+  float* grad;        // NCHW weight grad of group 0
+  int64_t ggs;        // element stride between groups in the flat grad buffer
+  int G, splits, Npad, Kpad, Co, Ci, Cs, KH, KW;
+  int64_t elems;      // G * Co * Ci * KH * KW
+  int64_t block0;     // first block index of this descriptor
+};
+
+enum TailKind { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, SIGMUL = 3, ADD_RELU = 4, POOL_RELU = 5 };
+
+struct TailArgs {
+  const bf16_t* y; int64_t ygs; int ldy;
+  BNArgs bn;
+  const bf16_t* r; int64_t rgs; int ldr;  // SIGMUL: multiplier; ADD_RELU: residual (raw x or y2)
+  BNArgs bn2; int r_bn;
+  bf16_t* out; int64_t ogs; int ldo;
+  int B, H, W, C;
+  // backward only
+  GradSrcs g;                       // upstream fp32 gradient(s) on the tail's output grid
+  float* ws; float* ws2;            // [G][NREP][2][C]
+  float* side; int64_t sgs; int lds;
+  bf16_t* dy; int64_t dgs; int ldd;
+  bf16_t* dy2; int64_t d2gs; int ldd2;
+  float* dgamma; float* dbeta; float* dgamma2; float* dbeta2; int64_t pgs;
+};
+
+struct HeadArgs {
+  const bf16_t* feat; int64_t fgs; int ldf;  // per task [B*HW][C] (+ t * fgs)
+  const int64_t* labels; int lab_stride, lab_off;  // label of (b, t) = labels[b*lab_stride + lab_off + t]
+  int T, B, HW, C;
+  int ncls[4];
+  float w[4];
+  float* logp;      // [T][B][16]
+  float* dfeat;     // [T][B*HW][C] fp32 (+ t * dgs), may be null (eval)
+  int64_t dgs;
+  float* metrics;   // [T][4]: loss_sum, correct, count, abs_err_sum
+  int* confusion;   // [T][16][16]
+  const int64_t* nvalid;  // samples b >= *nvalid are padding: no metrics, no gradient (may be null)
+};
+
+struct ClsArgs {
+  const bf16_t* x; int ldx;      // [B*HW][C] last feature map
+  const float* W; const float* bias;  // fc [N][C], [N]
+  const int64_t* labels;         // joint labels [B]
+  int B, HW, C, N;
+  float p_drop;                  // dropout probability (0 in eval)
+  const int64_t* seed;           // device counter (advanced by cls_wgrad each training step)
+  float* feat;                   // [B][C] post-dropout features (fp32)
+  float* logits;                 // [B][N]
+  float* dlogits;                // [B][N] (training)
+  float* dx;                     // [B*HW][C] fp32 grad (training), may be null
+  float* metrics;                // [3][4]: joint, distance, event -> loss, correct, count, abs_err
+  int* confusion;                // [2][16][16]: distance, event
+  float* dW; float* db;          // flat-grad slots (cls_wgrad)
+  const int64_t* nvalid;         // padding mask for metrics (may be null)
+};
+
+// ------------------------------------------------------------------------------------------------
+struct PoolArgs {
+  const bf16_t* x; int ldx;     // input [B*H*W][C] (bf16)
+  bf16_t* y; int ldy;           // output [B*Ho*Wo][C]
+  const float* g; int ldg;      // backward: grad of output (fp32)
+  float* dx; int lddx;          // backward: grad of input (fp32)
+  int B, H, W, C, Ho, Wo;
+};
+
+struct OptSeg {
+  int64_t off, n;
+  int kind;  // 0 = plain tensor, 1 = conv weight (write packed images)
+  bf16_t* wf;
+  bf16_t* wd;
+  int Co, Ci, KH, KW, Cs, Kpad_f, Kpad_d;
+  int64_t block0;
+};
+
+struct AdamArgs {
+  float* p; const float* g; float* m; float* v;
+  const float* lr; const float* step;  // device scalars (step = number of completed steps)
+  float b1, b2, eps, wd, grad_scale;
+  int update;  // 0: pack only
+};
+
+int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
+int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st);
+int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);
+int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);
+int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);
+int launch_mtl_head(const HeadArgs& a, hipStream_t st);
+int launch_cls_head(const ClsArgs& a, int64_t* seed_mut, hipStream_t st);
+int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
+                        int64_t* lab_out, int B, int Cin, int H, int W, hipStream_t st);
+int launch_pool3(int is_max, int backward, const PoolArgs& a, hipStream_t st);
+int launch_grad_sum(const GradSrcs& g, float* out, int ldo, int64_t M, int C, hipStream_t st);
+int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st);
+
+}  // namespace mda

@@ -1,0 +1,162 @@
+// Data movement and pooling kernels.
+//
+// gather_batch: the on-device replacement of the reference's host data path (DataLoader collate of
+//   loadmat'd arrays + pageable .cuda() copies, utils.py:264-266,351-353): picks the batch rows of an
+//   HBM-resident fp32 NCHW dataset by index, converts to bf16 NHWC with the channel dim zero-padded to
+//   8 (so the 1-channel stem runs on the generic MFMA implicit-GEMM path) and gathers the labels.
+// Inception pools (model C, torchvision semantics used by modelC_multiClassifier.py):
+//   maxpool 3x3/s2 (valid) and avgpool 3x3/s1/p1 (count_include_pad=True), forward and backward; the
+//   backward passes are written in gather form (each input pixel sums the windows that cover it and,
+//   for max, recomputes the first-max argmax), so they are deterministic and need no index tensors.
+#include "kernels.h"
+
+namespace mda {
+
+__global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restrict__ X, const int64_t* __restrict__ idx,
+                                                           const int64_t* __restrict__ lab, int lab_w,
+                                                           bf16_t* __restrict__ out, int64_t* __restrict__ lab_out,
+                                                           int B, int Cin, int H, int W) {
+  const int64_t M = (int64_t)B * H * W;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < M; p += (int64_t)gridDim.x * 256) {
+    const int b = (int)(p / (H * W));
+    const int r = (int)(p - (int64_t)b * H * W);
+    const int64_t src = idx[b];
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = c < Cin ? X[(src * Cin + c) * (int64_t)H * W + r] : 0.f;
+    store8(out + p * 8, v);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < B * lab_w) {
+    const int b = threadIdx.x / lab_w, k = threadIdx.x - b * lab_w;
+    lab_out[threadIdx.x] = lab[idx[b] * lab_w + k];
+  }
+}
+
+int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
+                        int64_t* lab_out, int B, int Cin, int H, int W, hipStream_t st) {
+  if (Cin > 8 || B * lab_w > 256) return -2;
+  const int64_t M = (int64_t)B * H * W;
+  int blocks = (int)std::min<int64_t>((M + 255) / 256, 2048);
+  hipLaunchKernelGGL(gather_batch_kernel, dim3(blocks), dim3(256), 0, st, X, idx, lab, lab_w, out, lab_out, B, Cin, H, W);
+  return (int)hipGetLastError();
+}
+
+
+template <int MAX>
+__global__ __launch_bounds__(256) void pool3_fwd_kernel(PoolArgs a) {
+  const int CG = a.C >> 3;
+  const int64_t n = (int64_t)a.B * a.Ho * a.Wo * CG;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int cg = (int)(i % CG);
+    const int64_t p = i / CG;
+    const int b = (int)(p / (a.Ho * a.Wo));
+    const int r = (int)(p - (int64_t)b * a.Ho * a.Wo);
+    const int oh = r / a.Wo, ow = r - oh * a.Wo;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = MAX ? -INFINITY : 0.f;
+    const int s = MAX ? 2 : 1, pd = MAX ? 0 : 1;
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = oh * s - pd + kh;
+      if (ih < 0 || ih >= a.H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = ow * s - pd + kw;
+        if (iw < 0 || iw >= a.W) continue;
+        float v[8];
+        load8(a.x + ((int64_t)(b * a.H + ih) * a.W + iw) * a.ldx + cg * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = MAX ? fmaxf(acc[j], v[j]) : acc[j] + v[j];
+      }
+    }
+    if (!MAX) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
+    }
+    store8(a.y + p * a.ldy + cg * 8, acc);
+  }
+}
+
+template <int MAX>
+__global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {
+  const int CG = a.C >> 3;
+  const int64_t n = (int64_t)a.B * a.H * a.W * CG;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int cg = (int)(i % CG);
+    const int64_t p = i / CG;
+    const int b = (int)(p / (a.H * a.W));
+    const int r = (int)(p - (int64_t)b * a.H * a.W);
+    const int ih = r / a.W, iw = r - ih * a.W;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    if (MAX) {
+      // windows (stride 2, no pad) covering ih: oh in [ceil((ih-2)/2), ih/2]
+      const int oh0 = max(0, (ih - 1) >> 1), oh1 = min(a.Ho - 1, ih >> 1);
+      const int ow0 = max(0, (iw - 1) >> 1), ow1 = min(a.Wo - 1, iw >> 1);
+      for (int oh = oh0; oh <= oh1; ++oh)
+        for (int ow = ow0; ow <= ow1; ++ow) {
+          if (ih < 2 * oh || ih > 2 * oh + 2 || iw < 2 * ow || iw > 2 * ow + 2) continue;
+          float mx[8];
+          int am[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { mx[j] = -INFINITY; am[j] = -1; }
+          for (int kh = 0; kh < 3; ++kh)
+            for (int kw = 0; kw < 3; ++kw) {
+              float v[8];
+              load8(a.x + ((int64_t)(b * a.H + 2 * oh + kh) * a.W + 2 * ow + kw) * a.ldx + cg * 8, v);
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                if (v[j] > mx[j]) { mx[j] = v[j]; am[j] = kh * 3 + kw; }
+            }
+          const int me = (ih - 2 * oh) * 3 + (iw - 2 * ow);
+          float g[8];
+          load8f(a.g + ((int64_t)(b * a.Ho + oh) * a.Wo + ow) * a.ldg + cg * 8, g);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) if (am[j] == me) acc[j] += g[j];
+        }
+    } else {
+      for (int oh = max(0, ih - 1); oh <= min(a.Ho - 1, ih + 1); ++oh)
+        for (int ow = max(0, iw - 1); ow <= min(a.Wo - 1, iw + 1); ++ow) {
+          float g[8];
+          load8f(a.g + ((int64_t)(b * a.Ho + oh) * a.Wo + ow) * a.ldg + cg * 8, g);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += g[j] * (1.f / 9.f);
+        }
+    }
+    store8f(a.dx + p * a.lddx + cg * 8, acc);
+  }
+}
+
+int launch_pool3(int is_max, int backward, const PoolArgs& a, hipStream_t st) {
+  const int64_t n = (int64_t)a.B * (backward ? a.H * a.W : a.Ho * a.Wo) * (a.C / 8);
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  if (!backward) {
+    if (is_max) hipLaunchKernelGGL(pool3_fwd_kernel<1>, dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(pool3_fwd_kernel<0>, dim3(blocks), dim3(256), 0, st, a);
+  } else {
+    if (is_max) hipLaunchKernelGGL(pool3_bwd_kernel<1>, dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(pool3_bwd_kernel<0>, dim3(blocks), dim3(256), 0, st, a);
+  }
+  return (int)hipGetLastError();
+}
+
+// sum of up to 6 fp32 gradient sources into one buffer (used where a consumer is not a fused tail)
+__global__ __launch_bounds__(256) void grad_sum_kernel(GradSrcs g, float* out, int ldo, int64_t M, int C) {
+  const int CG = C >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < M * CG; i += (int64_t)gridDim.x * 256) {
+    const int64_t p = i / CG;
+    const int c = (int)(i - p * CG) * 8;
+    float v[8];
+    gsum8(g, 0, p, c, v);
+    store8f(out + p * ldo + c, v);
+  }
+}
+
+int launch_grad_sum(const GradSrcs& g, float* out, int ldo, int64_t M, int C, hipStream_t st) {
+  const int64_t n = M * (C / 8);
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(grad_sum_kernel, dim3(blocks), dim3(256), 0, st, g, out, ldo, M, C);
+  return (int)hipGetLastError();
+}
+
+}  // namespace mda

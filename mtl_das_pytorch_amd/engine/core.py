@@ -1,0 +1,428 @@
+"""Engine core: flat parameter state, persistent device arena, and conv / BatchNorm layer handles.
+
+The engine does not use autograd.  A model is *lowered* once (for a fixed per-GPU batch size) into a
+static program of HIP kernel launches over preallocated NHWC buffers; forward and backward are both
+explicit, gradient buffers are written exactly once, and the whole train step is captured into a HIP
+graph (``engine/step.py``).  Parameters stay ordinary ``nn.Parameter`` objects of the reference module
+tree (so ``state_dict`` keys and checkpoints are unchanged) but their storage is re-pointed into one
+flat fp32 buffer, which is at the same time
+
+  * the DP all-reduce bucket (one RCCL call, ``parallel/``),
+  * the fused-Adam operand (one kernel, ``csrc/optim.hip``),
+  * grouped so that the per-task copies of a branch layer are adjacent with a constant stride: both task
+    branches of Model A run as ONE launch with ``grid.z = task`` (the shared input is read with group
+    stride 0).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ..ops.hip import lib, ptr
+
+NREP = 8  # must match csrc/common.h
+
+
+def pad_to(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+# ------------------------------------------------------------------------------------------------
+class FlatState:
+    """Flat fp32 parameter / gradient / Adam-moment buffers and flat BN running-stat buffers."""
+
+    def __init__(self, module: nn.Module, device, param_groups: Sequence[Sequence[nn.Parameter]] = (),
+                 bn_groups: Sequence[Sequence[nn.BatchNorm2d]] = ()):
+        self.module = module
+        self.device = torch.device(device)
+        order: List[nn.Parameter] = []
+        seen = set()
+        for grp in param_groups:
+            for p in grp:
+                if id(p) not in seen:
+                    order.append(p)
+                    seen.add(id(p))
+        for p in module.parameters():
+            if id(p) not in seen:
+                order.append(p)
+                seen.add(id(p))
+        self.offsets: Dict[int, int] = {}
+        off = 0
+        for p in order:
+            self.offsets[id(p)] = off
+            off += pad_to(p.numel(), 4)  # 16-byte aligned slots
+        self.numel = off
+        self.params = torch.zeros(off, device=self.device, dtype=torch.float32)
+        self.grads = torch.zeros_like(self.params)
+        self.exp_avg = torch.zeros_like(self.params)
+        self.exp_avg_sq = torch.zeros_like(self.params)
+        self.order = order
+        for p in order:
+            o = self.offsets[id(p)]
+            view = self.params[o:o + p.numel()].view_as(p)
+            view.copy_(p.data.to(self.device))
+            p.data = view
+        # BN buffers
+        bns: List[nn.BatchNorm2d] = []
+        seen = set()
+        for grp in bn_groups:
+            for m in grp:
+                if id(m) not in seen:
+                    bns.append(m)
+                    seen.add(id(m))
+        for m in module.modules():
+            if isinstance(m, nn.BatchNorm2d) and id(m) not in seen:
+                bns.append(m)
+                seen.add(id(m))
+        self.bn_offsets: Dict[int, int] = {}
+        off = 0
+        for m in bns:
+            self.bn_offsets[id(m)] = off
+            off += pad_to(m.num_features, 4)
+        self.bn_mean = torch.zeros(off, device=self.device)
+        self.bn_var = torch.ones(off, device=self.device)
+        self.bn_nbt = torch.zeros(len(bns), device=self.device, dtype=torch.int64)
+        self.bn_index = {id(m): i for i, m in enumerate(bns)}
+        self.bns = bns
+        for m in bns:
+            o, c = self.bn_offsets[id(m)], m.num_features
+            rm = self.bn_mean[o:o + c]
+            rv = self.bn_var[o:o + c]
+            nb = self.bn_nbt[self.bn_index[id(m)]:self.bn_index[id(m)] + 1].view(())
+            rm.copy_(m.running_mean.to(self.device))
+            rv.copy_(m.running_var.to(self.device))
+            nb.copy_(m.num_batches_tracked.to(self.device))
+            m.running_mean = rm
+            m.running_var = rv
+            m.num_batches_tracked = nb
+        # Adam device scalars: [lr, step]
+        self.lr = torch.zeros(1, device=self.device)
+        self.step = torch.zeros(1, device=self.device)
+
+    def off(self, p: nn.Parameter) -> int:
+        return self.offsets[id(p)]
+
+    def grad_of(self, p: nn.Parameter) -> torch.Tensor:
+        o = self.off(p)
+        return self.grads[o:o + p.numel()].view_as(p)
+
+    def group_stride(self, ps: Sequence[nn.Parameter]) -> int:
+        """Element stride between consecutive members of a layer group (0 for a single member)."""
+        if len(ps) == 1:
+            return 0
+        o = [self.off(p) for p in ps]
+        st = o[1] - o[0]
+        if any(o[i + 1] - o[i] != st for i in range(len(o) - 1)):
+            raise ValueError("parameter group is not evenly strided in the flat buffer")
+        return st
+
+    def bn_stride(self, ms: Sequence[nn.BatchNorm2d]) -> int:
+        if len(ms) == 1:
+            return 0
+        o = [self.bn_offsets[id(m)] for m in ms]
+        st = o[1] - o[0]
+        idx = [self.bn_index[id(m)] for m in ms]
+        if any(o[i + 1] - o[i] != st for i in range(len(o) - 1)) or any(idx[i + 1] - idx[i] != 1 for i in range(len(o) - 1)):
+            raise ValueError("BN group is not evenly strided")
+        # gamma/beta share the stride of the parameters; both must agree
+        return st
+
+    def sync_module_grads(self):
+        """Expose the flat gradients as ``p.grad`` (views, no copy) -- for inspection/tests."""
+        for p in self.order:
+            p.grad = self.grad_of(p)
+
+
+class Arena:
+    """Persistent device buffers for one lowered program.  ``zeroed`` buffers live in a single region
+    that is cleared with one memset at the start of every step (BN statistic accumulators, backward
+    workspaces, metric counters)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self._zero_specs: List[tuple] = []
+        self._zero_f32: Optional[torch.Tensor] = None
+        self._zero_i32: Optional[torch.Tensor] = None
+        self.views: List[torch.Tensor] = []
+
+    def empty(self, shape, dtype=torch.bfloat16) -> torch.Tensor:
+        return torch.empty(shape, device=self.device, dtype=dtype)
+
+    def zeros(self, shape, dtype=torch.bfloat16) -> torch.Tensor:
+        return torch.zeros(shape, device=self.device, dtype=dtype)
+
+    def zeroed(self, shape, dtype=torch.float32) -> "LazyView":
+        lv = LazyView(tuple(int(s) for s in shape), dtype)
+        self._zero_specs.append(lv)
+        return lv
+
+    def finalize(self):
+        nf = sum(pad_to(int(np.prod(v.shape)), 64) for v in self._zero_specs if v.dtype == torch.float32)
+        ni = sum(pad_to(int(np.prod(v.shape)), 64) for v in self._zero_specs if v.dtype == torch.int32)
+        self._zero_f32 = torch.zeros(max(nf, 64), device=self.device, dtype=torch.float32)
+        self._zero_i32 = torch.zeros(max(ni, 64), device=self.device, dtype=torch.int32)
+        of = oi = 0
+        for v in self._zero_specs:
+            n = int(np.prod(v.shape))
+            if v.dtype == torch.float32:
+                v.bind(self._zero_f32[of:of + n].view(v.shape))
+                of += pad_to(n, 64)
+            else:
+                v.bind(self._zero_i32[oi:oi + n].view(v.shape))
+                oi += pad_to(n, 64)
+
+    def clear(self):
+        self._zero_f32.zero_()
+        self._zero_i32.zero_()
+
+
+class LazyView:
+    """Placeholder for a slice of the arena's zeroed region (bound by ``Arena.finalize``)."""
+
+    def __init__(self, shape, dtype):
+        self.shape = shape
+        self.dtype = dtype
+        self.t: Optional[torch.Tensor] = None
+
+    def bind(self, t):
+        self.t = t
+
+    def __getattr__(self, k):
+        if k in ("shape", "dtype", "t", "bind"):
+            raise AttributeError(k)
+        return getattr(self.t, k)
+
+
+def P(x, off: int = 0) -> int:
+    """Device pointer of a tensor / LazyView (+ element offset)."""
+    if x is None:
+        return 0
+    t = x.t if isinstance(x, LazyView) else x
+    return t.data_ptr() + off * t.element_size()
+
+
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class Act:
+    """A bf16 NHWC activation (possibly a channel slice of a wider buffer, possibly per-group)."""
+    t: torch.Tensor          # backing buffer
+    off: int                 # element offset of channel 0 of group 0 / pixel 0
+    ld: int                  # pixel pitch (elements)
+    C: int                   # channels
+    gs: int = 0              # element stride between groups (0 = shared by all groups)
+    B: int = 0
+    H: int = 0
+    W: int = 0
+
+    @property
+    def p(self) -> int:
+        return P(self.t, self.off)
+
+    @property
+    def M(self) -> int:
+        return self.B * self.H * self.W
+
+    def slice(self, c0: int, C: int) -> "Act":
+        return Act(self.t, self.off + c0, self.ld, C, self.gs, self.B, self.H, self.W)
+
+
+def new_act(arena: Arena, G: int, B: int, H: int, W: int, C: int, dtype=torch.bfloat16, shared=False) -> Act:
+    t = arena.empty((G, B * H * W, C), dtype)
+    return Act(t, 0, C, C, 0 if (shared or G == 1) else B * H * W * C, B, H, W)
+
+
+def src_dict(a: Act, b: Optional[Act] = None) -> dict:
+    d = {"p0": a.p, "gs0": a.gs, "ld0": a.ld, "C0": a.C, "C1": 0}
+    if b is not None:
+        d.update({"p1": b.p, "gs1": b.gs, "ld1": b.ld, "C1": b.C})
+    return d
+
+
+def gsrc(x, off: int, gs: int, ld: int) -> tuple:
+    return (P(x, off), gs, ld)
+
+
+def grads_of(acts: Sequence[Act]) -> List[tuple]:
+    return [(a.p, a.gs, a.ld) for a in acts]
+
+
+# ------------------------------------------------------------------------------------------------
+class BNLayer:
+    """Training-mode BatchNorm state for one BN module or a group of identically shaped per-task BNs."""
+
+    def __init__(self, mods: Sequence[nn.BatchNorm2d], flat: FlatState, arena: Arena, count: int):
+        self.mods = list(mods)
+        self.G = len(mods)
+        m0 = mods[0]
+        self.C = m0.num_features
+        self.eps = float(m0.eps)
+        self.momentum = float(m0.momentum if m0.momentum is not None else 0.1)
+        self.count = count
+        self.flat = flat
+        self.pstride = flat.group_stride([m.weight for m in mods])
+        rs = flat.bn_stride(mods)
+        if self.G > 1 and rs != self.pstride:
+            raise ValueError("BN running-stat stride must equal the affine-parameter stride")
+        self.stats = arena.zeroed((self.G, NREP, 2, self.C))
+        self.ws = arena.zeroed((self.G, NREP, 2, self.C))
+        self.ws2 = None  # allocated on demand (second BN of a residual tail shares the dz)
+
+    def args(self, training: bool) -> dict:
+        f = self.flat
+        m0 = self.mods[0]
+        return {"stats": P(self.stats), "gamma": P(f.params, f.off(m0.weight)), "beta": P(f.params, f.off(m0.bias)),
+                "run_mean": P(f.bn_mean, f.bn_offsets[id(m0)]), "run_var": P(f.bn_var, f.bn_offsets[id(m0)]),
+                "nbt": P(f.bn_nbt, f.bn_index[id(m0)]), "pstride": self.pstride, "C": self.C, "count": self.count,
+                "eps": self.eps, "momentum": self.momentum, "training": 1 if training else 0}
+
+    def grad_ptrs(self) -> dict:
+        f = self.flat
+        m0 = self.mods[0]
+        return {"dgamma": P(f.grads, f.off(m0.weight)), "dbeta": P(f.grads, f.off(m0.bias)), "pgs": self.pstride}
+
+
+class ConvLayer:
+    """One convolution (or a group of identically shaped per-task convolutions) lowered to the MFMA
+    implicit-GEMM kernels.  Holds the packed bf16 weight images, the wgrad slab and the finalize /
+    Adam-pack descriptors."""
+
+    def __init__(self, mods: Sequence[nn.Conv2d], flat: FlatState, arena: Arena, B: int, Hi: int, Wi: int,
+                 cin_stored: Optional[int] = None):
+        self.mods = list(mods)
+        self.G = len(mods)
+        m = mods[0]
+        self.flat = flat
+        self.Co, self.Ci = m.out_channels, m.in_channels
+        self.KH, self.KW = m.kernel_size
+        self.sh, self.sw = m.stride
+        self.ph, self.pw = m.padding
+        if m.groups != 1 or m.dilation != (1, 1):
+            raise ValueError("grouped / dilated convolutions are not supported")
+        self.Cs = cin_stored if cin_stored is not None else self.Ci
+        if self.Cs % 8 or self.Co % 8:
+            raise ValueError(f"channels must be multiples of 8 (Cin stored {self.Cs}, Cout {self.Co})")
+        self.B, self.Hi, self.Wi = B, Hi, Wi
+        self.Ho = (Hi + 2 * self.ph - self.KH) // self.sh + 1
+        self.Wo = (Wi + 2 * self.pw - self.KW) // self.sw + 1
+        self.M_out = B * self.Ho * self.Wo
+        self.M_in = B * Hi * Wi
+        self.has_bias = m.bias is not None
+        self.wstride = flat.group_stride([x.weight for x in mods])
+        self.bstride = flat.group_stride([x.bias for x in mods]) if self.has_bias else 0
+        taps = self.KH * self.KW
+        self.Npad = pad_to(self.Co, 16)
+        self.Kpad = pad_to(taps * self.Cs, 32)
+        self.Npad_d = pad_to(self.Cs, 16)
+        self.Kpad_d = pad_to(taps * self.Co, 32)
+        self.wf = arena.zeros((self.G, self.Npad, self.Kpad))
+        self.wd = arena.zeros((self.G, self.Npad_d, self.Kpad_d))
+        # weight-gradient decomposition
+        self.Kpad_w = pad_to(taps * self.Cs, 64)
+        self.wcfg, TN, TK, MCH = self._wgrad_cfg()
+        tiles = math.ceil(self.Npad / TN) * (self.Kpad_w // TK) * self.G
+        max_splits = max(1, math.ceil(self.M_out / MCH))
+        splits = max(1, min(max_splits, math.ceil(512 / tiles)))
+        self.m_per_split = pad_to(math.ceil(self.M_out / splits), MCH)
+        self.splits = math.ceil(self.M_out / self.m_per_split)
+        self.slab = arena.empty((self.G, self.splits, self.Npad, self.Kpad_w), torch.float32)
+
+    def _wgrad_cfg(self):
+        if self.Co <= 16:
+            return 0, 16, 32, 128
+        if self.Co <= 32:
+            return (1, 32, 32, 128) if self.Kpad_w <= 64 else (2, 32, 64, 64)
+        return 3, 64, 64, 64
+
+    def fwd_cfg(self, N: int, M: int) -> int:
+        if N <= 16:
+            return 0
+        if N <= 32:
+            return 1
+        if N <= 64:
+            return 2 if M >= 64 * 256 else 4
+        return 3 if M >= 64 * 128 else 4
+
+    # ---- packed weight images / optimizer descriptors ------------------------------------------
+    def opt_segments(self) -> List[dict]:
+        segs = []
+        for g, m in enumerate(self.mods):
+            segs.append({"off": self.flat.off(m.weight), "n": m.weight.numel(), "kind": 1,
+                         "wf": P(self.wf, g * self.Npad * self.Kpad), "wd": P(self.wd, g * self.Npad_d * self.Kpad_d),
+                         "Co": self.Co, "Ci": self.Ci, "KH": self.KH, "KW": self.KW, "Cs": self.Cs,
+                         "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d})
+        return segs
+
+    def finalize_desc(self) -> dict:
+        m0 = self.mods[0]
+        return {"slab": P(self.slab), "grad": P(self.flat.grads, self.flat.off(m0.weight)), "ggs": self.wstride,
+                "G": self.G, "splits": self.splits, "Npad": self.Npad, "Kpad": self.Kpad_w, "Co": self.Co,
+                "Ci": self.Ci, "Cs": self.Cs, "KH": self.KH, "KW": self.KW,
+                "elems": self.G * m0.weight.numel()}
+
+    # ---- launches --------------------------------------------------------------------------------
+    def fwd_args(self, src: dict, out: Act, bn: Optional[BNLayer], training: bool) -> tuple:
+        f = self.flat
+        d = {"src": src, "w": P(self.wf), "wgs": self.Npad * self.Kpad if self.G > 1 else 0,
+             "bias": P(f.params, f.off(self.mods[0].bias)) if self.has_bias else 0, "bgs": self.bstride,
+             "out": out.p, "ogs": out.gs, "ldo": out.ld,
+             "stats": P(bn.stats) if (bn is not None and training) else 0,
+             "B": self.B, "Hs": self.Hi, "Ws": self.Wi, "Ho": self.Ho, "Wo": self.Wo, "N": self.Co, "Npad": self.Npad,
+             "Cs": self.Cs, "KH": self.KH, "KW": self.KW, "sh": self.sh, "sw": self.sw, "ph": self.ph, "pw": self.pw,
+             "Kpad": self.Kpad}
+        return (0, self.fwd_cfg(self.Co, self.M_out), self.G, d)
+
+    def dgrad_args(self, dy: Act, dx_out: Act) -> tuple:
+        d = {"src": src_dict(dy), "w": P(self.wd), "wgs": self.Npad_d * self.Kpad_d if self.G > 1 else 0,
+             "out": dx_out.p, "ogs": dx_out.gs, "ldo": dx_out.ld,
+             "B": self.B, "Hs": self.Ho, "Ws": self.Wo, "Ho": self.Hi, "Wo": self.Wi, "N": self.Cs, "Npad": self.Npad_d,
+             "Cs": self.Co, "KH": self.KH, "KW": self.KW, "sh": self.sh, "sw": self.sw, "ph": self.ph, "pw": self.pw,
+             "Kpad": self.Kpad_d}
+        return (1, self.fwd_cfg(self.Cs, self.M_in), self.G, d)
+
+    def wgrad_args(self, src: dict, dy: Act) -> tuple:
+        d = {"src": src, "dy": dy.p, "dgs": dy.gs, "ldd": dy.ld, "slab": P(self.slab), "splits": self.splits,
+             "m_per_split": self.m_per_split, "B": self.B, "Hi": self.Hi, "Wi": self.Wi, "Ho": self.Ho, "Wo": self.Wo,
+             "Co": self.Co, "Npad": self.Npad, "Cs": self.Cs, "KH": self.KH, "KW": self.KW, "sh": self.sh,
+             "sw": self.sw, "ph": self.ph, "pw": self.pw, "Kpad": self.Kpad_w}
+        return (self.wcfg, self.G, d)
+
+
+# ------------------------------------------------------------------------------------------------
+# descriptor tables (uploaded once; read by wgrad_finalize / adam_pack)
+def build_wgfin_table(descs: List[dict], device) -> tuple:
+    """Pack WgFinDesc structs (layout must match csrc/kernels.h)."""
+    dt = np.dtype([("slab", "<u8"), ("grad", "<u8"), ("ggs", "<i8"), ("G", "<i4"), ("splits", "<i4"),
+                   ("Npad", "<i4"), ("Kpad", "<i4"), ("Co", "<i4"), ("Ci", "<i4"), ("Cs", "<i4"), ("KH", "<i4"),
+                   ("KW", "<i4"), ("_pad", "<i4"), ("elems", "<i8"), ("block0", "<i8")])
+    assert dt.itemsize == lib().SIZEOF_WGFIN, (dt.itemsize, lib().SIZEOF_WGFIN)
+    arr = np.zeros(len(descs), dtype=dt)
+    b0 = 0
+    for i, d in enumerate(descs):
+        for k, v in d.items():
+            arr[i][k] = v
+        arr[i]["block0"] = b0
+        b0 += math.ceil(d["elems"] / 256)
+    t = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+    return t, len(descs), b0
+
+
+def build_optseg_table(segs: List[dict], device) -> tuple:
+    dt = np.dtype([("off", "<i8"), ("n", "<i8"), ("kind", "<i4"), ("_pad0", "<i4"), ("wf", "<u8"), ("wd", "<u8"),
+                   ("Co", "<i4"), ("Ci", "<i4"), ("KH", "<i4"), ("KW", "<i4"), ("Cs", "<i4"), ("Kpad_f", "<i4"),
+                   ("Kpad_d", "<i4"), ("_pad1", "<i4"), ("block0", "<i8")])
+    assert dt.itemsize == lib().SIZEOF_OPTSEG, (dt.itemsize, lib().SIZEOF_OPTSEG)
+    segs = sorted(segs, key=lambda s: s["off"])
+    arr = np.zeros(len(segs), dtype=dt)
+    b0 = 0
+    for i, s in enumerate(segs):
+        for k, v in s.items():
+            arr[i][k] = v
+        arr[i]["block0"] = b0
+        b0 += math.ceil(s["n"] / 1024)
+    t = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+    return t, len(segs), b0

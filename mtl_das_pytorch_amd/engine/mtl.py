@@ -1,0 +1,346 @@
+"""Lowering of the MTL network (reference Model A) and its single-task variant (Model B).
+
+Forward (reference modelA_MTL.py:127-174), per step, all on one HIP stream:
+
+    gather          dataset rows -> bf16 NHWC batch (C padded to 8) + labels
+    conv1           7x7/s3 MFMA conv (+BN sums)           -> tail BN+ReLU
+    resblock i      conv a (+sums) -> tail BN+ReLU -> conv b (+sums) [-> shortcut conv (+sums)]
+                    -> tail relu(BN(b) + BN(s) | x)        = F_i
+    level l, ALL TASKS IN ONE LAUNCH (grid.z = task; shared inputs read with group stride 0):
+                    1x1 conv(+bias) on F_{2l-1} or the two-segment input [F_{2l-1} | B_{l-1,t}]
+                    -> tail BN+ReLU -> 3x3 conv(+bias) -> tail sigmoid(BN) * F_{2l}   = A_{l,t}
+                    l<4: 3x3 conv -> tail maxpool2x2ceil(relu(BN))                   = B_{l,t}
+    head            GAP -> channel-group mean -> log_softmax -> NLL (+metrics, +dL/dA_4)
+
+Backward mirrors it level 4 -> 1 then resblock 8 -> 1 -> conv1; every activation gradient is written
+once and multi-consumer gradients (each F_k feeds the next block AND the task branches) are summed by
+the consuming kernel from a list of sources.  Weight gradients go to split-M slabs that one launch
+reduces into the flat gradient buffer; then one fused Adam launch updates the flat master weights and
+re-packs the bf16 MFMA images.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ..models.mtl import MTLNet
+from ..ops.hip import lib
+from .core import (NREP, Act, Arena, BNLayer, ConvLayer, FlatState, P, build_optseg_table, build_wgfin_table,
+                   new_act, src_dict)
+from .program import (Phase, k_adam, k_conv, k_gather, k_head, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad)
+
+ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
+
+
+def _blocks(M: int, C: int, cap: int = 1024, per_thread: int = 4) -> int:
+    cg = max(1, C // 8)
+    pl = max(1, 256 // cg)
+    return int(max(1, min(cap, math.ceil(M / (pl * per_thread)))))
+
+
+class MTLProgram:
+    """Static train/eval programs of an :class:`MTLNet` for a fixed per-GPU batch size."""
+
+    def __init__(self, model: MTLNet, batch: int, device, in_hw=(100, 250), loss_weights: Optional[Sequence[float]] = None):
+        self.model = model
+        self.B = B = batch
+        self.T = T = len(model.tasks)
+        self.device = torch.device(device)
+        self.H0, self.W0 = in_hw
+        self.cin = model.in_channels
+        if self.cin > 8:
+            raise ValueError("in_channels > 8 not supported by the gather kernel")
+        self.loss_weights = list(loss_weights) if loss_weights is not None else [1.0] * T
+        if len(self.loss_weights) != T:
+            raise ValueError("one loss weight per task")
+        # label column of each task in the [B, 2] (distance, event) label tensor
+        self.lab_off = [0 if t == "distance" else 1 for t in model.tasks]
+        if T == 2 and self.lab_off != [0, 1]:
+            raise ValueError("two-task model must be (distance, event)")
+
+        gens = model.att_generators
+        outs = model.output_layers
+        pgroups, bgroups = [], []
+        for lvl in range(4):
+            g = gens[lvl]
+            for idx in (0, 3):
+                pgroups += [[g[t][idx].weight for t in range(T)], [g[t][idx].bias for t in range(T)]]
+            for idx in (1, 4):
+                pgroups += [[g[t][idx].weight for t in range(T)], [g[t][idx].bias for t in range(T)]]
+                bgroups.append([g[t][idx] for t in range(T)])
+            if lvl < 3:
+                o = outs[lvl]
+                pgroups += [[o[t][0].weight for t in range(T)], [o[t][1].weight for t in range(T)],
+                            [o[t][1].bias for t in range(T)]]
+                bgroups.append([o[t][1] for t in range(T)])
+        model.to(self.device)
+        self.flat = FlatState(model, self.device, pgroups, bgroups)
+        self.arena = A = Arena(self.device)
+        self._alloc()
+        A.finalize()
+        self._emit()
+
+    # -------------------------------------------------------------------------------------------
+    def _alloc(self):
+        m, A, B, T, f = self.model, self.arena, self.B, self.T, self.flat
+        self.x = A.zeros((B, self.H0, self.W0, 8))
+        self.labels = torch.zeros((B, 2), dtype=torch.int64, device=self.device)
+        self.xin = Act(self.x, 0, 8, 8, 0, B, self.H0, self.W0)
+        # stem
+        c1 = ConvLayer([m.conv1[0]], f, A, B, self.H0, self.W0, cin_stored=8)
+        self.conv1 = c1
+        H, W = c1.Ho, c1.Wo
+        self.bn1 = BNLayer([m.conv1[1]], f, A, B * H * W)
+        self.y0 = new_act(A, 1, B, H, W, c1.Co)
+        self.f0 = new_act(A, 1, B, H, W, c1.Co)
+        # residual blocks
+        self.rbs = []
+        prev = self.f0
+        for rb in m.resblocks:
+            L = {}
+            ca = ConvLayer([rb.left[0]], f, A, B, prev.H, prev.W)
+            Ho, Wo, C = ca.Ho, ca.Wo, ca.Co
+            L["ca"], L["bna"] = ca, BNLayer([rb.left[1]], f, A, B * Ho * Wo)
+            L["cb"], L["bnb"] = ConvLayer([rb.left[3]], f, A, B, Ho, Wo), BNLayer([rb.left[4]], f, A, B * Ho * Wo)
+            L["proj"] = rb.has_projection
+            if rb.has_projection:
+                L["cs"] = ConvLayer([rb.shortcut[0]], f, A, B, prev.H, prev.W)
+                L["bns"] = BNLayer([rb.shortcut[1]], f, A, B * Ho * Wo)
+                L["bnb"].ws2 = A.zeroed((1, NREP, 2, C))
+                L["ys"] = new_act(A, 1, B, Ho, Wo, C)
+                L["dys"] = new_act(A, 1, B, Ho, Wo, C)
+                L["dxs"] = new_act(A, 1, B, prev.H, prev.W, prev.C, torch.float32)
+            else:
+                L["side"] = new_act(A, 1, B, Ho, Wo, C, torch.float32)
+            L["in"] = prev
+            L["ya"], L["ha"], L["yb"] = (new_act(A, 1, B, Ho, Wo, C) for _ in range(3))
+            L["out"] = new_act(A, 1, B, Ho, Wo, C)
+            L["dyb"], L["dya"] = new_act(A, 1, B, Ho, Wo, C), new_act(A, 1, B, Ho, Wo, C)
+            L["dha"] = new_act(A, 1, B, Ho, Wo, C, torch.float32)
+            L["dxa"] = new_act(A, 1, B, prev.H, prev.W, prev.C, torch.float32)
+            self.rbs.append(L)
+            prev = L["out"]
+        self.F = [L["out"] for L in self.rbs]  # F1..F8 (index 0..7)
+        # task levels (grouped over T)
+        gens, outs = m.att_generators, m.output_layers
+        self.levels = []
+        prevB = None
+        for lvl in range(4):
+            Fa, Fb = self.F[2 * lvl], self.F[2 * lvl + 1]
+            H, W, C = Fa.H, Fa.W, Fa.C
+            g = gens[lvl]
+            L = {"H": H, "W": W, "C": C, "Fa": Fa, "Fb": Fb, "prevB": prevB}
+            cin = C + (prevB.C if prevB is not None else 0)
+            L["c0"] = ConvLayer([g[t][0] for t in range(T)], f, A, B, H, W)
+            assert L["c0"].Ci == cin
+            cm = L["c0"].Co
+            L["bn0"] = BNLayer([g[t][1] for t in range(T)], f, A, B * H * W)
+            L["c3"] = ConvLayer([g[t][3] for t in range(T)], f, A, B, H, W)
+            L["bn3"] = BNLayer([g[t][4] for t in range(T)], f, A, B * H * W)
+            L["ym1"], L["hm"] = new_act(A, T, B, H, W, cm), new_act(A, T, B, H, W, cm)
+            L["ym2"], L["Aout"] = new_act(A, T, B, H, W, C), new_act(A, T, B, H, W, C)
+            L["dym2"] = new_act(A, T, B, H, W, C)
+            L["dF"] = new_act(A, T, B, H, W, C, torch.float32)   # side: gradient of F_{2l} per task
+            L["dhm"] = new_act(A, T, B, H, W, cm, torch.float32)
+            L["dym1"] = new_act(A, T, B, H, W, cm)
+            L["dcat"] = new_act(A, T, B, H, W, cin, torch.float32)
+            if lvl < 3:
+                o = outs[lvl]
+                L["co"] = ConvLayer([o[t][0] for t in range(T)], f, A, B, H, W)
+                L["bno"] = BNLayer([o[t][1] for t in range(T)], f, A, B * H * W)
+                Co = L["co"].Co
+                L["yo"], L["dyo"] = new_act(A, T, B, H, W, Co), new_act(A, T, B, H, W, Co)
+                L["dA"] = new_act(A, T, B, H, W, C, torch.float32)
+                Hp, Wp = (H + 1) // 2, (W + 1) // 2
+                L["Bp"] = new_act(A, T, B, Hp, Wp, Co)
+                prevB = L["Bp"]
+            self.levels.append(L)
+        L4 = self.levels[3]
+        self.dA4 = new_act(A, T, B, L4["H"], L4["W"], L4["C"], torch.float32)
+        self.levels[3]["dA"] = self.dA4
+        # head outputs / metrics (NOT in the per-step zeroed region: they accumulate across steps)
+        self.logp = torch.zeros((T, B, 16), device=self.device)
+        self.metrics = torch.zeros((T, 4), device=self.device)
+        self.confusion = torch.zeros((T, 16, 16), device=self.device, dtype=torch.int32)
+        self.nvalid = torch.full((1,), B, device=self.device, dtype=torch.int64)
+        self.convs: List[ConvLayer] = [c1] + [L[k] for L in self.rbs for k in ("ca", "cb", "cs") if k in L] + \
+                                      [L[k] for L in self.levels for k in ("c0", "c3", "co") if k in L]
+
+    # -------------------------------------------------------------------------------------------
+    def _tail(self, ph: Phase, kind: int, G: int, y: Act, bn: BNLayer, out: Act, training: bool, r: Act = None,
+              bn2: BNLayer = None, H=None, W=None):
+        d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(training), "out": out.p, "ogs": out.gs, "ldo": out.ld,
+             "B": self.B, "H": y.H if H is None else H, "W": y.W if W is None else W, "C": y.C}
+        if r is not None:
+            d.update({"r": r.p, "rgs": r.gs, "ldr": r.ld})
+        if bn2 is not None:
+            d["bn2"] = bn2.args(training)
+        M = self.B * d["H"] * d["W"]
+        ph.add(f"tail{kind}", k_tail_fwd, kind, G, _blocks(M, y.C), d)
+
+    def _tail_bwd(self, ph: Phase, kind: int, G: int, y: Act, bn: BNLayer, g: list, dy: Act, r: Act = None,
+                  bn2: BNLayer = None, side: Act = None, dy2: Act = None):
+        d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(True), "B": self.B, "H": y.H, "W": y.W, "C": y.C,
+             "g": g, "ws": P(bn.ws), "dy": dy.p, "dgs": dy.gs, "ldd": dy.ld}
+        d.update(bn.grad_ptrs())
+        if r is not None:
+            d.update({"r": r.p, "rgs": r.gs, "ldr": r.ld})
+        if bn2 is not None:
+            d["bn2"] = bn2.args(True)
+            d["ws2"] = P(bn.ws2)
+            gp = bn2.grad_ptrs()
+            d.update({"dgamma2": gp["dgamma"], "dbeta2": gp["dbeta"], "dy2": dy2.p, "d2gs": dy2.gs, "ldd2": dy2.ld})
+        if side is not None:
+            d.update({"side": side.p, "sgs": side.gs, "lds": side.ld})
+        ph.add(f"tailbwd{kind}", k_tail_bwd, kind, G, _blocks(y.M, y.C, cap=256), d)
+
+    def _conv_fwd(self, ph: Phase, c: ConvLayer, src: dict, out: Act, bn: BNLayer, training: bool):
+        mode, cfg, G, d = c.fwd_args(src, out, bn, training)
+        ph.add("conv_fwd", k_conv, mode, cfg, G, d)
+
+    def _conv_bwd(self, ph: Phase, c: ConvLayer, src: dict, dy: Act, dx: Optional[Act]):
+        cfg, G, d = c.wgrad_args(src, dy)
+        ph.add("conv_wgrad", k_wgrad, cfg, G, d)
+        if dx is not None:
+            mode, cfg, G, d = c.dgrad_args(dy, dx)
+            ph.add("conv_dgrad", k_conv, mode, cfg, G, d)
+
+    def _emit(self):
+        self.fwd_train = self._emit_forward(True)
+        self.fwd_eval = self._emit_forward(False)
+        self.bwd = self._emit_backward()
+        self.opt = self._emit_optimizer()
+
+    def set_source(self, X: torch.Tensor, labels: torch.Tensor, idx: torch.Tensor):
+        """Bind the dataset tensors the gather launch reads (X [N,C,H,W] fp32, labels [N,2], idx [B])."""
+        self.src = (X, labels, idx)
+
+    def gather_phase(self, X, labels, idx) -> Phase:
+        ph = Phase("gather")
+        ph.add("gather", k_gather, X, idx, labels, 2, self.x, self.labels, self.B, X.shape[1], self.H0, self.W0)
+        return ph
+
+    def _emit_forward(self, training: bool) -> Phase:
+        ph = Phase("forward_train" if training else "forward_eval")
+        T = self.T
+        self._conv_fwd(ph, self.conv1, src_dict(self.xin), self.y0, self.bn1, training)
+        self._tail(ph, ACT_RELU, 1, self.y0, self.bn1, self.f0, training)
+        for L in self.rbs:
+            s = src_dict(L["in"])
+            self._conv_fwd(ph, L["ca"], s, L["ya"], L["bna"], training)
+            self._tail(ph, ACT_RELU, 1, L["ya"], L["bna"], L["ha"], training)
+            self._conv_fwd(ph, L["cb"], src_dict(L["ha"]), L["yb"], L["bnb"], training)
+            if L["proj"]:
+                self._conv_fwd(ph, L["cs"], s, L["ys"], L["bns"], training)
+                self._tail(ph, ADD_RELU, 1, L["yb"], L["bnb"], L["out"], training, r=L["ys"], bn2=L["bns"])
+            else:
+                self._tail(ph, ADD_RELU, 1, L["yb"], L["bnb"], L["out"], training, r=L["in"])
+        for L in self.levels:
+            s = src_dict(L["Fa"], L["prevB"]) if L["prevB"] is not None else src_dict(L["Fa"])
+            self._conv_fwd(ph, L["c0"], s, L["ym1"], L["bn0"], training)
+            self._tail(ph, ACT_RELU, T, L["ym1"], L["bn0"], L["hm"], training)
+            self._conv_fwd(ph, L["c3"], src_dict(L["hm"]), L["ym2"], L["bn3"], training)
+            self._tail(ph, SIGMUL, T, L["ym2"], L["bn3"], L["Aout"], training, r=L["Fb"])
+            if "co" in L:
+                self._conv_fwd(ph, L["co"], src_dict(L["Aout"]), L["yo"], L["bno"], training)
+                self._tail(ph, POOL_RELU, T, L["yo"], L["bno"], L["Bp"], training)
+        A4 = self.levels[3]["Aout"]
+        hd = {"feat": A4.p, "fgs": A4.gs, "ldf": A4.ld, "labels": P(self.labels), "lab_stride": 2,
+              "lab_off": self.lab_off[0], "T": T, "B": self.B, "HW": A4.H * A4.W, "C": A4.C,
+              "ncls": list(self.model.task_cate_num), "w": [float(w) for w in self.loss_weights],
+              "logp": P(self.logp), "dfeat": self.dA4.p if training else 0, "dgs": self.dA4.gs,
+              "metrics": P(self.metrics), "confusion": P(self.confusion), "nvalid": P(self.nvalid)}
+        if T == 2:
+            hd["lab_off"] = 0
+        ph.add("mtl_head", k_head, hd)
+        return ph
+
+    def _emit_backward(self) -> Phase:
+        ph = Phase("backward")
+        T, lv = self.T, self.levels
+        for li in range(3, -1, -1):
+            L = lv[li]
+            if "co" in L:
+                nxt = lv[li + 1]
+                Cn = nxt["Fa"].C
+                dcat = nxt["dcat"]
+                g = [(P(dcat.t, Cn), dcat.gs, dcat.ld)]  # B_l part of d cat[F, B_l]
+                self._tail_bwd(ph, POOL_RELU, T, L["yo"], L["bno"], g, L["dyo"])
+                self._conv_bwd(ph, L["co"], src_dict(L["Aout"]), L["dyo"], L["dA"])
+            self._tail_bwd(ph, SIGMUL, T, L["ym2"], L["bn3"], [(L["dA"].p, L["dA"].gs, L["dA"].ld)], L["dym2"],
+                           r=L["Fb"], side=L["dF"])
+            self._conv_bwd(ph, L["c3"], src_dict(L["hm"]), L["dym2"], L["dhm"])
+            self._tail_bwd(ph, ACT_RELU, T, L["ym1"], L["bn0"], [(L["dhm"].p, L["dhm"].gs, L["dhm"].ld)], L["dym1"])
+            s = src_dict(L["Fa"], L["prevB"]) if L["prevB"] is not None else src_dict(L["Fa"])
+            self._conv_bwd(ph, L["c0"], s, L["dym1"], L["dcat"])
+        # gradient sources of each shared feature F_k (index k-1), plus f0
+        def sources(k: int) -> list:
+            src = []
+            if k >= 1:
+                lvl = (k - 1) // 2
+                L = lv[lvl]
+                for t in range(T):
+                    if k % 2 == 1:  # F_{2l-1}: first channel segment of the level's AMG input
+                        src.append((P(L["dcat"].t, t * L["dcat"].gs), 0, L["dcat"].ld))
+                    else:           # F_{2l}: attention-mask target
+                        src.append((P(L["dF"].t, t * L["dF"].gs), 0, L["dF"].ld))
+            if k < 8:
+                R = self.rbs[k]  # resblock k+1 consumes F_k (or f0 when k == 0)
+                src.append((R["dxa"].p, 0, R["dxa"].ld))
+                if R["proj"]:
+                    src.append((R["dxs"].p, 0, R["dxs"].ld))
+                else:
+                    src.append((R["side"].p, 0, R["side"].ld))
+            return src
+        for i in range(7, -1, -1):
+            R = self.rbs[i]
+            g = sources(i + 1)
+            if R["proj"]:
+                self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["ys"], bn2=R["bns"], dy2=R["dys"])
+            else:
+                self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["in"], side=R["side"])
+            self._conv_bwd(ph, R["cb"], src_dict(R["ha"]), R["dyb"], R["dha"])
+            self._tail_bwd(ph, ACT_RELU, 1, R["ya"], R["bna"], [(R["dha"].p, 0, R["dha"].ld)], R["dya"])
+            self._conv_bwd(ph, R["ca"], src_dict(R["in"]), R["dya"], R["dxa"])
+            if R["proj"]:
+                self._conv_bwd(ph, R["cs"], src_dict(R["in"]), R["dys"], R["dxs"])
+        self.dy0 = new_act(self.arena, 1, self.B, self.y0.H, self.y0.W, self.y0.C)
+        self._tail_bwd(ph, ACT_RELU, 1, self.y0, self.bn1, sources(0), self.dy0)
+        self._conv_bwd(ph, self.conv1, src_dict(self.xin), self.dy0, None)
+        # weight-gradient slabs -> flat fp32 gradients (one launch for every conv)
+        self.wgfin_table, nd, nblocks = build_wgfin_table([c.finalize_desc() for c in self.convs], self.device)
+        ph.add("wgrad_finalize", k_wgfin, self.wgfin_table, nd, nblocks)
+        return ph
+
+    def _emit_optimizer(self, grad_scale: float = 1.0) -> Dict[str, Phase]:
+        segs = []
+        conv_w = set()
+        for c in self.convs:
+            for s in c.opt_segments():
+                segs.append(s)
+            conv_w.update(id(m.weight) for m in c.mods)
+        for p in self.flat.order:
+            if id(p) not in conv_w:
+                segs.append({"off": self.flat.off(p), "n": p.numel(), "kind": 0})
+        self.optseg_table, ns, nblocks = build_optseg_table(segs, self.device)
+        f = self.flat
+        base = {"p": P(f.params), "g": P(f.grads), "m": P(f.exp_avg), "v": P(f.exp_avg_sq), "lr": P(f.lr),
+                "step": P(f.step), "segs": P(self.optseg_table), "nsegs": ns, "nblocks": nblocks}
+        self._opt_base = base
+        upd = Phase("adam")
+        upd.add("adam_pack", k_adam, dict(base, update=1, b1=0.9, b2=0.999, eps=1e-8, wd=0.0, grad_scale=grad_scale))
+        pack = Phase("pack")
+        pack.add("pack", k_adam, dict(base, update=0))
+        return {"adam": upd, "pack": pack}
+
+    def set_optimizer(self, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, grad_scale: float = 1.0):
+        d = dict(self._opt_base, update=1, b1=betas[0], b2=betas[1], eps=eps, wd=weight_decay, grad_scale=grad_scale)
+        upd = Phase("adam")
+        upd.add("adam_pack", k_adam, d)
+        self.opt["adam"] = upd
+
+    # -------------------------------------------------------------------------------------------
+    def num_launches(self) -> dict:
+        return {"forward_train": len(self.fwd_train), "backward": len(self.bwd), "adam": len(self.opt["adam"]) + 1}

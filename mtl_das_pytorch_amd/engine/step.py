@@ -1,0 +1,126 @@
+"""Train / eval step execution for a lowered program, with HIP-graph capture.
+
+A training step is
+
+    [memset zeroed arena] [gather batch] [forward] [backward]  ->  (DP: RCCL all-reduce of the flat
+    gradient bucket)  ->  [fused Adam + bf16 re-pack] [step++]
+
+Single GPU: the whole step is ONE captured HIP graph (``torch.cuda.CUDAGraph`` is a hipGraph on ROCm),
+so a step costs one graph launch from the host.  Data parallel: the all-reduce sits between two graphs
+(compute graph, optimizer graph) so RCCL runs eagerly on the same stream -- no reliance on collective
+capture -- and its ~4.5 MB bucket (Model A) is a single call.
+
+The batch indices live in a persistent device buffer that the host refreshes (device-to-device copy)
+before each replay; the learning rate is a device scalar, so the reference's LR schedule never forces
+a re-capture.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from .program import Phase
+
+
+class StateSnapshot:
+    """Save/restore every tensor a step mutates (used to make warm-up runs side-effect free)."""
+
+    def __init__(self, tensors: List[torch.Tensor]):
+        self.tensors = tensors
+        self.saved = [t.detach().clone() for t in tensors]
+
+    def restore(self):
+        for t, s in zip(self.tensors, self.saved):
+            t.copy_(s)
+
+
+class StepRunner:
+    def __init__(self, program, X: torch.Tensor, labels: torch.Tensor, use_graph: bool = True,
+                 allreduce: Optional[Callable[[torch.Tensor], None]] = None, X_eval: torch.Tensor = None,
+                 labels_eval: torch.Tensor = None):
+        self.p = program
+        self.use_graph = use_graph and program.device.type == "cuda"
+        self.allreduce = allreduce
+        B = program.B
+        self.idx = torch.zeros(B, dtype=torch.int64, device=program.device)
+        self.sources = {"train": (X, labels)}
+        if X_eval is not None:
+            self.sources["eval"] = (X_eval, labels_eval)
+        self.graphs: Dict[str, torch.cuda.CUDAGraph] = {}
+        self._packed = False
+
+    # -------------------------------------------------------------------------------------------
+    def _mutable_state(self) -> List[torch.Tensor]:
+        f = self.p.flat
+        return [f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step, self.p.metrics,
+                self.p.confusion, self.p.logp]
+
+    def pack_weights(self):
+        """(Re)build the bf16 MFMA weight images from the fp32 masters (after init / load_state_dict)."""
+        self.p.opt["pack"].run()
+        self._packed = True
+
+    def _phases(self, kind: str) -> List[Callable[[], None]]:
+        p = self.p
+        X, lab = self.sources["train" if kind.startswith("train") else "eval"]
+        gather = p.gather_phase(X, lab, self.idx)
+        if kind == "train_compute":
+            return [p.arena.clear, gather.run, p.fwd_train.run, p.bwd.run]
+        if kind == "train_opt":
+            return [p.opt["adam"].run]
+        if kind == "train_full":
+            return [p.arena.clear, gather.run, p.fwd_train.run, p.bwd.run, p.opt["adam"].run]
+        if kind == "eval":
+            return [gather.run, p.fwd_eval.run]
+        raise ValueError(kind)
+
+    def _run(self, kind: str):
+        fns = self._phases(kind)
+        if not self.use_graph:
+            for f in fns:
+                f()
+            return
+        g = self.graphs.get(kind)
+        if g is None:
+            snap = StateSnapshot(self._mutable_state())
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):  # warm-up (loads code objects); side effects are rolled back
+                for f in fns:
+                    f()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            snap.restore()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for f in fns:
+                    f()
+            torch.cuda.synchronize()
+            self.graphs[kind] = g
+        g.replay()
+
+    # -------------------------------------------------------------------------------------------
+    def set_lr(self, lr: float):
+        self.p.flat.lr.fill_(float(lr))
+
+    def train_step(self, idx: torch.Tensor):
+        if not self._packed:
+            self.pack_weights()
+        self.idx.copy_(idx, non_blocking=True)
+        if self.allreduce is None:
+            self._run("train_full")
+        else:
+            self._run("train_compute")
+            self.allreduce(self.p.flat.grads)
+            self._run("train_opt")
+
+    def eval_step(self, idx: torch.Tensor):
+        if not self._packed:
+            self.pack_weights()
+        self.idx.copy_(idx, non_blocking=True)
+        self._run("eval")
+
+    def reset_metrics(self):
+        self.p.metrics.zero_()
+        self.p.confusion.zero_()

@@ -1,0 +1,233 @@
+"""Functional (tensor-in / tensor-out) entry points to the HIP kernels.
+
+These are the stand-alone versions of what the engine launches from prebuilt programs; they are used by
+the kernel numerics tests and are convenient for experimentation.  All activations are NHWC
+(``[B, H, W, C]``) on the GPU; weights use the reference PyTorch layout ``[Co, Ci, KH, KW]`` (fp32).
+Every function requires a CUDA (ROCm) tensor and the built extension -- there is no silent fallback.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .hip import lib, ptr, stream
+
+NREP = 8
+
+
+def _pad(x, m):
+    return (x + m - 1) // m * m
+
+
+def _check(t: torch.Tensor, dtype=None):
+    if not t.is_cuda:
+        raise RuntimeError("HIP ops need a GPU tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError("expected a contiguous tensor")
+
+
+def pack_weight_fwd(w: torch.Tensor, cin_stored: Optional[int] = None) -> torch.Tensor:
+    Co, Ci, KH, KW = w.shape
+    Cs = cin_stored or Ci
+    t = torch.zeros(Co, KH, KW, Cs, device=w.device)
+    t[..., :Ci] = w.permute(0, 2, 3, 1)
+    K = KH * KW * Cs
+    out = torch.zeros(_pad(Co, 16), _pad(K, 32), device=w.device, dtype=torch.bfloat16)
+    out[:Co, :K] = t.reshape(Co, K).to(torch.bfloat16)
+    return out
+
+
+def pack_weight_dgrad(w: torch.Tensor, cin_stored: Optional[int] = None) -> torch.Tensor:
+    Co, Ci, KH, KW = w.shape
+    Cs = cin_stored or Ci
+    K = KH * KW * Co
+    out = torch.zeros(_pad(Cs, 16), _pad(K, 32), device=w.device, dtype=torch.bfloat16)
+    out[:Ci, :K] = w.permute(1, 2, 3, 0).reshape(Ci, K).to(torch.bfloat16)
+    return out
+
+
+def _geom(x_shape, w_shape, stride, padding):
+    B, H, W, _ = x_shape
+    Co, Ci, KH, KW = w_shape
+    sh, sw = (stride, stride) if isinstance(stride, int) else stride
+    ph, pw = (padding, padding) if isinstance(padding, int) else padding
+    Ho = (H + 2 * ph - KH) // sh + 1
+    Wo = (W + 2 * pw - KW) // sw + 1
+    return B, H, W, Co, Ci, KH, KW, sh, sw, ph, pw, Ho, Wo
+
+
+def _fwd_cfg(N, M):
+    if N <= 16:
+        return 0
+    if N <= 32:
+        return 1
+    if N <= 64:
+        return 2 if M >= 64 * 256 else 4
+    return 3 if M >= 64 * 128 else 4
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0,
+           stats: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
+    """NHWC bf16 convolution.  ``x2`` (optional) is a second input whose channels are concatenated after
+    ``x``'s (the kernel reads both without materialising the concat).  ``stats`` ([NREP, 2, Co] fp32,
+    zero-initialised by the caller) receives per-channel sums of the output and its square."""
+    _check(x, torch.bfloat16)
+    C1 = x2.shape[-1] if x2 is not None else 0
+    Cs = x.shape[-1] + C1
+    B, H, W, Co, Ci, KH, KW, sh, sw, ph, pw, Ho, Wo = _geom(x.shape, w.shape, stride, padding)
+    if Ci > Cs:
+        raise ValueError("weight has more input channels than the input")
+    wf = pack_weight_fwd(w.float(), Cs)
+    y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=torch.bfloat16)
+    src = {"p0": ptr(x), "ld0": x.shape[-1], "C0": x.shape[-1], "C1": C1}
+    if x2 is not None:
+        _check(x2, torch.bfloat16)
+        src.update({"p1": ptr(x2), "ld1": C1})
+    d = {"src": src, "w": ptr(wf), "bias": ptr(bias) if bias is not None else 0, "out": ptr(y), "ldo": Co,
+         "stats": ptr(stats) if stats is not None else 0, "B": B, "Hs": H, "Ws": W, "Ho": Ho, "Wo": Wo, "N": Co,
+         "Npad": wf.shape[0], "Cs": Cs, "KH": KH, "KW": KW, "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": wf.shape[1]}
+    lib().conv(0, _fwd_cfg(Co, B * Ho * Wo) if cfg is None else cfg, 1, stream(), d)
+    return y
+
+
+def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw: Tuple[int, int], stride=1, padding=0,
+                 cin_stored: Optional[int] = None, cfg: Optional[int] = None):
+    """Gradient w.r.t. the NHWC input: fp32 ``[B, H, W, Cin_stored]``."""
+    _check(dy, torch.bfloat16)
+    B, Ho, Wo, Co = dy.shape
+    _, Ci, KH, KW = w.shape
+    Cs = cin_stored or Ci
+    H, W = in_hw
+    sh, sw = (stride, stride) if isinstance(stride, int) else stride
+    ph, pw = (padding, padding) if isinstance(padding, int) else padding
+    wd = pack_weight_dgrad(w.float(), Cs)
+    dx = torch.empty(B, H, W, Cs, device=dy.device, dtype=torch.float32)
+    d = {"src": {"p0": ptr(dy), "ld0": Co, "C0": Co, "C1": 0}, "w": ptr(wd), "out": ptr(dx), "ldo": Cs,
+         "B": B, "Hs": Ho, "Ws": Wo, "Ho": H, "Wo": W, "N": Cs, "Npad": wd.shape[0], "Cs": Co, "KH": KH, "KW": KW,
+         "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": wd.shape[1]}
+    lib().conv(1, _fwd_cfg(Cs, B * H * W) if cfg is None else cfg, 1, stream(), d)
+    return dx
+
+
+def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, w_shape, stride=1, padding=0, x2: Optional[torch.Tensor] = None,
+                 splits: Optional[int] = None, cfg: Optional[int] = None):
+    """Weight gradient in the reference layout ``[Co, Ci, KH, KW]`` (fp32)."""
+    _check(x, torch.bfloat16)
+    _check(dy, torch.bfloat16)
+    Co, Ci, KH, KW = w_shape
+    C1 = x2.shape[-1] if x2 is not None else 0
+    Cs = x.shape[-1] + C1
+    B, H, W, _ = x.shape
+    _, Ho, Wo, _ = dy.shape
+    sh, sw = (stride, stride) if isinstance(stride, int) else stride
+    ph, pw = (padding, padding) if isinstance(padding, int) else padding
+    Kpad = _pad(KH * KW * Cs, 64)
+    Npad = _pad(Co, 16)
+    if cfg is None:
+        cfg = 0 if Co <= 16 else ((1 if Kpad <= 64 else 2) if Co <= 32 else 3)
+    TN, TK, MCH = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 64)}[cfg]
+    M = B * Ho * Wo
+    tiles = math.ceil(Npad / TN) * (Kpad // TK)
+    if splits is None:
+        splits = max(1, min(math.ceil(M / MCH), math.ceil(512 / tiles)))
+    mps = _pad(math.ceil(M / splits), MCH)
+    splits = math.ceil(M / mps)
+    slab = torch.empty(1, splits, Npad, Kpad, device=x.device, dtype=torch.float32)
+    src = {"p0": ptr(x), "ld0": x.shape[-1], "C0": x.shape[-1], "C1": C1}
+    if x2 is not None:
+        src.update({"p1": ptr(x2), "ld1": C1})
+    d = {"src": src, "dy": ptr(dy), "ldd": Co, "slab": ptr(slab), "splits": splits, "m_per_split": mps,
+         "B": B, "Hi": H, "Wi": W, "Ho": Ho, "Wo": Wo, "Co": Co, "Npad": Npad, "Cs": Cs, "KH": KH, "KW": KW,
+         "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": Kpad}
+    lib().wgrad(cfg, 1, stream(), d)
+    dWp = slab.sum(dim=1)[0, :Co, :KH * KW * Cs].view(Co, KH, KW, Cs)[..., :Ci]
+    return dWp.permute(0, 3, 1, 2).contiguous()
+
+
+# ---------------------------------------------------------------------------------------------------
+ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
+
+
+def bn_args(stats, gamma, beta, run_mean, run_var, nbt, count, eps=1e-5, momentum=0.1, training=True):
+    """Kernel BN descriptor.  The dict keeps references to the tensors it points at (``_keep``) so that
+    they cannot be freed while a launch may still use them."""
+    return {"_keep": (stats, gamma, beta, run_mean, run_var, nbt),"stats": ptr(stats), "gamma": ptr(gamma), "beta": ptr(beta), "run_mean": ptr(run_mean),
+            "run_var": ptr(run_var), "nbt": ptr(nbt) if nbt is not None else 0, "pstride": 0, "C": gamma.numel(),
+            "count": count, "eps": eps, "momentum": momentum, "training": 1 if training else 0}
+
+
+def bn_tail(kind: int, y: torch.Tensor, bn: dict, r: Optional[torch.Tensor] = None, bn2: Optional[dict] = None,
+            blocks: int = 64):
+    """Fused BN(+act/+mul/+residual/+pool) forward on NHWC bf16 ``y``; returns the bf16 output."""
+    B, H, W, C = y.shape
+    if kind == POOL_RELU:
+        out = torch.empty(B, (H + 1) // 2, (W + 1) // 2, C, device=y.device, dtype=torch.bfloat16)
+    else:
+        out = torch.empty_like(y)
+    d = {"y": ptr(y), "ldy": C, "bn": bn, "out": ptr(out), "ldo": C, "B": B, "H": H, "W": W, "C": C}
+    if r is not None:
+        d.update({"r": ptr(r), "ldr": r.shape[-1]})
+    if bn2 is not None:
+        d["bn2"] = bn2
+    lib().tail_fwd(kind, 1, blocks, stream(), d)
+    return out
+
+
+def bn_tail_backward(kind: int, y: torch.Tensor, bn: dict, grads: Sequence[torch.Tensor], dgamma, dbeta,
+                     r: Optional[torch.Tensor] = None, bn2: Optional[dict] = None, dgamma2=None, dbeta2=None,
+                     blocks: int = 64):
+    """Returns ``(dy bf16, side fp32 | None, dy2 bf16 | None)``; writes dgamma/dbeta (and 2) in place."""
+    B, H, W, C = y.shape
+    ws = torch.zeros(1, NREP, 2, C, device=y.device)
+    dy = torch.empty_like(y)
+    d = {"y": ptr(y), "ldy": C, "bn": bn, "B": B, "H": H, "W": W, "C": C,
+         "g": [(ptr(g), 0, g.shape[-1]) for g in grads], "ws": ptr(ws), "dy": ptr(dy), "ldd": C,
+         "dgamma": ptr(dgamma), "dbeta": ptr(dbeta)}
+    side = dy2 = None
+    if r is not None:
+        d.update({"r": ptr(r), "ldr": r.shape[-1]})
+    if kind in (SIGMUL,) or (kind == ADD_RELU and bn2 is None):
+        side = torch.empty(B, H, W, C, device=y.device, dtype=torch.float32)
+        d.update({"side": ptr(side), "lds": C})
+    if bn2 is not None:
+        ws2 = torch.zeros(1, NREP, 2, C, device=y.device)
+        dy2 = torch.empty_like(y)
+        d.update({"bn2": bn2, "ws2": ptr(ws2), "dy2": ptr(dy2), "ldd2": C, "dgamma2": ptr(dgamma2),
+                  "dbeta2": ptr(dbeta2)})
+    lib().tail_bwd(kind, 1, blocks, stream(), d)
+    return dy, side, dy2
+
+
+def pool3(x: torch.Tensor, is_max: bool):
+    """Inception pools on NHWC bf16: max 3x3/s2 (valid) or avg 3x3/s1/p1 (count_include_pad)."""
+    B, H, W, C = x.shape
+    Ho, Wo = ((H - 3) // 2 + 1, (W - 3) // 2 + 1) if is_max else (H, W)
+    y = torch.empty(B, Ho, Wo, C, device=x.device, dtype=torch.bfloat16)
+    lib().pool3(int(is_max), 0, stream(), {"x": ptr(x), "ldx": C, "y": ptr(y), "ldy": C, "B": B, "H": H, "W": W,
+                                            "C": C, "Ho": Ho, "Wo": Wo})
+    return y
+
+
+def pool3_backward(x: torch.Tensor, g: torch.Tensor, is_max: bool):
+    B, H, W, C = x.shape
+    _, Ho, Wo, _ = g.shape
+    dx = torch.empty(B, H, W, C, device=x.device, dtype=torch.float32)
+    lib().pool3(int(is_max), 1, stream(), {"x": ptr(x), "ldx": C, "g": ptr(g), "ldg": C, "dx": ptr(dx), "lddx": C,
+                                            "B": B, "H": H, "W": W, "C": C, "Ho": Ho, "Wo": Wo})
+    return dx
+
+
+def gather_batch(X: torch.Tensor, labels: torch.Tensor, idx: torch.Tensor):
+    """HBM-resident dataset rows -> (bf16 NHWC batch with C padded to 8, labels)."""
+    N, Cin, H, W = X.shape
+    B = idx.numel()
+    lw = labels.shape[1] if labels.dim() == 2 else 1
+    out = torch.empty(B, H, W, 8, device=X.device, dtype=torch.bfloat16)
+    lab = torch.empty(B, lw, device=X.device, dtype=torch.int64)
+    lib().gather_batch(ptr(X), ptr(idx), ptr(labels), lw, ptr(out), ptr(lab), B, Cin, H, W, stream())
+    return out, lab

@@ -1,0 +1,171 @@
+"""Data-parallel training over RCCL (torch.distributed backend "nccl" is RCCL on ROCm) across xGMI.
+
+The reference has no distributed code at all; this module adds, MI355X-first:
+
+  C1  broadcast of parameters + BN buffers from rank 0 (once, and after loading a checkpoint)
+  C2  all-reduce(SUM) of the *flat* fp32 gradient buffer -- the engine's gradients already live in one
+      contiguous, persistent buffer, so there is no pack/unpack; the 1/world averaging is folded into
+      the fused Adam kernel (grad_scale).  Model A's whole gradient is 4.5 MB: one bucket.  Larger
+      models are split into ``bucket_mb`` chunks issued back to back (xGMI is point-to-point, so one
+      ring per collective is link-bound; RCCL spreads channels over the 7 links itself).
+  C3  all-reduce of on-device metric counters / confusion matrices (validation)
+  C4  averaging of BN running statistics before evaluation / checkpointing (ranks see different data)
+  C5  barriers around rank-0 I/O
+
+Launch with one process per GPU: ``torchrun --nproc-per-node N --master-addr 127.0.0.1 ...``.  The
+same code runs on CPU with the gloo backend (tests use world_size 2).
+"""
+from __future__ import annotations
+
+import datetime
+import math
+import os
+from dataclasses import dataclass
+from typing import Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: Optional[str] = None
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    def barrier(self):
+        if self.enabled:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def all_reduce_(self, t: torch.Tensor, op=None):
+        if self.enabled:
+            dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
+        return t
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0):
+        if self.enabled:
+            dist.broadcast(t, src=src)
+        return t
+
+    def max_scalar(self, x: float) -> float:
+        if not self.enabled:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> DistContext:
+    """Initialise from torchrun's environment (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available()
+    device = torch.device(f"cuda:{local_rank}") if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    if world <= 1:
+        return DistContext(0, 1, 0, device, None)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    backend = backend or ("nccl" if use_gpu else "gloo")
+    if not dist.is_initialized():
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    return DistContext(rank, world, local_rank, device, backend)
+
+
+def shutdown(ctx: DistContext):
+    if ctx.enabled and dist.is_initialized():
+        dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------------------------
+class FlatGradAllReducer:
+    """All-reduce(SUM) of a flat gradient buffer in ``bucket_mb`` chunks (0 = one bucket)."""
+
+    def __init__(self, ctx: DistContext, bucket_mb: float = 0.0):
+        self.ctx = ctx
+        self.bucket_elems = int(bucket_mb * 2 ** 20 / 4) if bucket_mb > 0 else 0
+
+    def __call__(self, grads: torch.Tensor):
+        if not self.ctx.enabled:
+            return
+        n = grads.numel()
+        if self.bucket_elems <= 0 or n <= self.bucket_elems:
+            dist.all_reduce(grads)
+            return
+        handles = [dist.all_reduce(grads[o:o + self.bucket_elems], async_op=True)
+                   for o in range(0, n, self.bucket_elems)]
+        for h in handles:
+            h.wait()
+
+
+def broadcast_module_state(ctx: DistContext, tensors: Iterable[torch.Tensor], src: int = 0):
+    """C1: make every rank start from rank ``src``'s parameters and buffers."""
+    if not ctx.enabled:
+        return
+    for t in tensors:
+        dist.broadcast(t, src=src)
+
+
+def average_(ctx: DistContext, tensors: Iterable[torch.Tensor]):
+    """C4: average (float) tensors across ranks, e.g. BN running statistics before eval/checkpoint."""
+    if not ctx.enabled:
+        return
+    for t in tensors:
+        if t.is_floating_point():
+            dist.all_reduce(t)
+            t.div_(ctx.world)
+
+
+def sum_(ctx: DistContext, tensors: Iterable[torch.Tensor]):
+    """C3: sum metric counters / confusion matrices across ranks."""
+    if not ctx.enabled:
+        return
+    for t in tensors:
+        dist.all_reduce(t)
+
+
+# ------------------------------------------------------------------------------------------------
+class ShardedIndexSampler:
+    """Per-epoch shuffled indices, sharded across ranks (rank r takes batches r, r+W, ...).
+
+    Every rank receives the same number of full batches: the permutation is padded with a seeded random
+    draw so that no rank runs a shorter epoch (the engine's HIP graph has a fixed batch size)."""
+
+    def __init__(self, n: int, batch: int, ctx: DistContext, shuffle: bool = True, seed: int = 0,
+                 pad_random: bool = True):
+        self.n, self.batch, self.ctx, self.shuffle, self.seed = n, batch, ctx, shuffle, seed
+        self.pad_random = pad_random
+
+    def num_batches(self) -> int:
+        return math.ceil(self.n / (self.batch * self.ctx.world))
+
+    def epoch(self, epoch: int, device) -> List[torch.Tensor]:
+        g = torch.Generator().manual_seed(self.seed * 1000003 + epoch)
+        order = torch.randperm(self.n, generator=g) if self.shuffle else torch.arange(self.n)
+        per_step = self.batch * self.ctx.world
+        total = self.num_batches() * per_step
+        if total > self.n:
+            extra = torch.randint(0, self.n, (total - self.n,), generator=g) if self.pad_random else \
+                order[torch.arange(total - self.n) % self.n]
+            order = torch.cat([order, extra])
+        order = order.view(self.num_batches(), self.ctx.world, self.batch)[:, self.ctx.rank]
+        order = order.to(device)
+        return [order[i] for i in range(order.shape[0])]
