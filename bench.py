@@ -41,12 +41,14 @@ def main():
     ap.add_argument("--dataset-size", type=int, default=2048, help="synthetic samples resident per GPU")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per step")
     ap.add_argument("--bucket-mb", type=float, default=0.0)
+    ap.add_argument("--no-tune", action="store_true", help="skip per-layer kernel autotuning (cached table only)")
     args = ap.parse_args()
 
     import torch
     from mtl_das_pytorch_amd.data.synthetic import generate
     from mtl_das_pytorch_amd.engine.mtl import MTLProgram
     from mtl_das_pytorch_amd.engine.step import StepRunner
+    from mtl_das_pytorch_amd.engine.tune import autotune_program, load_cache, autotune_phases
     from mtl_das_pytorch_amd.models import build_model
     from mtl_das_pytorch_amd.parallel.dist import (FlatGradAllReducer, ShardedIndexSampler,
                                                    broadcast_module_state, init_distributed, shutdown)
@@ -60,6 +62,10 @@ def main():
     model = build_model(args.model)
     prog = MTLProgram(model, args.batch, dev)
     prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world)
+    if args.no_tune:
+        autotune_phases([], load_cache())
+    else:
+        autotune_program(prog, out_path=os.path.join("gpurun_out", "tuned_cfgs.json") if ctx.is_main else None)
     f = prog.flat
     broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
     X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev)

@@ -205,6 +205,8 @@ void grad_sum(py::list g, int64_t out, int ldo, int64_t M, int C, int64_t stream
 void adam_pack(int64_t stream, py::dict d) {
   AdamArgs a{};
   a.p = P<float>(d, "p"); a.g = P<const float>(d, "g"); a.m = P<float>(d, "m"); a.v = P<float>(d, "v");
+  a.n = I(d, "n");
+  if (a.n % 4) throw std::runtime_error("adam: flat length must be a multiple of 4");
   a.lr = P<const float>(d, "lr"); a.step = P<const float>(d, "step");
   a.b1 = (float)F(d, "b1", 0.9); a.b2 = (float)F(d, "b2", 0.999); a.eps = (float)F(d, "eps", 1e-8);
   a.wd = (float)F(d, "wd", 0.0); a.grad_scale = (float)F(d, "grad_scale", 1.0);

@@ -262,8 +262,10 @@ __global__ __launch_bounds__(256) void tail_bwd_reduce_kernel(TailArgs a) {
         store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
     }
   }
-  // block reduction over pixel lanes
+  // block reduction over pixel lanes: partials -> LDS [PL][3][C], then all 256 threads reduce
+  // (item, segment) pairs and a second short pass combines segments; one atomic per item per block.
   const int PL = L.PL;
+  const int NI = (two ? 3 : 2) * C;  // items: (statistic, channel)
   if (L.active) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -273,21 +275,28 @@ __global__ __launch_bounds__(256) void tail_bwd_reduce_kernel(TailArgs a) {
     }
   }
   __syncthreads();
+  float* s_seg = s_part + PL * 3 * C;  // [S][NI]
+  const int S = NI >= 256 ? 1 : min(PL, 256 / NI);
+  const int rows = (PL + S - 1) / S;
+  for (int q = threadIdx.x; q < NI * S; q += blockDim.x) {
+    const int item = q % NI, seg = q / NI;
+    const int k = item / C, ch = item - k * C;
+    float t = 0.f;
+    const int r0 = seg * rows, r1 = min(PL, r0 + rows);
+    for (int r = r0; r < r1; ++r) t += s_part[(r * 3 + k) * C + ch];
+    s_seg[seg * NI + item] = t;
+  }
+  __syncthreads();
   const int rep = blockIdx.x % NREP;
-  for (int ch = threadIdx.x; ch < C; ch += blockDim.x) {
-    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
-    for (int q = 0; q < PL; ++q) {
-      t0 += s_part[(q * 3 + 0) * C + ch];
-      t1 += s_part[(q * 3 + 1) * C + ch];
-      if (two) t2 += s_part[(q * 3 + 2) * C + ch];
-    }
-    float* w = a.ws + ((int64_t)z * NREP + rep) * 2 * C;
-    atomicAdd(w + ch, t0);
-    atomicAdd(w + C + ch, t1);
+  for (int item = threadIdx.x; item < NI; item += blockDim.x) {
+    float t = 0.f;
+    for (int seg = 0; seg < S; ++seg) t += s_seg[seg * NI + item];
+    const int k = item / C, ch = item - k * C;
+    if (k < 2) atomicAdd(a.ws + ((int64_t)z * NREP + rep) * 2 * C + k * C + ch, t);
     if (two) {
       float* w2 = a.ws2 + ((int64_t)z * NREP + rep) * 2 * C;
-      atomicAdd(w2 + ch, t0);
-      atomicAdd(w2 + C + ch, t2);
+      if (k == 0) atomicAdd(w2 + ch, t);
+      if (k == 2) atomicAdd(w2 + C + ch, t);
     }
   }
 }
@@ -373,7 +382,7 @@ int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t 
 int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st) {
   const int CG = a.C / 8;
   const int PL = 256 / CG;
-  size_t lds_r = (size_t)(8 * a.C + 3 * PL * a.C) * sizeof(float);
+  size_t lds_r = (size_t)(8 * a.C + 3 * PL * a.C + 3 * a.C + 256) * sizeof(float);
   size_t lds_a = (size_t)(14 * a.C) * sizeof(float);
   dim3 grid(blocks, 1, G);
   switch (kind) {

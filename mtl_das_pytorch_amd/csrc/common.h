@@ -19,7 +19,7 @@
 
 namespace mda {
 
-constexpr int NREP = 8;  // BN-statistic replicas
+constexpr int NREP = 32;  // BN-statistic replicas (atomic contention spread)
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));

@@ -38,19 +38,61 @@ DEV int encode_kg(int i, int Ktot, int Cs8, int KW, int C0) {
   return c | (kw << 14) | (kh << 21) | (seg << 28) | (1 << 29);
 }
 
-template <int MODE, int WN, int WM, int WAVES_N, int WAVES_M>
+// One wave's fragment loads for k-step `ks`: FM im2col fragments (B operand) + FN weight fragments (A).
+template <int MODE, int FN, int FM>
+DEV void conv_load_stage(const ConvArgs& a, const int* s_tab, int ks, int kgl, int l16, int n_base,
+                         const int* pb, const int* py, const int* px, const bool* pv, const bf16_t* base0,
+                         const bf16_t* base1, int ld0, int ld1, const bf16_t* wz, bf16x8* afr, bf16x8* bfr) {
+  const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int e = s_tab[ks * 4 + kgl];
+  const bool valid = (e >> 29) & 1;
+  const int seg = (e >> 28) & 1;
+  const int kh = (e >> 21) & 127, kw = (e >> 14) & 127, c = e & 16383;
+  const bf16_t* sb = seg ? base1 : base0;
+  const int sld = seg ? ld1 : ld0;
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    int ih, iw;
+    bool ok;
+    if (MODE == MODE_FWD) {
+      ih = py[f] + kh; iw = px[f] + kw;
+      ok = valid && pv[f] && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+    } else {
+      int nh = py[f] - kh, nw = px[f] - kw;
+      ok = valid && pv[f] && nh >= 0 && nw >= 0;
+      if (a.sh == 2) { ok = ok && !(nh & 1); ih = nh >> 1; } else if (a.sh == 1) { ih = nh; } else { ok = ok && (nh % a.sh == 0); ih = nh / a.sh; }
+      if (a.sw == 2) { ok = ok && !(nw & 1); iw = nw >> 1; } else if (a.sw == 1) { iw = nw; } else { ok = ok && (nw % a.sw == 0); iw = nw / a.sw; }
+      ok = ok && ih < a.Hs && iw < a.Ws;
+    }
+    bfr[f] = ok ? *reinterpret_cast<const bf16x8*>(sb + ((int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw) * sld + c) : zero8;
+  }
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int n = n_base + i * 16 + l16;
+    afr[i] = n < a.Npad ? *reinterpret_cast<const bf16x8*>(wz + (int64_t)n * a.Kpad + ks * 32 + kgl * 8) : zero8;
+  }
+}
+
+// Block = 4 waves laid out WAVES_N (channels) x WAVES_M (pixels) x KSPLIT (reduction).  Each wave walks
+// its share of K with a two-stage register pipeline (loads of step k+1 in flight during the MFMAs of
+// step k); KSPLIT > 1 partial accumulators are summed through LDS, so small-M / long-K layers (the 5x11
+// and 9x21 stages, K up to 1152) get up to 4x shorter dependency chains.
+template <int MODE, int WN, int WM, int WAVES_N, int WAVES_M, int KSPLIT>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
-  extern __shared__ int s_tab[];
+  static_assert(WAVES_N * WAVES_M * KSPLIT == 4, "4 waves per block");
   constexpr int FN = WN / 16, FM = WM / 16;
   constexpr int BN_T = WN * WAVES_N, BM_T = WM * WAVES_M;
-  const int z = blockIdx.z;
+  extern __shared__ __attribute__((aligned(16))) int s_dyn[];
+  int* s_tab = s_dyn;  // [Kpad/8]
   const int nkg = a.Kpad >> 3;
+  float* s_red = reinterpret_cast<float*>(s_dyn + ((nkg + 3) & ~3));  // KSPLIT partials, then stats
+  const int z = blockIdx.z;
   const int Ktot = a.KH * a.KW * a.Cs;
   for (int i = threadIdx.x; i < nkg; i += 256) s_tab[i] = encode_kg(i, Ktot, a.Cs >> 3, a.KW, a.src.C0);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wn = wid % WAVES_N, wm = wid / WAVES_N;
+  const int wn = wid % WAVES_N, wm = (wid / WAVES_N) % WAVES_M, wk = wid / (WAVES_N * WAVES_M);
   const int n_base = blockIdx.y * BN_T + wn * WN;
   const int m_base = blockIdx.x * BM_T + wm * WM;
   const int HWo = a.Ho * a.Wo;
@@ -81,99 +123,128 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int f = 0; f < FM; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   const int nks = a.Kpad >> 5;
-  for (int ks = 0; ks < nks; ++ks) {
-    const int e = s_tab[ks * 4 + kgl];
-    const bool valid = (e >> 29) & 1;
-    const int seg = (e >> 28) & 1;
-    const int kh = (e >> 21) & 127, kw = (e >> 14) & 127, c = e & 16383;
-    const bf16_t* sb = seg ? base1 : base0;
-    const int sld = seg ? ld1 : ld0;
-    bf16x8 bfr[FM];
+  const int kchunk = (nks + KSPLIT - 1) / KSPLIT;
+  const int kbeg = wk * kchunk, kend = min(nks, kbeg + kchunk);
+  bf16x8 a0[FN], b0[FM], a1[FN], b1[FM];
+#define LOAD_STAGE(KS, AF, BF) \
+  conv_load_stage<MODE, FN, FM>(a, s_tab, KS, kgl, l16, n_base, pb, py, px, pv, base0, base1, ld0, ld1, wz, AF, BF)
+#define MMA_STAGE(AF, BF)                                                                                 \
+  _Pragma("unroll") for (int i = 0; i < FN; ++i)                                                          \
+  _Pragma("unroll") for (int f = 0; f < FM; ++f)                                                          \
+    acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AF[i], BF[f], acc[i][f], 0, 0, 0);
+  if (kbeg < kend) LOAD_STAGE(kbeg, a0, b0);
+  for (int ks = kbeg; ks < kend; ks += 2) {
+    if (ks + 1 < kend) LOAD_STAGE(ks + 1, a1, b1);
+    MMA_STAGE(a0, b0)
+    if (ks + 2 < kend) LOAD_STAGE(ks + 2, a0, b0);
+    if (ks + 1 < kend) { MMA_STAGE(a1, b1) }
+  }
+#undef LOAD_STAGE
+#undef MMA_STAGE
+
+  constexpr int TILE = FN * FM * 4 * 64;  // floats per wave accumulator tile
+  if (KSPLIT > 1) {
+    const int slot = wn + WAVES_N * wm;
+    if (wk > 0) {
+      float* dst = s_red + ((wk - 1) * WAVES_N * WAVES_M + slot) * TILE;
 #pragma unroll
-    for (int f = 0; f < FM; ++f) {
-      int ih, iw;
-      bool ok;
-      if (MODE == MODE_FWD) {
-        ih = py[f] + kh; iw = px[f] + kw;
-        ok = valid && pv[f] && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
-      } else {
-        int nh = py[f] - kh, nw = px[f] - kw;
-        ok = valid && pv[f] && nh >= 0 && nw >= 0;
-        if (a.sh == 2) { ok = ok && !(nh & 1); ih = nh >> 1; } else if (a.sh == 1) { ih = nh; } else { ok = ok && (nh % a.sh == 0); ih = nh / a.sh; }
-        if (a.sw == 2) { ok = ok && !(nw & 1); iw = nw >> 1; } else if (a.sw == 1) { iw = nw; } else { ok = ok && (nw % a.sw == 0); iw = nw / a.sw; }
-        ok = ok && ih < a.Hs && iw < a.Ws;
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dst[((i * FM + f) * 4 + r) * 64 + lane] = acc[i][f][r];
+    }
+    __syncthreads();
+    if (wk == 0) {
+#pragma unroll
+      for (int q = 1; q < KSPLIT; ++q) {
+        const float* src = s_red + ((q - 1) * WAVES_N * WAVES_M + slot) * TILE;
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int f = 0; f < FM; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][f][r] += src[((i * FM + f) * 4 + r) * 64 + lane];
       }
-      bfr[f] = ok ? *reinterpret_cast<const bf16x8*>(sb + ((int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw) * sld + c) : zero8;
     }
-    bf16x8 afr[FN];
-#pragma unroll
-    for (int i = 0; i < FN; ++i) {
-      int n = n_base + i * 16 + l16;
-      afr[i] = n < a.Npad ? *reinterpret_cast<const bf16x8*>(wz + (int64_t)n * a.Kpad + ks * 32 + kgl * 8) : zero8;
-    }
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int f = 0; f < FM; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], bfr[f], acc[i][f], 0, 0, 0);
+    __syncthreads();  // partial tiles consumed: s_red may be reused for the statistics below
   }
 
   // ---------------------------------------------------------------- epilogue
-  const int rep = blockIdx.x % NREP;
+  // BN partial sums are reduced across the block's pixel-waves in LDS and published with ONE atomic per
+  // (channel, statistic) per block into replica blockIdx.x % NREP.
+  float* s_st = s_red;  // [WAVES_M][BN_T][2]
+  const bool want_stats = MODE == MODE_FWD && a.stats != nullptr;
+  if (wk == 0) {
 #pragma unroll
-  for (int i = 0; i < FN; ++i) {
-    const int n0 = n_base + i * 16 + 4 * kgl;
-    const bool nok = n0 < a.N;
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    if (MODE == MODE_FWD && a.bias && nok) {
+    for (int i = 0; i < FN; ++i) {
+      const int n0 = n_base + i * 16 + 4 * kgl;
+      const bool nok = n0 < a.N;
+      float bias[4] = {0.f, 0.f, 0.f, 0.f};
+      if (MODE == MODE_FWD && a.bias && nok) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bias[r] = a.bias[a.bgs * z + n0 + r];
-    }
-    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < 4; ++r) bias[r] = a.bias[a.bgs * z + n0 + r];
+      }
+      float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int f = 0; f < FM; ++f) {
-      const int m = m_base + f * 16 + l16;
-      float v[4];
+      for (int f = 0; f < FM; ++f) {
+        const int m = m_base + f * 16 + l16;
+        float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] + bias[r];
-      if (nok && pv[f]) {
-        if (MODE == MODE_FWD) {
-          bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
-          uint2 w;
-          w.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          w.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *reinterpret_cast<uint2*>(o) = w;
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] + bias[r];
+        if (nok && pv[f]) {
+          if (MODE == MODE_FWD) {
+            bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
+            uint2 w;
+            w.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+            w.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+            *reinterpret_cast<uint2*>(o) = w;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) { s[r] += v[r]; ss[r] += v[r] * v[r]; }
-        } else {
-          float* o = reinterpret_cast<float*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
-          *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+            for (int r = 0; r < 4; ++r) { s[r] += v[r]; ss[r] += v[r] * v[r]; }
+          } else {
+            float* o = reinterpret_cast<float*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
+            *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+          }
         }
       }
-    }
-    if (MODE == MODE_FWD && a.stats) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s[r] += __shfl_xor(s[r], o, 64);
-          ss[r] += __shfl_xor(ss[r], o, 64);
-        }
-      }
-      if (l16 == 0 && nok) {
-        float* st = a.stats + ((int64_t)z * NREP + rep) * 2 * a.N;
+      if (want_stats) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          atomicAdd(st + n0 + r, s[r]);
-          atomicAdd(st + a.N + n0 + r, ss[r]);
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s[r] += __shfl_xor(s[r], o, 64);
+            ss[r] += __shfl_xor(ss[r], o, 64);
+          }
         }
+        if (l16 == 0) {
+          const int cl = wn * WN + i * 16 + 4 * kgl;  // channel within the block tile
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s_st[(wm * BN_T + cl + r) * 2 + 0] = s[r];
+            s_st[(wm * BN_T + cl + r) * 2 + 1] = ss[r];
+          }
+        }
+      }
+    }
+  }
+  if (want_stats) {
+    __syncthreads();
+    const int rep = blockIdx.x % NREP;
+    for (int q = threadIdx.x; q < BN_T * 2; q += 256) {
+      const int cl = q >> 1, which = q & 1;
+      const int n = blockIdx.y * BN_T + cl;
+      if (n < a.N) {
+        float v = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < WAVES_M; ++w2) v += s_st[(w2 * BN_T + cl) * 2 + which];
+        atomicAdd(a.stats + ((int64_t)z * NREP + rep) * 2 * a.N + which * a.N + n, v);
       }
     }
   }
 }
 
-
+// ------------------------------------------------------------------------------------------------
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
@@ -189,6 +260,8 @@ DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
 }
 
 // Block: 256 threads, output tile TN (rows = cout) x TK (cols = k), MCH pixels staged per iteration.
+// Global loads of chunk c+1 are issued into registers before the MFMAs of chunk c (which read LDS), so
+// the load latency overlaps compute; one LDS image per operand, two barriers per chunk.
 template <int TN, int TK, int MCH>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   constexpr int PAD = 8;  // rows stay 16-byte aligned (ds_write_b128 staging, 8-byte tr-read addresses)
@@ -198,6 +271,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   __shared__ int s_tab[TK / 8];
   constexpr int FN = TN / 16, FK = TK / 16, NFR = FN * FK;
   constexpr int FPW = (NFR + 3) / 4;  // fragments per wave
+  constexpr int VY = MCH * (TN / 8), VX = MCH * (TK / 8);
+  constexpr int NY = (VY + 255) / 256, NX = (VX + 255) / 256;
 
   const int z = blockIdx.z;
   const int split = blockIdx.y;
@@ -221,37 +296,64 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   for (int j = 0; j < FPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
 
-  for (int mc = mbeg; mc < mend; mc += MCH) {
-    // stage dy tile [MCH][TN]
-    constexpr int VY = MCH * (TN / 8);
-    for (int v = threadIdx.x; v < VY; v += 256) {
-      int p = v / (TN / 8), cg = v - p * (TN / 8);
-      int m = mc + p, n = n0 + cg * 8;
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (m < mend && n < a.Co) val = *reinterpret_cast<const uint4*>(dyz + (int64_t)m * a.ldd + n);
-      *reinterpret_cast<uint4*>(&s_dy[p * LDY + cg * 8]) = val;
+  uint4 ry[NY], rx[NX];
+  auto load_chunk = [&](int mc) {
+#pragma unroll
+    for (int i = 0; i < NY; ++i) {
+      const int v = threadIdx.x + 256 * i;
+      ry[i] = make_uint4(0, 0, 0, 0);
+      if (v < VY) {
+        const int p = v / (TN / 8), cg = v - p * (TN / 8);
+        const int m = mc + p, n = n0 + cg * 8;
+        if (m < mend && n < a.Co) ry[i] = *reinterpret_cast<const uint4*>(dyz + (int64_t)m * a.ldd + n);
+      }
     }
-    // stage im2col tile [MCH][TK]
-    constexpr int VX = MCH * (TK / 8);
-    for (int v = threadIdx.x; v < VX; v += 256) {
-      int p = v / (TK / 8), g = v - p * (TK / 8);
-      int m = mc + p;
-      int e = s_tab[g];
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (m < mend && ((e >> 29) & 1)) {
-        int b = m / HWo, r = m - b * HWo;
-        int oh = r / a.Wo, ow = r - oh * a.Wo;
-        int ih = oh * a.sh - a.ph + ((e >> 21) & 127);
-        int iw = ow * a.sw - a.pw + ((e >> 14) & 127);
-        if (ih >= 0 && ih < a.Hi && iw >= 0 && iw < a.Wi) {
-          int seg = (e >> 28) & 1;
-          const bf16_t* sb = seg ? base1 : base0;
-          val = *reinterpret_cast<const uint4*>(sb + ((int64_t)(b * a.Hi + ih) * a.Wi + iw) * a.src.ld[seg] + (e & 16383));
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int v = threadIdx.x + 256 * i;
+      rx[i] = make_uint4(0, 0, 0, 0);
+      if (v < VX) {
+        const int p = v / (TK / 8), g = v - p * (TK / 8);
+        const int m = mc + p;
+        const int e = s_tab[g];
+        if (m < mend && ((e >> 29) & 1)) {
+          const int b = m / HWo, r = m - b * HWo;
+          const int oh = r / a.Wo, ow = r - oh * a.Wo;
+          const int ih = oh * a.sh - a.ph + ((e >> 21) & 127);
+          const int iw = ow * a.sw - a.pw + ((e >> 14) & 127);
+          if (ih >= 0 && ih < a.Hi && iw >= 0 && iw < a.Wi) {
+            const int seg = (e >> 28) & 1;
+            const bf16_t* sb = seg ? base1 : base0;
+            rx[i] = *reinterpret_cast<const uint4*>(sb + ((int64_t)(b * a.Hi + ih) * a.Wi + iw) * a.src.ld[seg] + (e & 16383));
+          }
         }
       }
-      *reinterpret_cast<uint4*>(&s_x[p * LDX + g * 8]) = val;
     }
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int i = 0; i < NY; ++i) {
+      const int v = threadIdx.x + 256 * i;
+      if (v < VY) {
+        const int p = v / (TN / 8), cg = v - p * (TN / 8);
+        *reinterpret_cast<uint4*>(&s_dy[p * LDY + cg * 8]) = ry[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int v = threadIdx.x + 256 * i;
+      if (v < VX) {
+        const int p = v / (TK / 8), g = v - p * (TK / 8);
+        *reinterpret_cast<uint4*>(&s_x[p * LDX + g * 8]) = rx[i];
+      }
+    }
+  };
+
+  if (mbeg < mend) load_chunk(mbeg);
+  for (int mc = mbeg; mc < mend; mc += MCH) {
+    store_chunk();
     __syncthreads();
+    if (mc + MCH < mend) load_chunk(mc + MCH);  // in flight during this chunk's MFMAs
 #pragma unroll
     for (int kk = 0; kk < MCH / 32; ++kk) {
       const int prow = kk * 32 + 8 * (lane >> 4);
@@ -283,21 +385,25 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
-
+// Sums the split-M partial slabs of many convolutions into the flat fp32 gradient buffer (deterministic,
+// one launch per backward), reference weight layout [Cout][Cin][KH][KW].
 __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale) {
   int lo = 0, hi = nd - 1;  // last descriptor with block0 <= blockIdx.x
   while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (descs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
   const WgFinDesc& D = descs[lo];
-  int64_t e = ((int64_t)blockIdx.x - D.block0) * 256 + threadIdx.x;
+  // threads walk the slab in its own (k-fastest) order so the split reads are coalesced; the single
+  // write per weight is scattered into the NCHW layout.
+  const int Kt = D.KH * D.KW * D.Cs;
+  const int64_t e = ((int64_t)blockIdx.x - D.block0) * 256 + threadIdx.x;
   if (e >= D.elems) return;
-  const int64_t per = (int64_t)D.Co * D.Ci * D.KH * D.KW;
-  int g = (int)(e / per);
+  const int64_t per = (int64_t)D.Co * Kt;
+  const int g = (int)(e / per);
   int64_t r = e - g * per;
-  int kw = r % D.KW; r /= D.KW;
-  int kh = r % D.KH; r /= D.KH;
-  int ci = r % D.Ci;
-  int co = (int)(r / D.Ci);
-  int k = (kh * D.KW + kw) * D.Cs + ci;
+  const int co = (int)(r / Kt);
+  const int k = (int)(r - (int64_t)co * Kt);
+  const int ci = k % D.Cs, tap = k / D.Cs;
+  if (ci >= D.Ci) return;
+  const int kh = tap / D.KW, kw = tap - kh * D.KW;
   const float* s = D.slab + (((int64_t)g * D.splits) * D.Npad + co) * D.Kpad + k;
   const int64_t sstride = (int64_t)D.Npad * D.Kpad;
   float acc = 0.f;
@@ -311,19 +417,32 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
 template <int MODE>
 static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
   const int M = a.B * a.Ho * a.Wo;
-  const size_t lds = (size_t)(a.Kpad / 8) * sizeof(int);
-#define LAUNCH_CFG(WN, WM, WAN, WAM)                                                               \
-  {                                                                                                \
-    dim3 grid((M + WM * WAM - 1) / (WM * WAM), (a.N + WN * WAN - 1) / (WN * WAN), G);               \
-    hipLaunchKernelGGL((conv_igemm_kernel<MODE, WN, WM, WAN, WAM>), grid, dim3(256), lds, st, a);  \
-    break;                                                                                         \
+  const int nkg4 = ((a.Kpad / 8) + 3) & ~3;
+#define LAUNCH_CFG(WN, WM, WAN, WAM, KS)                                                                \
+  {                                                                                                     \
+    constexpr int TILE = (WN / 16) * (WM / 16) * 4 * 64;                                                \
+    size_t red = (size_t)(KS - 1) * WAN * WAM * TILE;                                                   \
+    size_t st2 = (size_t)WAM * WN * WAN * 2;                                                            \
+    size_t lds = (size_t)nkg4 * 4 + (red > st2 ? red : st2) * 4;                                        \
+    dim3 grid((M + WM * WAM - 1) / (WM * WAM), (a.N + WN * WAN - 1) / (WN * WAN), G);                    \
+    hipLaunchKernelGGL((conv_igemm_kernel<MODE, WN, WM, WAN, WAM, KS>), grid, dim3(256), lds, st, a);   \
+    break;                                                                                              \
   }
   switch (cfg) {
-    case 0: LAUNCH_CFG(16, 64, 1, 4)   // N <= 16
-    case 1: LAUNCH_CFG(32, 32, 1, 4)   // N <= 32
-    case 2: LAUNCH_CFG(32, 32, 2, 2)   // N <= 64
-    case 3: LAUNCH_CFG(64, 32, 2, 2)   // N <= 128 and wide layers
-    case 4: LAUNCH_CFG(32, 16, 2, 2)   // small-M layers: more blocks
+    case 0: LAUNCH_CFG(16, 64, 1, 4, 1)
+    case 1: LAUNCH_CFG(32, 32, 1, 4, 1)
+    case 2: LAUNCH_CFG(32, 32, 2, 2, 1)
+    case 3: LAUNCH_CFG(64, 32, 2, 2, 1)
+    case 4: LAUNCH_CFG(32, 16, 2, 2, 1)
+    case 5: LAUNCH_CFG(16, 32, 1, 2, 2)
+    case 6: LAUNCH_CFG(32, 16, 1, 2, 2)
+    case 7: LAUNCH_CFG(32, 16, 2, 1, 2)
+    case 8: LAUNCH_CFG(32, 16, 1, 1, 4)
+    case 9: LAUNCH_CFG(64, 16, 1, 1, 4)
+    case 10: LAUNCH_CFG(16, 16, 1, 1, 4)
+    case 11: LAUNCH_CFG(64, 32, 1, 1, 4)
+    case 12: LAUNCH_CFG(16, 32, 1, 4, 1)
+    case 13: LAUNCH_CFG(16, 16, 1, 4, 1)
     default: return -1;
   }
 #undef LAUNCH_CFG
@@ -348,6 +467,10 @@ int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st) {
     case 1: LAUNCH_WG(32, 32, 128)
     case 2: LAUNCH_WG(32, 64, 64)
     case 3: LAUNCH_WG(64, 64, 64)
+    case 4: LAUNCH_WG(16, 64, 128)
+    case 5: LAUNCH_WG(16, 32, 256)
+    case 6: LAUNCH_WG(32, 32, 256)
+    case 7: LAUNCH_WG(64, 32, 64)
     default: return -1;
   }
 #undef LAUNCH_WG

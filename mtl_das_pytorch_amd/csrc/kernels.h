@@ -111,7 +111,7 @@ struct PoolArgs {
 
 struct OptSeg {
   int64_t off, n;
-  int kind;  // 0 = plain tensor, 1 = conv weight (write packed images)
+  int kind;  // 1 = forward image of a conv weight, 2 = data-gradient image (pack_kernel)
   bf16_t* wf;
   bf16_t* wd;
   int Co, Ci, KH, KW, Cs, Kpad_f, Kpad_d;
@@ -120,6 +120,7 @@ struct OptSeg {
 
 struct AdamArgs {
   float* p; const float* g; float* m; float* v;
+  int64_t n;  // flat buffer length (multiple of 4)
   const float* lr; const float* step;  // device scalars (step = number of completed steps)
   float b1, b2, eps, wd, grad_scale;
   int update;  // 0: pack only

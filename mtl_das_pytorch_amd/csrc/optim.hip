@@ -19,59 +19,85 @@ namespace mda {
 
 
 
-constexpr int ADAM_EPT = 4;  // elements per thread
-
-__global__ __launch_bounds__(256) void adam_pack_kernel(AdamArgs a, const OptSeg* __restrict__ segs, int ns) {
-  int lo = 0, hi = ns - 1;  // last segment with block0 <= blockIdx.x
-  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (segs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
-  const OptSeg S = segs[lo];
-  float lr = 0.f, c1 = 0.f, c2 = 0.f;
-  if (a.update) {
-    const float t = a.step[0] + 1.f;
-    lr = a.lr[0];
-    c1 = lr / (1.f - powf(a.b1, t));
-    c2 = 1.f / sqrtf(1.f - powf(a.b2, t));
-  }
-  const int64_t base = ((int64_t)blockIdx.x - S.block0) * 256 * ADAM_EPT;
+// Elementwise Adam over the whole flat buffer (padding slots hold p = g = 0 and stay 0).
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, int64_t n) {
+  const float t = a.step[0] + 1.f;
+  const float lr = a.lr[0];
+  const float c1 = lr / (1.f - powf(a.b1, t));
+  const float c2 = 1.f / sqrtf(1.f - powf(a.b2, t));
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 p = reinterpret_cast<float4*>(a.p)[i];
+    const float4 g = reinterpret_cast<const float4*>(a.g)[i];
+    float4 m = reinterpret_cast<float4*>(a.m)[i];
+    float4 v = reinterpret_cast<float4*>(a.v)[i];
+    float* pp = &p.x; const float* gg = &g.x; float* mm = &m.x; float* vv = &v.x;
 #pragma unroll
-  for (int k = 0; k < ADAM_EPT; ++k) {
-    const int64_t e = base + k * 256 + threadIdx.x;
-    if (e >= S.n) break;
-    const int64_t i = S.off + e;
-    float p = a.p[i];
-    if (a.update) {
-      const float g = a.g[i] * a.grad_scale + a.wd * p;
-      const float m = a.b1 * a.m[i] + (1.f - a.b1) * g;
-      const float v = a.b2 * a.v[i] + (1.f - a.b2) * g * g;
-      a.m[i] = m;
-      a.v[i] = v;
-      p -= c1 * m / (sqrtf(v) * c2 + a.eps);
-      a.p[i] = p;
+    for (int j = 0; j < 4; ++j) {
+      const float gj = gg[j] * a.grad_scale + a.wd * pp[j];
+      mm[j] = a.b1 * mm[j] + (1.f - a.b1) * gj;
+      vv[j] = a.b2 * vv[j] + (1.f - a.b2) * gj * gj;
+      pp[j] -= c1 * mm[j] / (sqrtf(vv[j]) * c2 + a.eps);
     }
-    if (S.kind == 1) {
-      int64_t r = e;
-      const int kw = r % S.KW; r /= S.KW;
-      const int kh = r % S.KH; r /= S.KH;
-      const int ci = r % S.Ci;
-      const int co = (int)(r / S.Ci);
-      const int tap = kh * S.KW + kw;
-      const bf16_t pb = f2bf(p);
-      S.wf[(int64_t)co * S.Kpad_f + tap * S.Cs + ci] = pb;
-      S.wd[(int64_t)ci * S.Kpad_d + tap * S.Co + co] = pb;
-    }
+    reinterpret_cast<float4*>(a.p)[i] = p;
+    reinterpret_cast<float4*>(a.m)[i] = m;
+    reinterpret_cast<float4*>(a.v)[i] = v;
   }
 }
 
-__global__ void step_inc_kernel(float* step, int64_t* extra) {
-  step[0] += 1.f;
-  if (extra) extra[0] += 1;
+// Writes the packed bf16 MFMA images of every conv weight, one thread per 8 packed elements (16-B
+// stores, coalesced); padding is (re)written as zeros.  Segment `kind` selects the image:
+// 1 = forward [Co][(kh,kw,ci)] (rows Npad, cols Kpad_f), 2 = data-gradient [Ci][(kh,kw,co)].
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, const OptSeg* __restrict__ segs, int ns) {
+  int lo = 0, hi = ns - 1;
+  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (segs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
+  const OptSeg& S = segs[lo];
+  const int64_t e8 = ((int64_t)blockIdx.x - S.block0) * 256 + threadIdx.x;  // index of an 8-element chunk
+  const int K = S.kind == 1 ? S.Kpad_f : S.Kpad_d;
+  const int64_t total8 = S.n / 8;  // S.n = rows * K (multiple of 8)
+  if (e8 >= total8) return;
+  const int64_t e = e8 * 8;
+  const int row = (int)(e / K);
+  const int k0 = (int)(e - (int64_t)row * K);
+  const float* W = P + S.off;
+  const int taps = S.KH * S.KW;
+  uint32_t w4[4];
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    float v[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = k0 + j + h;
+      float x = 0.f;
+      if (S.kind == 1) {  // row = co, k = tap*Cs + ci
+        const int ci = k % S.Cs, tap = k / S.Cs;
+        if (row < S.Co && tap < taps && ci < S.Ci) x = W[((int64_t)row * S.Ci + ci) * taps + tap];
+      } else {            // row = ci, k = tap*Co + co
+        const int co = k % S.Co, tap = k / S.Co;
+        if (row < S.Ci && tap < taps) x = W[((int64_t)co * S.Ci + row) * taps + tap];
+      }
+      v[h] = x;
+    }
+    w4[j / 2] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  }
+  bf16_t* dst = (S.kind == 1 ? S.wf : S.wd) + e;
+  *reinterpret_cast<uint4*>(dst) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
 }
+
+__global__ void step_inc_kernel(float* step) { step[0] += 1.f; }
 
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st) {
-  hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, a, d_segs, ns);
+  if (a.update) {
+    const int64_t n4 = a.n >> 2;
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, st, a, a.n);
+    int rc = (int)hipGetLastError();
+    if (rc) return rc;
+  }
+  if (nblocks > 0) hipLaunchKernelGGL(pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, (const float*)a.p, d_segs, ns);
   int rc = (int)hipGetLastError();
   if (rc || !a.update) return rc;
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, const_cast<float*>(a.step), (int64_t*)nullptr);
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, const_cast<float*>(a.step));
   return (int)hipGetLastError();
 }
 

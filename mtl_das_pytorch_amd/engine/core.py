@@ -23,9 +23,10 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from ..ops.functional import WGRAD_TILES, wgrad_cfg
 from ..ops.hip import lib, ptr
 
-NREP = 8  # must match csrc/common.h
+NREP = 32  # must match csrc/common.h
 
 
 def pad_to(x: int, m: int) -> int:
@@ -321,22 +322,26 @@ class ConvLayer:
         self.Kpad_d = pad_to(taps * self.Co, 32)
         self.wf = arena.zeros((self.G, self.Npad, self.Kpad))
         self.wd = arena.zeros((self.G, self.Npad_d, self.Kpad_d))
-        # weight-gradient decomposition
+        # weight-gradient decomposition (tile config chosen by the autotuner; the slab is sized for the
+        # largest split count any config can ask for)
         self.Kpad_w = pad_to(taps * self.Cs, 64)
-        self.wcfg, TN, TK, MCH = self._wgrad_cfg()
-        tiles = math.ceil(self.Npad / TN) * (self.Kpad_w // TK) * self.G
-        max_splits = max(1, math.ceil(self.M_out / MCH))
-        splits = max(1, min(max_splits, math.ceil(512 / tiles)))
-        self.m_per_split = pad_to(math.ceil(self.M_out / splits), MCH)
-        self.splits = math.ceil(self.M_out / self.m_per_split)
-        self.slab = arena.empty((self.G, self.splits, self.Npad, self.Kpad_w), torch.float32)
+        self._wgrad_args = None
+        max_splits = max(self.wgrad_plan(c)[0] for c in WGRAD_TILES)
+        self.slab = arena.empty((self.G, max_splits, self.Npad, self.Kpad_w), torch.float32)
+        self.set_wgrad_cfg(wgrad_cfg(self.Co, self.Kpad_w))
 
-    def _wgrad_cfg(self):
-        if self.Co <= 16:
-            return 0, 16, 32, 128
-        if self.Co <= 32:
-            return (1, 32, 32, 128) if self.Kpad_w <= 64 else (2, 32, 64, 64)
-        return 3, 64, 64, 64
+    def wgrad_plan(self, cfg: int):
+        TN, TK, MCH = WGRAD_TILES[cfg]
+        tiles = math.ceil(self.Npad / TN) * (self.Kpad_w // TK) * self.G
+        splits = max(1, min(math.ceil(self.M_out / MCH), math.ceil(512 / tiles)))
+        mps = pad_to(math.ceil(self.M_out / splits), MCH)
+        return math.ceil(self.M_out / mps), mps
+
+    def set_wgrad_cfg(self, cfg: int):
+        self.wcfg = cfg
+        self.splits, self.m_per_split = self.wgrad_plan(cfg)
+        if self._wgrad_args is not None:
+            self._wgrad_args.update(splits=self.splits, m_per_split=self.m_per_split)
 
     def fwd_cfg(self, N: int, M: int) -> int:
         if N <= 16:
@@ -349,12 +354,15 @@ class ConvLayer:
 
     # ---- packed weight images / optimizer descriptors ------------------------------------------
     def opt_segments(self) -> List[dict]:
+        """Pack jobs (csrc/optim.hip pack_kernel): the forward and data-gradient bf16 images of every
+        group member, rebuilt from the fp32 masters after each optimizer step."""
         segs = []
         for g, m in enumerate(self.mods):
-            segs.append({"off": self.flat.off(m.weight), "n": m.weight.numel(), "kind": 1,
-                         "wf": P(self.wf, g * self.Npad * self.Kpad), "wd": P(self.wd, g * self.Npad_d * self.Kpad_d),
-                         "Co": self.Co, "Ci": self.Ci, "KH": self.KH, "KW": self.KW, "Cs": self.Cs,
-                         "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d})
+            common = {"off": self.flat.off(m.weight), "Co": self.Co, "Ci": self.Ci, "KH": self.KH, "KW": self.KW,
+                      "Cs": self.Cs, "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d}
+            segs.append(dict(common, kind=1, n=self.Npad * self.Kpad, wf=P(self.wf, g * self.Npad * self.Kpad)))
+            segs.append(dict(common, kind=2, n=self.Npad_d * self.Kpad_d,
+                             wd=P(self.wd, g * self.Npad_d * self.Kpad_d)))
         return segs
 
     def finalize_desc(self) -> dict:
@@ -362,7 +370,7 @@ class ConvLayer:
         return {"slab": P(self.slab), "grad": P(self.flat.grads, self.flat.off(m0.weight)), "ggs": self.wstride,
                 "G": self.G, "splits": self.splits, "Npad": self.Npad, "Kpad": self.Kpad_w, "Co": self.Co,
                 "Ci": self.Ci, "Cs": self.Cs, "KH": self.KH, "KW": self.KW,
-                "elems": self.G * m0.weight.numel()}
+                "elems": self.G * self.Co * self.KH * self.KW * self.Cs}
 
     # ---- launches --------------------------------------------------------------------------------
     def fwd_args(self, src: dict, out: Act, bn: Optional[BNLayer], training: bool) -> tuple:
@@ -385,7 +393,7 @@ class ConvLayer:
         return (1, self.fwd_cfg(self.Cs, self.M_in), self.G, d)
 
     def wgrad_args(self, src: dict, dy: Act) -> tuple:
-        d = {"src": src, "dy": dy.p, "dgs": dy.gs, "ldd": dy.ld, "slab": P(self.slab), "splits": self.splits,
+        self._wgrad_args = d = {"src": src, "dy": dy.p, "dgs": dy.gs, "ldd": dy.ld, "slab": P(self.slab), "splits": self.splits,
              "m_per_split": self.m_per_split, "B": self.B, "Hi": self.Hi, "Wi": self.Wi, "Ho": self.Ho, "Wo": self.Wo,
              "Co": self.Co, "Npad": self.Npad, "Cs": self.Cs, "KH": self.KH, "KW": self.KW, "sh": self.sh,
              "sw": self.sw, "ph": self.ph, "pw": self.pw, "Kpad": self.Kpad_w}
@@ -416,13 +424,12 @@ def build_optseg_table(segs: List[dict], device) -> tuple:
                    ("Co", "<i4"), ("Ci", "<i4"), ("KH", "<i4"), ("KW", "<i4"), ("Cs", "<i4"), ("Kpad_f", "<i4"),
                    ("Kpad_d", "<i4"), ("_pad1", "<i4"), ("block0", "<i8")])
     assert dt.itemsize == lib().SIZEOF_OPTSEG, (dt.itemsize, lib().SIZEOF_OPTSEG)
-    segs = sorted(segs, key=lambda s: s["off"])
     arr = np.zeros(len(segs), dtype=dt)
     b0 = 0
     for i, s in enumerate(segs):
         for k, v in s.items():
             arr[i][k] = v
         arr[i]["block0"] = b0
-        b0 += math.ceil(s["n"] / 1024)
+        b0 += math.ceil(s["n"] / 2048)  # 256 threads x 8 packed elements
     t = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
     return t, len(segs), b0

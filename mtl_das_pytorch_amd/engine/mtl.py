@@ -198,14 +198,14 @@ class MTLProgram:
 
     def _conv_fwd(self, ph: Phase, c: ConvLayer, src: dict, out: Act, bn: BNLayer, training: bool):
         mode, cfg, G, d = c.fwd_args(src, out, bn, training)
-        ph.add("conv_fwd", k_conv, mode, cfg, G, d)
+        ph.add("conv_fwd", k_conv, mode, cfg, G, d, owner=c)
 
     def _conv_bwd(self, ph: Phase, c: ConvLayer, src: dict, dy: Act, dx: Optional[Act]):
         cfg, G, d = c.wgrad_args(src, dy)
-        ph.add("conv_wgrad", k_wgrad, cfg, G, d)
+        ph.add("conv_wgrad", k_wgrad, cfg, G, d, owner=c)
         if dx is not None:
             mode, cfg, G, d = c.dgrad_args(dy, dx)
-            ph.add("conv_dgrad", k_conv, mode, cfg, G, d)
+            ph.add("conv_dgrad", k_conv, mode, cfg, G, d, owner=c)
 
     def _emit(self):
         self.fwd_train = self._emit_forward(True)
@@ -310,24 +310,25 @@ class MTLProgram:
         self._tail_bwd(ph, ACT_RELU, 1, self.y0, self.bn1, sources(0), self.dy0)
         self._conv_bwd(ph, self.conv1, src_dict(self.xin), self.dy0, None)
         # weight-gradient slabs -> flat fp32 gradients (one launch for every conv)
-        self.wgfin_table, nd, nblocks = build_wgfin_table([c.finalize_desc() for c in self.convs], self.device)
-        ph.add("wgrad_finalize", k_wgfin, self.wgfin_table, nd, nblocks)
+        ph.add("wgrad_finalize", k_wgfin, *self._wgfin_args())
         return ph
 
+    def _wgfin_args(self):
+        self.wgfin_table, nd, nblocks = build_wgfin_table([c.finalize_desc() for c in self.convs], self.device)
+        return self.wgfin_table, nd, nblocks
+
+    def refresh_wgrad_finalize(self):
+        """Rebuild the finalize descriptor table after wgrad configs (split counts) changed."""
+        for l in self.bwd.launches:
+            if l.name == "wgrad_finalize":
+                l.args = self._wgfin_args()
+
     def _emit_optimizer(self, grad_scale: float = 1.0) -> Dict[str, Phase]:
-        segs = []
-        conv_w = set()
-        for c in self.convs:
-            for s in c.opt_segments():
-                segs.append(s)
-            conv_w.update(id(m.weight) for m in c.mods)
-        for p in self.flat.order:
-            if id(p) not in conv_w:
-                segs.append({"off": self.flat.off(p), "n": p.numel(), "kind": 0})
+        segs = [s for c in self.convs for s in c.opt_segments()]
         self.optseg_table, ns, nblocks = build_optseg_table(segs, self.device)
         f = self.flat
-        base = {"p": P(f.params), "g": P(f.grads), "m": P(f.exp_avg), "v": P(f.exp_avg_sq), "lr": P(f.lr),
-                "step": P(f.step), "segs": P(self.optseg_table), "nsegs": ns, "nblocks": nblocks}
+        base = {"p": P(f.params), "g": P(f.grads), "m": P(f.exp_avg), "v": P(f.exp_avg_sq), "n": f.numel,
+                "lr": P(f.lr), "step": P(f.step), "segs": P(self.optseg_table), "nsegs": ns, "nblocks": nblocks}
         self._opt_base = base
         upd = Phase("adam")
         upd.add("adam_pack", k_adam, dict(base, update=1, b1=0.9, b2=0.999, eps=1e-8, wd=0.0, grad_scale=grad_scale))

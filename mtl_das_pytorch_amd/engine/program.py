@@ -11,12 +11,13 @@ from ..ops.hip import lib, stream
 
 
 class Launch:
-    __slots__ = ("name", "fn", "args")
+    __slots__ = ("name", "fn", "args", "owner")
 
-    def __init__(self, name: str, fn: Callable, *args):
+    def __init__(self, name: str, fn: Callable, *args, owner=None):
         self.name = name
         self.fn = fn
         self.args = args
+        self.owner = owner  # the layer object that emitted it (used by the autotuner)
 
     def __call__(self, st: int):
         self.fn(*self.args, st)
@@ -27,8 +28,8 @@ class Phase:
         self.name = name
         self.launches: List[Launch] = []
 
-    def add(self, name, fn, *args):
-        self.launches.append(Launch(name, fn, *args))
+    def add(self, name, fn, *args, owner=None):
+        self.launches.append(Launch(name, fn, *args, owner=owner))
 
     def run(self, st=None):
         st = stream() if st is None else st

@@ -92,6 +92,7 @@ class StepRunner:
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
             snap.restore()
+            self.p.opt["pack"].run()  # the bf16 weight images are derived state: rebuild from restored masters
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 for f in fns:

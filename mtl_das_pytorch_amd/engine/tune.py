@@ -1,0 +1,116 @@
+"""Per-layer kernel autotuning on the device.
+
+Every conv forward / data-gradient launch of a lowered program has 14 tile configurations
+(csrc/conv.hip ``launch_conv_cfg``: wave layout channels x pixels x K-split).  The best one depends on
+the layer's M (B*H*W), N (channels) and K (taps*Cin) and on MI355X's CU count, so it is *measured*:
+each candidate is timed from a HIP graph of back-to-back launches (no host overhead), the fastest is
+written into the launch, and the result is cached by shape signature in ``tuned_cfgs.json`` (shipped in
+the package, so normal runs do not pay the tuning time).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, Iterable, Optional
+
+import torch
+
+from ..ops.hip import lib
+
+CONV_CFGS = list(range(14))
+WGRAD_CFGS = list(range(8))
+_CACHE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_cfgs.json")
+
+
+def conv_signature(mode: int, G: int, d: dict) -> str:
+    keys = ("B", "Hs", "Ws", "Ho", "Wo", "N", "Cs", "KH", "KW", "sh", "sw", "ph", "pw")
+    src = d["src"]
+    return f"conv{mode}|G{G}|" + ",".join(str(d[k]) for k in keys) + f"|seg{int(src.get('C1', 0) > 0)}" + \
+           f"|st{int(bool(d.get('stats')))}"
+
+
+def load_cache(path: str = _CACHE_PATH) -> Dict[str, int]:
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def save_cache(cache: Dict[str, int], path: str):
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        json.dump(dict(sorted(cache.items())), f, indent=0)
+
+
+def _time(fn, inner: int = 10, reps: int = 5) -> float:
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(inner):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        g.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / (inner * reps)
+
+
+def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, verbose: bool = False) -> Dict[str, int]:
+    """Choose the conv tile config of every conv launch in ``phases`` (mutates the launches)."""
+    cache = load_cache() if cache is None else cache
+    L = lib()
+    for ph in phases:
+        for launch in ph.launches:
+            if launch.name not in ("conv_fwd", "conv_dgrad"):
+                continue
+            mode, cfg, G, d = launch.args
+            sig = conv_signature(mode, G, d)
+            if sig not in cache:
+                best, best_t = cfg, float("inf")
+                for c in CONV_CFGS:
+                    t = _time(lambda: L.conv(mode, c, G, torch.cuda.current_stream().cuda_stream, d))
+                    if t < best_t:
+                        best, best_t = c, t
+                cache[sig] = best
+                if verbose:
+                    print(f"tuned {sig}: cfg {best} ({best_t * 1e3:.1f} us)", flush=True)
+            launch.args = (mode, cache[sig], G, d)
+    for ph in phases:
+        for launch in ph.launches:
+            if launch.name != "conv_wgrad" or launch.owner is None:
+                continue
+            cfg, G, d = launch.args
+            conv = launch.owner
+            sig = "wgrad|" + conv_signature(0, G, dict(d, N=d["Co"], Hs=d["Hi"], Ws=d["Wi"], stats=0))
+            if sig not in cache:
+                best, best_t = cfg, float("inf")
+                for c in WGRAD_CFGS:
+                    conv.set_wgrad_cfg(c)
+                    t = _time(lambda: L.wgrad(c, G, torch.cuda.current_stream().cuda_stream, d))
+                    if t < best_t:
+                        best, best_t = c, t
+                cache[sig] = best
+                if verbose:
+                    print(f"tuned {sig}: cfg {best} ({best_t * 1e3:.1f} us)", flush=True)
+            conv.set_wgrad_cfg(cache[sig])
+            launch.args = (cache[sig], G, d)
+    return cache
+
+
+def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False) -> Dict[str, int]:
+    """Tune every conv launch of a lowered program (train forward, eval forward, backward)."""
+    if prog.device.type != "cuda":
+        return {}
+    cache = load_cache()
+    n0 = len(cache)
+    autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose)
+    prog.refresh_wgrad_finalize()
+    if out_path and len(cache) != n0:
+        save_cache(cache, out_path)
+    return cache

@@ -15,7 +15,7 @@ import torch.nn.functional as F
 
 from .hip import lib, ptr, stream
 
-NREP = 8
+NREP = 32  # must match csrc/common.h
 
 
 def _pad(x, m):
@@ -71,11 +71,27 @@ def _fwd_cfg(N, M):
     return 3 if M >= 64 * 128 else 4
 
 
-def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0,
-           stats: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
-    """NHWC bf16 convolution.  ``x2`` (optional) is a second input whose channels are concatenated after
-    ``x``'s (the kernel reads both without materialising the concat).  ``stats`` ([NREP, 2, Co] fp32,
-    zero-initialised by the caller) receives per-channel sums of the output and its square."""
+class ConvCall:
+    """A prepared convolution launch (packed weights + argument dict); ``run()`` enqueues it again."""
+
+    def __init__(self, mode, cfg, d, out, keep):
+        self.mode, self.cfg, self.d, self.out, self._keep = mode, cfg, d, out, keep
+
+    def run(self):
+        lib().conv(self.mode, self.cfg, 1, stream(), self.d)
+        return self.out
+
+
+class WgradCall:
+    def __init__(self, cfg, d, slab, post, keep):
+        self.cfg, self.d, self.slab, self.post, self._keep = cfg, d, slab, post, keep
+
+    def run(self):
+        lib().wgrad(self.cfg, 1, stream(), self.d)
+        return self.post(self.slab)
+
+
+def prepare_conv2d(x, w, bias=None, stride=1, padding=0, stats=None, x2=None, cfg=None) -> ConvCall:
     _check(x, torch.bfloat16)
     C1 = x2.shape[-1] if x2 is not None else 0
     Cs = x.shape[-1] + C1
@@ -91,13 +107,18 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     d = {"src": src, "w": ptr(wf), "bias": ptr(bias) if bias is not None else 0, "out": ptr(y), "ldo": Co,
          "stats": ptr(stats) if stats is not None else 0, "B": B, "Hs": H, "Ws": W, "Ho": Ho, "Wo": Wo, "N": Co,
          "Npad": wf.shape[0], "Cs": Cs, "KH": KH, "KW": KW, "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": wf.shape[1]}
-    lib().conv(0, _fwd_cfg(Co, B * Ho * Wo) if cfg is None else cfg, 1, stream(), d)
-    return y
+    return ConvCall(0, _fwd_cfg(Co, B * Ho * Wo) if cfg is None else cfg, d, y, (x, x2, wf, bias, stats))
 
 
-def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw: Tuple[int, int], stride=1, padding=0,
-                 cin_stored: Optional[int] = None, cfg: Optional[int] = None):
-    """Gradient w.r.t. the NHWC input: fp32 ``[B, H, W, Cin_stored]``."""
+def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0,
+           stats: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
+    """NHWC bf16 convolution.  ``x2`` (optional) is a second input whose channels are concatenated after
+    ``x``'s (the kernel reads both without materialising the concat).  ``stats`` ([NREP, 2, Co] fp32,
+    zero-initialised by the caller) receives per-channel sums of the output and its square."""
+    return prepare_conv2d(x, w, bias, stride, padding, stats, x2, cfg).run()
+
+
+def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg=None) -> ConvCall:
     _check(dy, torch.bfloat16)
     B, Ho, Wo, Co = dy.shape
     _, Ci, KH, KW = w.shape
@@ -110,13 +131,24 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw: Tuple[int, int], stri
     d = {"src": {"p0": ptr(dy), "ld0": Co, "C0": Co, "C1": 0}, "w": ptr(wd), "out": ptr(dx), "ldo": Cs,
          "B": B, "Hs": Ho, "Ws": Wo, "Ho": H, "Wo": W, "N": Cs, "Npad": wd.shape[0], "Cs": Co, "KH": KH, "KW": KW,
          "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": wd.shape[1]}
-    lib().conv(1, _fwd_cfg(Cs, B * H * W) if cfg is None else cfg, 1, stream(), d)
-    return dx
+    return ConvCall(1, _fwd_cfg(Cs, B * H * W) if cfg is None else cfg, d, dx, (dy, wd))
 
 
-def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, w_shape, stride=1, padding=0, x2: Optional[torch.Tensor] = None,
-                 splits: Optional[int] = None, cfg: Optional[int] = None):
-    """Weight gradient in the reference layout ``[Co, Ci, KH, KW]`` (fp32)."""
+def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw: Tuple[int, int], stride=1, padding=0,
+                 cin_stored: Optional[int] = None, cfg: Optional[int] = None):
+    """Gradient w.r.t. the NHWC input: fp32 ``[B, H, W, Cin_stored]``."""
+    return prepare_conv2d_dgrad(dy, w, in_hw, stride, padding, cin_stored, cfg).run()
+
+
+WGRAD_TILES = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 64), 4: (16, 64, 128),
+               5: (16, 32, 256), 6: (32, 32, 256), 7: (64, 32, 64)}  # (TN, TK, MCH), csrc/conv.hip
+
+
+def wgrad_cfg(Co: int, Kpad: int) -> int:
+    return 0 if Co <= 16 else ((1 if Kpad <= 64 else 2) if Co <= 32 else 3)
+
+
+def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=None, cfg=None) -> WgradCall:
     _check(x, torch.bfloat16)
     _check(dy, torch.bfloat16)
     Co, Ci, KH, KW = w_shape
@@ -129,8 +161,8 @@ def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, w_shape, stride=1, padding=0
     Kpad = _pad(KH * KW * Cs, 64)
     Npad = _pad(Co, 16)
     if cfg is None:
-        cfg = 0 if Co <= 16 else ((1 if Kpad <= 64 else 2) if Co <= 32 else 3)
-    TN, TK, MCH = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 64)}[cfg]
+        cfg = wgrad_cfg(Co, Kpad)
+    TN, TK, MCH = WGRAD_TILES[cfg]
     M = B * Ho * Wo
     tiles = math.ceil(Npad / TN) * (Kpad // TK)
     if splits is None:
@@ -144,9 +176,17 @@ def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, w_shape, stride=1, padding=0
     d = {"src": src, "dy": ptr(dy), "ldd": Co, "slab": ptr(slab), "splits": splits, "m_per_split": mps,
          "B": B, "Hi": H, "Wi": W, "Ho": Ho, "Wo": Wo, "Co": Co, "Npad": Npad, "Cs": Cs, "KH": KH, "KW": KW,
          "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": Kpad}
-    lib().wgrad(cfg, 1, stream(), d)
-    dWp = slab.sum(dim=1)[0, :Co, :KH * KW * Cs].view(Co, KH, KW, Cs)[..., :Ci]
-    return dWp.permute(0, 3, 1, 2).contiguous()
+
+    def post(sl):
+        dWp = sl.sum(dim=1)[0, :Co, :KH * KW * Cs].view(Co, KH, KW, Cs)[..., :Ci]
+        return dWp.permute(0, 3, 1, 2).contiguous()
+    return WgradCall(cfg, d, slab, post, (x, x2, dy))
+
+
+def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, w_shape, stride=1, padding=0, x2: Optional[torch.Tensor] = None,
+                 splits: Optional[int] = None, cfg: Optional[int] = None):
+    """Weight gradient in the reference layout ``[Co, Ci, KH, KW]`` (fp32)."""
+    return prepare_conv2d_wgrad(x, dy, w_shape, stride, padding, x2, splits, cfg).run()
 
 
 # ---------------------------------------------------------------------------------------------------
