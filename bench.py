@@ -48,7 +48,7 @@ def main():
     from mtl_das_pytorch_amd.data.synthetic import generate
     from mtl_das_pytorch_amd.engine.mtl import MTLProgram
     from mtl_das_pytorch_amd.engine.step import StepRunner
-    from mtl_das_pytorch_amd.engine.tune import autotune_program, load_cache, autotune_phases
+    from mtl_das_pytorch_amd.engine.tune import autotune_program
     from mtl_das_pytorch_amd.models import build_model
     from mtl_das_pytorch_amd.parallel.dist import (FlatGradAllReducer, ShardedIndexSampler,
                                                    broadcast_module_state, init_distributed, shutdown)
@@ -62,10 +62,8 @@ def main():
     model = build_model(args.model)
     prog = MTLProgram(model, args.batch, dev)
     prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world)
-    if args.no_tune:
-        autotune_phases([], load_cache())
-    else:
-        autotune_program(prog, out_path=os.path.join("gpurun_out", "tuned_cfgs.json") if ctx.is_main else None)
+    autotune_program(prog, out_path=os.path.join("gpurun_out", "tuned_cfgs.json") if ctx.is_main else None,
+                     measure=not args.no_tune)
     f = prog.flat
     broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
     X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev)

@@ -406,9 +406,16 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
   const int kh = tap / D.KW, kw = tap - kh * D.KW;
   const float* s = D.slab + (((int64_t)g * D.splits) * D.Npad + co) * D.Kpad + k;
   const int64_t sstride = (int64_t)D.Npad * D.Kpad;
-  float acc = 0.f;
-  for (int sp = 0; sp < D.splits; ++sp) acc += s[sp * sstride];
-  D.grad[g * D.ggs + (((int64_t)co * D.Ci + ci) * D.KH + kh) * D.KW + kw] = acc * scale;
+  // 8 independent partial sums keep 8 loads in flight (the split count reaches ~150 on the big-M layers)
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int sp = 0;
+  for (; sp + 8 <= D.splits; sp += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += s[(sp + j) * sstride];
+  }
+  for (; sp < D.splits; ++sp) acc[0] += s[sp * sstride];
+  const float t = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  D.grad[g * D.ggs + (((int64_t)co * D.Ci + ci) * D.KH + kh) * D.KW + kw] = t * scale;
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -178,7 +178,7 @@ class MTLProgram:
         if bn2 is not None:
             d["bn2"] = bn2.args(training)
         M = self.B * d["H"] * d["W"]
-        ph.add(f"tail{kind}", k_tail_fwd, kind, G, _blocks(M, y.C), d)
+        ph.add(f"tail{kind}", k_tail_fwd, kind, G, _blocks(M, y.C, per_thread=2), d)
 
     def _tail_bwd(self, ph: Phase, kind: int, G: int, y: Act, bn: BNLayer, g: list, dy: Act, r: Act = None,
                   bn2: BNLayer = None, side: Act = None, dy2: Act = None):
@@ -194,15 +194,19 @@ class MTLProgram:
             d.update({"dgamma2": gp["dgamma"], "dbeta2": gp["dbeta"], "dy2": dy2.p, "d2gs": dy2.gs, "ldd2": dy2.ld})
         if side is not None:
             d.update({"side": side.p, "sgs": side.gs, "lds": side.ld})
-        ph.add(f"tailbwd{kind}", k_tail_bwd, kind, G, _blocks(y.M, y.C, cap=256), d)
+        ph.add(f"tailbwd{kind}", k_tail_bwd, kind, G, _blocks(y.M, y.C, cap=1024, per_thread=2), d)
 
     def _conv_fwd(self, ph: Phase, c: ConvLayer, src: dict, out: Act, bn: BNLayer, training: bool):
         mode, cfg, G, d = c.fwd_args(src, out, bn, training)
         ph.add("conv_fwd", k_conv, mode, cfg, G, d, owner=c)
 
     def _conv_bwd(self, ph: Phase, c: ConvLayer, src: dict, dy: Act, dx: Optional[Act]):
+        # the weight gradient is off the critical path: it runs on side stream 2 as soon as its dy exists
+        tag = f"dy{len(ph.launches)}"
+        ph.mark(tag)
         cfg, G, d = c.wgrad_args(src, dy)
-        ph.add("conv_wgrad", k_wgrad, cfg, G, d, owner=c)
+        ph.add("conv_wgrad", k_wgrad, cfg, G, d, owner=c, stream=2, waits=(tag,))
+        self._last_wgrad = len(ph.launches) - 1
         if dx is not None:
             mode, cfg, G, d = c.dgrad_args(dy, dx)
             ph.add("conv_dgrad", k_conv, mode, cfg, G, d, owner=c)
@@ -227,7 +231,8 @@ class MTLProgram:
         T = self.T
         self._conv_fwd(ph, self.conv1, src_dict(self.xin), self.y0, self.bn1, training)
         self._tail(ph, ACT_RELU, 1, self.y0, self.bn1, self.f0, training)
-        for L in self.rbs:
+        ph.cur_stream = 0
+        for ri, L in enumerate(self.rbs):
             s = src_dict(L["in"])
             self._conv_fwd(ph, L["ca"], s, L["ya"], L["bna"], training)
             self._tail(ph, ACT_RELU, 1, L["ya"], L["bna"], L["ha"], training)
@@ -237,7 +242,11 @@ class MTLProgram:
                 self._tail(ph, ADD_RELU, 1, L["yb"], L["bnb"], L["out"], training, r=L["ys"], bn2=L["bns"])
             else:
                 self._tail(ph, ADD_RELU, 1, L["yb"], L["bnb"], L["out"], training, r=L["in"])
-        for L in self.levels:
+            ph.mark(f"F{ri + 1}")
+        # task branches (both tasks per launch) on side stream 1, overlapping the backbone
+        ph.cur_stream = 1
+        for lvl, L in enumerate(self.levels):
+            ph.pending_waits.append(f"F{2 * lvl + 2}")
             s = src_dict(L["Fa"], L["prevB"]) if L["prevB"] is not None else src_dict(L["Fa"])
             self._conv_fwd(ph, L["c0"], s, L["ym1"], L["bn0"], training)
             self._tail(ph, ACT_RELU, T, L["ym1"], L["bn0"], L["hm"], training)
@@ -246,6 +255,9 @@ class MTLProgram:
             if "co" in L:
                 self._conv_fwd(ph, L["co"], src_dict(L["Aout"]), L["yo"], L["bno"], training)
                 self._tail(ph, POOL_RELU, T, L["yo"], L["bno"], L["Bp"], training)
+        ph.mark("levels")
+        ph.cur_stream = 0
+        ph.pending_waits.append("levels")
         A4 = self.levels[3]["Aout"]
         hd = {"feat": A4.p, "fgs": A4.gs, "ldf": A4.ld, "labels": P(self.labels), "lab_stride": 2,
               "lab_off": self.lab_off[0], "T": T, "B": self.B, "HW": A4.H * A4.W, "C": A4.C,
@@ -260,6 +272,7 @@ class MTLProgram:
     def _emit_backward(self) -> Phase:
         ph = Phase("backward")
         T, lv = self.T, self.levels
+        ph.cur_stream = 1
         for li in range(3, -1, -1):
             L = lv[li]
             if "co" in L:
@@ -275,6 +288,8 @@ class MTLProgram:
             self._tail_bwd(ph, ACT_RELU, T, L["ym1"], L["bn0"], [(L["dhm"].p, L["dhm"].gs, L["dhm"].ld)], L["dym1"])
             s = src_dict(L["Fa"], L["prevB"]) if L["prevB"] is not None else src_dict(L["Fa"])
             self._conv_bwd(ph, L["c0"], s, L["dym1"], L["dcat"])
+            ph.mark(f"lvl{li}")
+        ph.cur_stream = 0
         # gradient sources of each shared feature F_k (index k-1), plus f0
         def sources(k: int) -> list:
             src = []
@@ -297,6 +312,7 @@ class MTLProgram:
         for i in range(7, -1, -1):
             R = self.rbs[i]
             g = sources(i + 1)
+            ph.pending_waits.append(f"lvl{i // 2}")  # F_{i+1}'s task-branch gradients
             if R["proj"]:
                 self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["ys"], bn2=R["bns"], dy2=R["dys"])
             else:
@@ -309,8 +325,9 @@ class MTLProgram:
         self.dy0 = new_act(self.arena, 1, self.B, self.y0.H, self.y0.W, self.y0.C)
         self._tail_bwd(ph, ACT_RELU, 1, self.y0, self.bn1, sources(0), self.dy0)
         self._conv_bwd(ph, self.conv1, src_dict(self.xin), self.dy0, None)
-        # weight-gradient slabs -> flat fp32 gradients (one launch for every conv)
-        ph.add("wgrad_finalize", k_wgfin, *self._wgfin_args())
+        # weight-gradient slabs -> flat fp32 gradients (one launch for every conv), after all wgrads
+        ph.launches[self._last_wgrad].record = "wgrads"
+        ph.add("wgrad_finalize", k_wgfin, *self._wgfin_args(), waits=("wgrads",))
         return ph
 
     def _wgfin_args(self):

@@ -2,22 +2,37 @@
 
 Launch arguments (device pointers, geometry, descriptor tables) are resolved once at lowering time,
 so executing a phase is a tight loop of pybind calls; on the GPU the loop is captured once into a
-HIP graph and replayed (engine/step.py)."""
+HIP graph and replayed (engine/step.py).
+
+Launches carry a logical stream id: 0 is the caller's stream (the critical path), 1..3 are side streams
+forked from it at phase start.  Dependencies between streams are explicit ``record``/``wait`` event
+tags; every side stream is joined back into stream 0 at the end of the phase.  Under graph capture the
+events become graph edges, so independent branches (task branches vs. backbone, weight gradients vs.
+the data-gradient chain) run concurrently on the GPU."""
 from __future__ import annotations
 
 from typing import Callable, List
 
+import os
+
 from ..ops.hip import lib, stream
+
+# Side-stream execution is opt-in: measured on MI355X (round 1) the replayed graph showed no kernel
+# overlap for this workload while adding event edges, so the default is the serial order of the list.
+MULTI_STREAM = os.environ.get("MDA_STREAMS", "0") == "1"
 
 
 class Launch:
-    __slots__ = ("name", "fn", "args", "owner")
+    __slots__ = ("name", "fn", "args", "owner", "stream", "waits", "record")
 
-    def __init__(self, name: str, fn: Callable, *args, owner=None):
+    def __init__(self, name: str, fn: Callable, *args, owner=None, stream: int = 0, waits=(), record=None):
         self.name = name
         self.fn = fn
         self.args = args
         self.owner = owner  # the layer object that emitted it (used by the autotuner)
+        self.stream = stream
+        self.waits = tuple(waits)
+        self.record = record
 
     def __call__(self, st: int):
         self.fn(*self.args, st)
@@ -27,14 +42,51 @@ class Phase:
     def __init__(self, name: str):
         self.name = name
         self.launches: List[Launch] = []
+        self._streams = None
+        self.cur_stream = 0      # default stream id for add()
+        self.pending_waits = []  # waits attached to the next add() on any stream
 
-    def add(self, name, fn, *args, owner=None):
-        self.launches.append(Launch(name, fn, *args, owner=owner))
+    def add(self, name, fn, *args, owner=None, stream=None, waits=(), record=None):
+        sid = self.cur_stream if stream is None else stream
+        w = tuple(waits) + tuple(self.pending_waits)
+        self.pending_waits = []
+        self.launches.append(Launch(name, fn, *args, owner=owner, stream=sid, waits=w, record=record))
+
+    def mark(self, tag: str):
+        """Record event ``tag`` after the last launch added on the current stream."""
+        for l in reversed(self.launches):
+            if l.stream == self.cur_stream:
+                if l.record is not None and l.record != tag:
+                    raise ValueError("launch already records an event")
+                l.record = tag
+                return
+        raise ValueError("no launch to mark")
 
     def run(self, st=None):
-        st = stream() if st is None else st
+        import torch
+        if not MULTI_STREAM or all(l.stream == 0 and not l.waits for l in self.launches):
+            st = stream() if st is None else st
+            for l in self.launches:
+                l(st)
+            return
+        main = torch.cuda.current_stream()
+        if self._streams is None or self._streams[0].device != main.device:
+            self._streams = [torch.cuda.Stream(device=main.device) for _ in range(3)]
+        streams = [main] + self._streams
+        used = {l.stream for l in self.launches}
+        start = main.record_event()
+        for sid in used - {0}:
+            streams[sid].wait_event(start)
+        events = {}
         for l in self.launches:
-            l(st)
+            s = streams[l.stream]
+            for tag in l.waits:
+                s.wait_event(events[tag])
+            l(s.cuda_stream)
+            if l.record is not None:
+                events[l.record] = s.record_event()
+        for sid in used - {0}:
+            main.wait_stream(streams[sid])
 
     def __len__(self):
         return len(self.launches)

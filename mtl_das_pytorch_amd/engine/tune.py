@@ -61,8 +61,10 @@ def _time(fn, inner: int = 10, reps: int = 5) -> float:
     return s.elapsed_time(e) / (inner * reps)
 
 
-def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, verbose: bool = False) -> Dict[str, int]:
-    """Choose the conv tile config of every conv launch in ``phases`` (mutates the launches)."""
+def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, verbose: bool = False,
+                    measure: bool = True) -> Dict[str, int]:
+    """Choose the conv tile config of every conv launch in ``phases`` (mutates the launches).  With
+    ``measure=False`` only cached choices are applied (layers missing from the cache keep the heuristic)."""
     cache = load_cache() if cache is None else cache
     L = lib()
     for ph in phases:
@@ -71,6 +73,8 @@ def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, ve
                 continue
             mode, cfg, G, d = launch.args
             sig = conv_signature(mode, G, d)
+            if sig not in cache and not measure:
+                continue
             if sig not in cache:
                 best, best_t = cfg, float("inf")
                 for c in CONV_CFGS:
@@ -88,6 +92,8 @@ def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, ve
             cfg, G, d = launch.args
             conv = launch.owner
             sig = "wgrad|" + conv_signature(0, G, dict(d, N=d["Co"], Hs=d["Hi"], Ws=d["Wi"], stats=0))
+            if sig not in cache and not measure:
+                continue
             if sig not in cache:
                 best, best_t = cfg, float("inf")
                 for c in WGRAD_CFGS:
@@ -103,13 +109,13 @@ def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, ve
     return cache
 
 
-def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False) -> Dict[str, int]:
+def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False, measure: bool = True) -> Dict[str, int]:
     """Tune every conv launch of a lowered program (train forward, eval forward, backward)."""
     if prog.device.type != "cuda":
         return {}
     cache = load_cache()
     n0 = len(cache)
-    autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose)
+    autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose, measure)
     prog.refresh_wgrad_finalize()
     if out_path and len(cache) != n0:
         save_cache(cache, out_path)

@@ -1,0 +1,26 @@
+"""Summarise a rocprofv3 kernel trace: per-kernel totals per step and the per-step span/gap breakdown."""
+import collections
+import csv
+import sys
+
+d = sys.argv[1]
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 24
+rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+tot = collections.defaultdict(float)
+cnt = collections.Counter()
+for r in rows:
+    n = r["Kernel_Name"].split("(")[0][:70]
+    tot[n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    cnt[n] += 1
+S = sum(tot.values())
+print(f"kernel time total {S/1e3:.2f} ms over {steps} steps -> {S/steps:.1f} us/step")
+for n, t in sorted(tot.items(), key=lambda x: -x[1])[:25]:
+    print(f"{t/steps:8.1f} us/step {100*t/S:5.1f}%  {cnt[n]/steps:5.1f} calls/step  {t/cnt[n]:6.1f} us/call  {n}")
+# last step window: kernels after the last gather_batch
+idx = [i for i, r in enumerate(rows) if "gather_batch" in r["Kernel_Name"]]
+if len(idx) >= 2:
+    w = rows[idx[-2]:idx[-1]]
+    span = (int(w[-1]["End_Timestamp"]) - int(w[0]["Start_Timestamp"])) / 1e3
+    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in w) / 1e3
+    print(f"one step: {len(w)} kernels, span {span:.1f} us, busy {busy:.1f} us, gaps {span-busy:.1f} us")
