@@ -1,0 +1,270 @@
+"""Execution backends used by the trainer.
+
+``EngineBackend``  the MI355X path: the model lowered onto the HIP kernels (engine/mtl.py), bf16 MFMA
+                   compute with fp32 masters, one HIP graph per step, fused Adam, on-device metrics.
+``TorchBackend``   the reference-math path in plain PyTorch (fp32 autograd + torch.optim.Adam): runs on
+                   the CPU (tests, BASELINE config #1 plumbing) and serves models not yet lowered.
+
+Both expose the same interface: train/eval a batch given device indices into a resident dataset,
+accumulate per-task loss sums / correct counts / confusion matrices, read them back only when the
+trainer logs, and keep the reference ``state_dict`` format for checkpoints.
+
+Reported tasks: Model A -> distance (16) + event (2); Model B -> its single task; Model C -> the joint
+32-way label decoded into distance + event (plus the joint loss), as in reference utils.py:597-793.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..models import decode_joint, model_tasks
+from ..parallel.dist import DistContext, FlatGradAllReducer, average_, broadcast_module_state, sum_
+
+N_DIST, N_EVENT = 16, 2
+
+
+class Metrics:
+    """Host-side view of the per-task accumulators."""
+
+    def __init__(self, names: Sequence[str], ncls: Sequence[int]):
+        self.names = list(names)
+        self.ncls = list(ncls)
+        self.loss = np.zeros(len(names))
+        self.correct = np.zeros(len(names))
+        self.count = np.zeros(len(names))
+        self.cm = [np.zeros((n, n), dtype=np.int64) for n in ncls]
+
+    def acc(self, t: int) -> float:
+        return float(self.correct[t] / self.count[t]) if self.count[t] else 0.0
+
+    def __sub__(self, o: "Metrics") -> "Metrics":
+        m = Metrics(self.names, self.ncls)
+        m.loss, m.correct, m.count = self.loss - o.loss, self.correct - o.correct, self.count - o.count
+        m.cm = [a - b for a, b in zip(self.cm, o.cm)]
+        return m
+
+
+class Backend:
+    model_type: str
+    names: List[str]
+    ncls: List[int]
+
+    def set_lr(self, lr: float): ...
+    def train_batch(self, idx: torch.Tensor): ...
+    def eval_batch(self, idx: torch.Tensor, nvalid: int): ...
+    def read_metrics(self) -> Metrics: ...
+    def reset_metrics(self): ...
+    def sync_bn_stats(self): ...
+    def optimizer_state(self) -> dict: ...
+    def load_optimizer_state(self, st: dict): ...
+
+
+def _report_tasks(model_type: str):
+    if model_type == "MTL":
+        return ["distance", "event"], [N_DIST, N_EVENT]
+    if model_type == "single_distance":
+        return ["distance"], [N_DIST]
+    if model_type == "single_event":
+        return ["event"], [N_EVENT]
+    return ["distance", "event"], [N_DIST, N_EVENT]  # multi_classifier: decoded joint prediction
+
+
+class TorchBackend(Backend):
+    """Reference-math training in plain PyTorch (fp32)."""
+
+    def __init__(self, model: nn.Module, model_type: str, X: torch.Tensor, labels: torch.Tensor,
+                 X_eval: torch.Tensor, labels_eval: torch.Tensor, ctx: DistContext, batch: int, lr: float,
+                 weight_decay: float, loss_weights: Sequence[float] = (1.0, 1.0)):
+        self.model = model
+        self.model_type = model_type
+        self.ctx = ctx
+        self.device = X.device
+        self.X, self.labels, self.X_eval, self.labels_eval = X, labels, X_eval, labels_eval
+        self.B = batch
+        self.names, self.ncls = _report_tasks(model_type)
+        self.loss_weights = list(loss_weights)
+        self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
+        self._m = Metrics(self.names, self.ncls)
+        self._joint_loss = 0.0
+        self._flat_grads = None
+        broadcast_module_state(ctx, list(model.parameters()) + list(model.buffers()))
+
+    def set_lr(self, lr: float):
+        for g in self.opt.param_groups:
+            g["lr"] = lr
+
+    def _targets(self, lab: torch.Tensor):
+        """Per-reported-task label vectors from the stored labels ([N,2] or joint [N])."""
+        if self.model_type == "multi_classifier":
+            d, e = decode_joint(lab)
+            return [d, e], lab
+        if self.model_type == "MTL":
+            return [lab[:, 0], lab[:, 1]], None
+        return [lab[:, 0] if self.model_type == "single_distance" else lab[:, 1]], None
+
+    def _forward_losses(self, x, lab, train: bool, nvalid: Optional[int] = None):
+        targets, joint = self._targets(lab)
+        out = self.model(x)
+        if self.model_type == "multi_classifier":
+            if isinstance(out, tuple):
+                out = out[0]
+            loss_vec = F.cross_entropy(out, joint, reduction="none")
+            pred = out.argmax(1)
+            preds = list(decode_joint(pred))
+            losses = [loss_vec, loss_vec]
+            total = loss_vec.mean()
+        else:
+            outs = out if isinstance(out, tuple) else (out,)
+            losses = [F.nll_loss(o, t, reduction="none") for o, t in zip(outs, targets)]
+            preds = [o.argmax(1) for o in outs]
+            w = self.loss_weights if len(outs) > 1 else [1.0]
+            total = sum(wi * l.mean() for wi, l in zip(w, losses))
+        n = len(lab) if nvalid is None else nvalid
+        with torch.no_grad():
+            for t in range(len(self.names)):
+                self._m.loss[t] += float(losses[t][:n].sum())
+                self._m.correct[t] += float((preds[t][:n] == targets[t][:n]).sum())
+                self._m.count[t] += n
+                np.add.at(self._m.cm[t], (targets[t][:n].cpu().numpy(), preds[t][:n].cpu().numpy()), 1)
+        return total
+
+    def train_batch(self, idx: torch.Tensor):
+        self.model.train()
+        x, lab = self.X[idx], self.labels[idx]
+        loss = self._forward_losses(x, lab, True)
+        self.opt.zero_grad(set_to_none=False)
+        loss.backward()
+        if self.ctx.enabled:
+            params = [p for p in self.model.parameters() if p.grad is not None]
+            flat = torch.cat([p.grad.reshape(-1) for p in params])
+            FlatGradAllReducer(self.ctx)(flat)
+            flat /= self.ctx.world
+            o = 0
+            for p in params:
+                n = p.numel()
+                p.grad.copy_(flat[o:o + n].view_as(p))
+                o += n
+        self.opt.step()
+
+    @torch.no_grad()
+    def eval_batch(self, idx: torch.Tensor, nvalid: int):
+        self.model.eval()
+        self._forward_losses(self.X_eval[idx], self.labels_eval[idx], False, nvalid)
+
+    def read_metrics(self) -> Metrics:
+        m = Metrics(self.names, self.ncls)
+        m.loss, m.correct, m.count = self._m.loss.copy(), self._m.correct.copy(), self._m.count.copy()
+        m.cm = [c.copy() for c in self._m.cm]
+        return m
+
+    def reset_metrics(self):
+        self._m = Metrics(self.names, self.ncls)
+
+    def sync_bn_stats(self):
+        average_(self.ctx, [b for n, b in self.model.named_buffers() if b.is_floating_point()])
+
+    def optimizer_state(self) -> dict:
+        return {"torch_adam": self.opt.state_dict()}
+
+    def load_optimizer_state(self, st: dict):
+        if "torch_adam" in st:
+            self.opt.load_state_dict(st["torch_adam"])
+
+
+class EngineBackend(Backend):
+    """The MI355X HIP engine (Models A and B)."""
+
+    def __init__(self, model: nn.Module, model_type: str, X: torch.Tensor, labels: torch.Tensor,
+                 X_eval: torch.Tensor, labels_eval: torch.Tensor, ctx: DistContext, batch: int, lr: float,
+                 weight_decay: float, loss_weights: Sequence[float] = (1.0, 1.0), use_graph: bool = True,
+                 tune: bool = False):
+        from .mtl import MTLProgram
+        from .step import StepRunner
+        from .tune import autotune_program
+        if model_type == "multi_classifier":
+            raise NotImplementedError("Model C is served by the torch backend in this round")
+        self.model_type = model_type
+        self.ctx = ctx
+        self.names, self.ncls = _report_tasks(model_type)
+        w = list(loss_weights) if model_type == "MTL" else [1.0]
+        self.prog = MTLProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), loss_weights=w)
+        self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world)
+        autotune_program(self.prog, measure=tune)
+        f = self.prog.flat
+        broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
+        lab_eval = labels_eval if labels_eval is not None else labels
+        self.runner = StepRunner(self.prog, X, labels, use_graph=use_graph,
+                                 allreduce=FlatGradAllReducer(ctx) if ctx.enabled else None,
+                                 X_eval=X_eval if X_eval is not None else X, labels_eval=lab_eval)
+        self.runner.set_lr(lr)
+        self.B = batch
+
+    def set_lr(self, lr: float):
+        self.runner.set_lr(lr)
+
+    def train_batch(self, idx: torch.Tensor):
+        self.runner.train_step(idx)
+
+    def eval_batch(self, idx: torch.Tensor, nvalid: int):
+        if idx.numel() < self.B:  # pad the last batch (BN uses running stats in eval: padding is inert)
+            idx = torch.cat([idx, idx[:1].expand(self.B - idx.numel())])
+        self.prog.nvalid.fill_(nvalid)
+        self.runner.eval_step(idx)
+        self.prog.nvalid.fill_(self.B)
+
+    def read_metrics(self) -> Metrics:
+        met = self.prog.metrics.detach().double().cpu().numpy()
+        conf = self.prog.confusion.detach().cpu().numpy().astype(np.int64)
+        m = Metrics(self.names, self.ncls)
+        for t in range(len(self.names)):
+            m.loss[t], m.correct[t], m.count[t] = met[t, 0], met[t, 1], met[t, 2]
+            n = self.ncls[t]
+            m.cm[t] = conf[t, :n, :n].copy()
+        return m
+
+    def reset_metrics(self):
+        self.runner.reset_metrics()
+
+    def sync_bn_stats(self):
+        f = self.prog.flat
+        average_(self.ctx, [f.bn_mean, f.bn_var])
+
+    def optimizer_state(self) -> dict:
+        f = self.prog.flat
+        return {"engine_adam": {"exp_avg": f.exp_avg.detach().cpu().clone(),
+                                "exp_avg_sq": f.exp_avg_sq.detach().cpu().clone(),
+                                "step": float(f.step.item())}}
+
+    def load_optimizer_state(self, st: dict):
+        if "engine_adam" in st:
+            f = self.prog.flat
+            s = st["engine_adam"]
+            f.exp_avg.copy_(s["exp_avg"].to(f.exp_avg.device))
+            f.exp_avg_sq.copy_(s["exp_avg_sq"].to(f.exp_avg_sq.device))
+            f.step.fill_(s["step"])
+
+    def after_load(self):
+        """Re-pack bf16 weight images after the fp32 masters were overwritten (checkpoint load)."""
+        self.runner.pack_weights()
+
+
+def reduce_metrics(ctx: DistContext, m: Metrics) -> Metrics:
+    """C3: sum counters and confusion matrices over ranks."""
+    if not ctx.enabled:
+        return m
+    t = torch.tensor(np.concatenate([m.loss, m.correct, m.count] + [c.reshape(-1) for c in m.cm]),
+                     dtype=torch.float64, device=ctx.device)
+    sum_(ctx, [t])
+    a = t.cpu().numpy()
+    k = len(m.names)
+    out = Metrics(m.names, m.ncls)
+    out.loss, out.correct, out.count = a[:k], a[k:2 * k], a[2 * k:3 * k]
+    o = 3 * k
+    for i, n in enumerate(m.ncls):
+        out.cm[i] = a[o:o + n * n].reshape(n, n).round().astype(np.int64)
+        o += n * n
+    return out

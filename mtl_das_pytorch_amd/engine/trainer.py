@@ -1,0 +1,296 @@
+"""The generic multi-task trainer behind train.py / test.py.
+
+One trainer replaces the reference's three near-identical loops (trainer_MTL, trainer_single_task,
+trainer_multiClassifier; utils.py:226-793) and its orchestrator (main_process, utils.py:78-223):
+
+  * model factory, output directory ``<out>/<%m-%d-%H_%M_%S> model_type=X is_test=Y/`` and console tee;
+  * optional ``load_state_dict(strict=True)`` of a reference-format ``.pth``;
+  * Adam(lr 1e-3, wd 1e-5); LR divided by 1.5 at every validation epoch (also epoch 0 for A/B, not for C);
+  * epoch loop ``0..epoch_num``: validation every 5 epochs (before training that epoch), training for
+    epochs ``< epoch_num``; every 100 batches the running loss/accuracy line and the ``train*Line.npy``
+    curves; after each validation the ``test*Line.npy`` curves, and -- when the validation distance
+    accuracy reaches 0.98 (A/B) / 0.95 (C) -- a ``{time}__{acc:.5f}_{epoch}.pth`` state_dict checkpoint
+    plus ``confusion matrix <task> <acc> <epoch>.npy`` files;
+  * after training the four curve PNGs, after testing the confusion-matrix SVGs.
+
+Console lines and artefact names/formats follow the reference.  Documented fixes: runs with fewer than
+100 batches per epoch no longer crash (curve files always exist); the single-task accuracy line prints
+its value and the event-task matrix is saved under "event"; Model C's matrices get formatted names;
+every validation also reports the distance MAE in metres (new metric).
+
+Data parallel: one process per GPU (torchrun); each rank trains on its shard of every epoch's
+permutation, gradients are all-reduced over RCCL, validation counters and confusion matrices are
+summed, BN running statistics are averaged before validation, and only rank 0 writes files.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import sys
+import time
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..data.mat_dataset import Dataset_mat_MTL
+from ..data.synthetic import N_DIST, generate
+from ..models import build_model
+from ..parallel.dist import DistContext, ShardedIndexSampler, init_distributed
+from ..utils.config import TrainConfig
+from ..utils.logger import Logger
+from ..utils.metrics import format_task_report, mae_from_confusion, metrics_from_confusion
+from ..utils.plots import plot_confusion_files, plot_curves
+from .backends import EngineBackend, Metrics, TorchBackend, reduce_metrics
+
+
+# ------------------------------------------------------------------------------------------------
+def _labels_tensor(label_list, joint: bool) -> torch.Tensor:
+    return torch.as_tensor(np.asarray(label_list, dtype=np.int64))
+
+
+def load_datasets(cfg: TrainConfig, device):
+    """(X_train, lab_train, X_val, lab_val) resident on ``device``; labels [N,2] or joint [N]."""
+    joint = cfg.model == "multi_classifier"
+    if cfg.synthetic > 0:
+        per = cfg.synthetic
+        d = torch.arange(N_DIST).repeat_interleave(2 * per)
+        e = torch.arange(2).repeat_interleave(per).repeat(N_DIST)
+        seed = cfg.synthetic_seed + (7919 if cfg.is_test else 0)
+        X, d_, e_ = generate(len(d), seed=seed, device="cpu", in_channels=cfg.in_channels, distance=d, event=e)
+        lab = (d_ + N_DIST * e_) if joint else torch.stack([d_, e_], 1)
+        if cfg.is_test:
+            return None, None, X.to(device), lab.to(device)
+        # per-class KFold-like split: every 5th sample of each class goes to validation
+        g = torch.Generator().manual_seed(cfg.random_state)
+        perm = torch.randperm(len(d), generator=g)
+        nval = max(1, len(d) // 5)
+        val_idx, tr_idx = perm[:nval], perm[nval:]
+        return X[tr_idx].to(device), lab[tr_idx].to(device), X[val_idx].to(device), lab[val_idx].to(device)
+    if cfg.is_test:
+        dirs = (cfg.test_set_striking, cfg.test_set_excavating)
+    else:
+        dirs = (cfg.trainVal_set_striking, cfg.trainVal_set_excavating)
+    ds = Dataset_mat_MTL(dirs[0], dirs[1], random_state=cfg.random_state, ram=True, is_test=cfg.is_test,
+                         fold_index=cfg.fold_index, multi_categories=joint, snr_db=cfg.snr_db, progress=False)
+    xtr, ytr = ds.dataset["train"].as_arrays()
+    xva, yva = ds.dataset["val"].as_arrays()
+    if cfg.is_test:
+        return None, None, torch.as_tensor(xva).to(device), torch.as_tensor(yva).to(device)
+    return (torch.as_tensor(xtr).to(device), torch.as_tensor(ytr).to(device),
+            torch.as_tensor(xva).to(device), torch.as_tensor(yva).to(device))
+
+
+class Trainer:
+    def __init__(self, cfg: TrainConfig, ctx: Optional[DistContext] = None):
+        self.cfg = cfg
+        self.ctx = ctx or init_distributed()
+        self.is_main = self.ctx.is_main
+        use_gpu = cfg.GPU_device and torch.cuda.is_available()
+        self.device = self.ctx.device if use_gpu else torch.device("cpu")
+        torch.manual_seed(cfg.seed)
+        self.model = build_model(cfg.model, in_channels=cfg.in_channels)
+        note = "model_type={} is_test={}".format(cfg.model, cfg.is_test)
+        stamp = datetime.datetime.now().strftime("%m-%d-%H_%M_%S")
+        if self.ctx.enabled:  # every rank must agree on the directory name
+            t = torch.tensor([float(datetime.datetime.now().timestamp())], dtype=torch.float64, device=self.ctx.device)
+            self.ctx.broadcast_(t)
+            stamp = datetime.datetime.fromtimestamp(float(t.item())).strftime("%m-%d-%H_%M_%S")
+        self.save_dir = os.path.join(cfg.output_savedir, "{} {}".format(stamp, note)) + "/"
+        if self.is_main:
+            os.makedirs(self.save_dir, exist_ok=True)
+        self.logger = Logger("console output.log", self.save_dir, enabled=self.is_main)
+        if cfg.model_path and cfg.is_test:
+            sd = torch.load(cfg.model_path, map_location="cpu", weights_only=True)
+            self.model.load_state_dict(sd, strict=True)
+        self.backend_name = self._pick_backend()
+
+    def _pick_backend(self) -> str:
+        c = self.cfg
+        if c.backend == "torch" or self.device.type != "cuda":
+            return "torch"
+        if c.backend == "engine":
+            return "engine"
+        return "torch" if c.model == "multi_classifier" else "engine"
+
+    def print(self, *a, **k):
+        if self.is_main:
+            print(*a, **k, file=self.logger)
+
+    # --------------------------------------------------------------------------------------------
+    def run(self):
+        cfg = self.cfg
+        self.print(os.path.abspath(__file__))
+        X, Y, Xv, Yv = load_datasets(cfg, self.device)
+        if X is None:  # test mode evaluates the (whole) test set
+            X, Y = Xv, Yv
+        kw = dict(ctx=self.ctx, batch=cfg.batch_size, lr=cfg.lr, weight_decay=cfg.weight_decay,
+                  loss_weights=cfg.loss_weights)
+        if self.backend_name == "engine":
+            self.model.to(self.device)
+            self.backend = EngineBackend(self.model, cfg.model, X, Y, Xv, Yv, use_graph=cfg.graph, tune=cfg.tune, **kw)
+        else:
+            self.model.to(self.device)
+            self.backend = TorchBackend(self.model, cfg.model, X, Y, Xv, Yv, **kw)
+        self.n_train, self.n_val = len(X), len(Xv)
+        self.print(f"backend: {self.backend_name}  device: {self.device}  world: {self.ctx.world}  "
+                   f"train samples: {0 if cfg.is_test else self.n_train}  val samples: {self.n_val}")
+        start_epoch, lr = 0, cfg.lr
+        if cfg.resume:
+            start_epoch, lr = self._load_resume(cfg.resume)
+        self.lr = lr
+        self.backend.set_lr(lr)
+        self.curves = {"trainAccLine": [[], []], "trainLossLine": [[], []], "testAccLine": [[], []],
+                       "testLossLine": [[], []]}
+        self.start_time = datetime.datetime.now()
+        if cfg.model == "multi_classifier":
+            self.print("{}：{}".format("Start Test" if cfg.is_test else "Start Training", self.start_time))
+        sampler = ShardedIndexSampler(self.n_train, cfg.batch_size, self.ctx, shuffle=True, seed=cfg.seed)
+        E = cfg.epoch_num
+        for epoch in range(start_epoch, E + 1):
+            if epoch % cfg.val_every == 0:
+                resumed_here = cfg.resume and epoch == start_epoch
+                if not resumed_here and (cfg.model != "multi_classifier" or epoch != 0):
+                    self.lr /= cfg.lr_decay
+                    self.backend.set_lr(self.lr)
+                self.validate(epoch)
+                self._save_resume(epoch)
+                if cfg.is_test:
+                    break
+            if epoch < E:
+                self.train_epoch(epoch, sampler)
+                self.print("Epoch {} finished！".format(epoch + 1))
+        if self.is_main:
+            if cfg.is_test:
+                plot_confusion_files(self.save_dir)
+            else:
+                for name in ("trainAccLine", "trainLossLine"):
+                    p = os.path.join(self.save_dir, name + ".npy")
+                    if not os.path.exists(p):  # fewer than log_every batches ran: keep the artefact set complete
+                        np.save(p, self._train_line(name))
+                plot_curves(self.save_dir, cfg.model)
+        self.ctx.barrier()
+        self.logger.save()
+        self.logger.close()
+        return self.save_dir
+
+    # --------------------------------------------------------------------------------------------
+    def _train_line(self, name):
+        rows = self.curves[name]
+        if self.cfg.model in ("single_distance", "single_event"):
+            return np.asarray([rows[0]], dtype=np.float64)
+        return np.asarray(rows, dtype=np.float64)
+
+    def train_epoch(self, epoch: int, sampler: ShardedIndexSampler):
+        cfg, be = self.cfg, self.backend
+        batches = sampler.epoch(epoch, self.device)
+        be.reset_metrics()
+        last = be.read_metrics()
+        for bi, idx in enumerate(batches):
+            be.train_batch(idx)
+            if (bi + 1) % cfg.log_every == 0:
+                now = be.read_metrics()
+                delta = reduce_metrics(self.ctx, now - last)
+                last = now
+                nt = len(delta.names)
+                acc = [float(delta.correct[t] / max(delta.count[t], 1)) for t in range(nt)]
+                # reference: mean over the 100 batches of (batch-mean loss / batch size)
+                loss = [float(delta.loss[t] / max(delta.count[t], 1) / cfg.batch_size) for t in range(nt)]
+                if cfg.model == "multi_classifier":
+                    loss = [loss[0], loss[0]]
+                self.print("epoch-iteration:{}-{}, loss:{}, accuracy:{}".format(epoch + 1, bi + 1, loss, acc))
+                self.print("time:{}".format(datetime.datetime.now() - self.start_time))
+                for t in range(2):
+                    self.curves["trainLossLine"][t].append(loss[min(t, nt - 1)])
+                    self.curves["trainAccLine"][t].append(acc[min(t, nt - 1)])
+                if self.is_main:
+                    np.save(os.path.join(self.save_dir, "trainLossLine"), self._train_line("trainLossLine"))
+                    np.save(os.path.join(self.save_dir, "trainAccLine"), self._train_line("trainAccLine"))
+
+    @torch.no_grad()
+    def validate(self, epoch: int):
+        cfg, be = self.cfg, self.backend
+        be.sync_bn_stats()
+        be.reset_metrics()
+        n = self.n_val
+        # shard the validation set over ranks; every rank runs full batches (the last one masked)
+        order = torch.arange(n, device=self.device)
+        per = (n + self.ctx.world - 1) // self.ctx.world
+        mine = order[self.ctx.rank * per:min(n, (self.ctx.rank + 1) * per)]
+        batch_means = np.zeros(len(be.names))
+        prev = be.read_metrics()
+        for i in range(0, len(mine), cfg.batch_size):
+            idx = mine[i:i + cfg.batch_size]
+            be.eval_batch(idx, idx.numel())
+            cur = be.read_metrics()
+            d = cur - prev
+            prev = cur
+            batch_means += d.loss / np.maximum(d.count, 1)  # reference: sum of batch-mean losses
+        m = reduce_metrics(self.ctx, be.read_metrics())
+        if self.ctx.enabled:
+            bm = torch.tensor(batch_means, dtype=torch.float64, device=self.ctx.device)
+            self.ctx.all_reduce_(bm)
+            batch_means = bm.cpu().numpy()
+        nt = len(m.names)
+        accs = [m.acc(t) for t in range(nt)]
+        if cfg.model == "multi_classifier":
+            val_loss = [batch_means[0] / n] * 2
+        else:
+            val_loss = [batch_means[t] / n for t in range(nt)]
+        for t in range(2):
+            self.curves["testLossLine"][t].append(float(val_loss[min(t, nt - 1)]))
+            self.curves["testAccLine"][t].append(accs[min(t, nt - 1)])
+        star = "*" * 50
+        if cfg.model == "MTL":
+            self.print("{}\nepoch:{}  Validation Accuracy: distance:{}  event:{}".format(star, epoch, accs[0], accs[1]))
+        elif cfg.model == "multi_classifier":
+            self.print("{}\nepoch:{}  Accuracy: distance:{}  event:{}".format(star, epoch + 1, accs[0], accs[1]))
+        else:
+            self.print("{}\nepoch:{}  Validation Accuracy: {}:{}".format(star, epoch, m.names[0], accs[0]))
+        for t in range(nt):
+            self.print(format_task_report("Task {}：{}".format(t + 1, m.names[t]), m.cm[t]))
+        if "distance" in m.names:
+            self.print("Distance MAE (m)：{}".format(mae_from_confusion(m.cm[m.names.index("distance")])))
+        if self.is_main:
+            if not cfg.is_test:
+                np.save(os.path.join(self.save_dir, "testAccLine"), np.asarray(self.curves["testAccLine"]))
+                np.save(os.path.join(self.save_dir, "testLossLine"), np.asarray(self.curves["testLossLine"]))
+            acc1 = accs[0]
+            if acc1 >= cfg.threshold:
+                sd = {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()}
+                name = "{}__{:.5f}_{}.pth".format(datetime.datetime.now().strftime("%Y_%m_%d__%H_%M_%S"), acc1, epoch)
+                torch.save(sd, os.path.join(self.save_dir, name))
+                for t in range(nt):
+                    np.save(os.path.join(self.save_dir, "confusion matrix {} {:.5f} {}.npy".format(
+                        m.names[t], accs[t], epoch)), m.cm[t])
+        self.last_val = {"epoch": epoch, "acc": dict(zip(m.names, accs)), "loss": val_loss,
+                         "mae_m": mae_from_confusion(m.cm[0]) if m.names[0] == "distance" else None}
+        self.ctx.barrier()
+
+    # --------------------------------------------------------------------------------------------
+    def _save_resume(self, epoch: int):
+        """Resumable sidecar (never inside the reference-format .pth): weights, optimizer moments, epoch,
+        LR and RNG state, written by rank 0 after every validation."""
+        if not self.is_main or self.cfg.is_test:
+            return
+        st = {"epoch": epoch, "lr": self.lr, "model": {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()},
+              "optimizer": self.backend.optimizer_state(), "rng": torch.get_rng_state(),
+              "curves": self.curves, "model_type": self.cfg.model}
+        tmp = os.path.join(self.save_dir, "last.resume.pt.tmp")
+        torch.save(st, tmp)
+        os.replace(tmp, os.path.join(self.save_dir, "last.resume.pt"))
+
+    def _load_resume(self, path: str):
+        st = torch.load(path, map_location="cpu", weights_only=True)
+        self.model.load_state_dict(st["model"], strict=True)
+        self.backend.load_optimizer_state(st["optimizer"])
+        if hasattr(self.backend, "after_load"):
+            self.backend.after_load()
+        torch.set_rng_state(st["rng"])
+        self.print(f"resumed from {path} at epoch {st['epoch']} (lr {st['lr']})")
+        return int(st["epoch"]), float(st["lr"])
+
+
+def main_process(cfg: TrainConfig) -> str:
+    """Reference-compatible orchestrator entry point (utils.main_process)."""
+    return Trainer(cfg).run()

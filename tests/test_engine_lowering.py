@@ -1,0 +1,44 @@
+"""The MI355X lowering is pure bookkeeping until launch time: build it on the CPU and check the program
+structure, the grouped (per-task) parameter layout and the descriptor tables."""
+import torch
+
+from mtl_das_pytorch_amd.engine.mtl import MTLProgram
+from mtl_das_pytorch_amd.models import MTL_Net, Single_Task_Net
+
+
+def test_mtl_program_structure():
+    m = MTL_Net()
+    sd_before = {k: v.clone() for k, v in m.state_dict().items()}
+    p = MTLProgram(m, 32, "cpu")
+    # parameters now live in the flat buffer but keep their values and keys
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, sd_before[k]), k
+    assert p.flat.numel >= sum(x.numel() for x in m.parameters())
+    n = p.num_launches()
+    assert n["forward_train"] == 60 and n["backward"] == 90
+    # both task branches of a level are ONE grouped launch with an even parameter stride
+    L = p.levels[1]
+    assert L["c0"].G == 2 and L["c0"].wstride > 0
+    g0, g1 = m.att_mask_generato2[0][0].weight, m.att_mask_generato2[1][0].weight
+    assert p.flat.off(g1) - p.flat.off(g0) == L["c0"].wstride
+    # shared backbone input read with group stride 0, per-task prev level with stride > 0
+    assert L["Fa"].gs == 0 and L["prevB"].gs > 0
+    assert p.wgfin_table.numel() == len(p.convs) * 80
+    assert p.optseg_table.numel() == 2 * sum(c.G for c in p.convs) * 80
+
+
+def test_single_task_program():
+    p = MTLProgram(Single_Task_Net("event"), 8, "cpu")
+    assert p.T == 1 and p.lab_off == [1]
+    assert all(c.G == 1 for c in p.convs)
+
+
+def test_flat_state_views_track_module():
+    m = MTL_Net()
+    p = MTLProgram(m, 4, "cpu")
+    with torch.no_grad():
+        m.conv1[0].weight.fill_(0.5)
+    o = p.flat.off(m.conv1[0].weight)
+    assert torch.all(p.flat.params[o:o + m.conv1[0].weight.numel()] == 0.5)
+    m.conv1[1].running_mean.fill_(2.0)
+    assert p.flat.bn_mean[p.flat.bn_offsets[id(m.conv1[1])]].item() == 2.0
