@@ -29,6 +29,8 @@ METRIC = "samples/sec (whole node) MTL train bs=32 at 1/2/4/8 MI355X; event-cls 
 # MI355X measured 4,037 samples/s (profiles/r1_eager_reference_probe.log) and is reported alongside.
 BASELINE_VALUE = 176.1
 EAGER_MI355X_PER_GPU = 4037.0
+MODEL_NAMES = {"MTL": "modelA_MTL", "single_distance": "modelB_singleTask_distance",
+               "single_event": "modelB_singleTask_event", "multi_classifier": "modelC_multiClassifier"}
 
 
 def main():
@@ -37,7 +39,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32, help="per-GPU batch")
-    ap.add_argument("--model", default="MTL", choices=["MTL", "single_distance", "single_event"])
+    ap.add_argument("--model", default="MTL", choices=["MTL", "single_distance", "single_event", "multi_classifier"])
     ap.add_argument("--dataset-size", type=int, default=2048, help="synthetic samples resident per GPU")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per step")
     ap.add_argument("--bucket-mb", type=float, default=0.0)
@@ -46,10 +48,11 @@ def main():
 
     import torch
     from mtl_das_pytorch_amd.data.synthetic import generate
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
     from mtl_das_pytorch_amd.engine.mtl import MTLProgram
     from mtl_das_pytorch_amd.engine.step import StepRunner
     from mtl_das_pytorch_amd.engine.tune import autotune_program
-    from mtl_das_pytorch_amd.models import build_model
+    from mtl_das_pytorch_amd.models import build_model, encode_joint
     from mtl_das_pytorch_amd.parallel.dist import (FlatGradAllReducer, ShardedIndexSampler,
                                                    broadcast_module_state, init_distributed, shutdown)
 
@@ -60,14 +63,15 @@ def main():
     dev = ctx.device
     torch.manual_seed(1234)  # identical init on every rank (then broadcast for certainty)
     model = build_model(args.model)
-    prog = MTLProgram(model, args.batch, dev)
+    joint = args.model == "multi_classifier"
+    prog = InceptionProgram(model, args.batch, dev) if joint else MTLProgram(model, args.batch, dev)
     prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world)
     autotune_program(prog, out_path=os.path.join("gpurun_out", "tuned_cfgs.json") if ctx.is_main else None,
                      measure=not args.no_tune)
     f = prog.flat
     broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
     X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev)
-    labels = torch.stack([d, e], 1)
+    labels = encode_joint(d, e) if joint else torch.stack([d, e], 1)
     runner = StepRunner(prog, X, labels, use_graph=not args.no_graph,
                         allreduce=FlatGradAllReducer(ctx, args.bucket_mb) if world > 1 else None)
     runner.set_lr(1e-3 / 1.5)  # reference: lr/1.5 applied at the epoch-0 validation
@@ -107,12 +111,14 @@ def main():
         "vs_baseline": round(value / BASELINE_VALUE, 3),
         "dtype": "bf16",
         "data": "synthetic (DAS time-space matrices 1x100x250, HBM-resident, random-init weights)",
-        "config": {"model": "modelA_MTL" if args.model == "MTL" else f"modelB_singleTask_{args.model.split('_')[1]}",
+        "config": {"model": MODEL_NAMES.get(args.model, args.model),
                    "global_batch": args.batch * world, "seq_len": 250, "input_shape": [1, 100, 250],
                    "parallelism": f"dp{world}"},
-        "train_acc_timed_steps": {"distance": round(float(m[0, 1] / m[0, 2]), 4),
-                                  "event": round(float(m[-1, 1] / m[-1, 2]), 4)},
-        "vs_eager_pytorch_mi355x": round(value / (EAGER_MI355X_PER_GPU * world), 3),
+        "train_acc_timed_steps": ({"distance": round(float(m[1, 1] / m[1, 2]), 4),
+                                   "event": round(float(m[2, 1] / m[2, 2]), 4)} if joint else
+                                  {"distance": round(float(m[0, 1] / m[0, 2]), 4),
+                                   "event": round(float(m[-1, 1] / m[-1, 2]), 4)}),
+        "vs_eager_pytorch_mi355x": round(value / (EAGER_MI355X_PER_GPU * world), 3) if args.model == "MTL" else None,
         "hip_graph": not args.no_graph,
         "baseline_note": "vs_baseline divides by BASELINE.md's 176.1 samples/s (reference on CPU, the only "
                          "throughput number it has); vs_eager_pytorch_mi355x divides by the reference-style "

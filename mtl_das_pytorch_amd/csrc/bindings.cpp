@@ -190,7 +190,11 @@ void pool3(int is_max, int backward, int64_t stream, py::dict d) {
   PoolArgs a{};
   a.x = P<const bf16_t>(d, "x"); a.ldx = (int)I(d, "ldx");
   a.y = P<bf16_t>(d, "y"); a.ldy = (int)I(d, "ldy");
-  a.g = P<const float>(d, "g"); a.ldg = (int)I(d, "ldg");
+  if (d.contains("g")) {
+    // a list of (ptr, group stride, pitch) sources, or one pointer with pitch "ldg"
+    if (py::isinstance<py::list>(d["g"])) a.g = parse_grads(d["g"].cast<py::list>());
+    else { a.g.n = 1; a.g.p[0] = P<const float>(d, "g"); a.g.ld[0] = (int)I(d, "ldg"); }
+  }
   a.dx = P<float>(d, "dx"); a.lddx = (int)I(d, "lddx");
   a.B = (int)I(d, "B"); a.H = (int)I(d, "H"); a.W = (int)I(d, "W"); a.C = (int)I(d, "C");
   a.Ho = (int)I(d, "Ho"); a.Wo = (int)I(d, "Wo");

@@ -104,7 +104,7 @@ struct ClsArgs {
 struct PoolArgs {
   const bf16_t* x; int ldx;     // input [B*H*W][C] (bf16)
   bf16_t* y; int ldy;           // output [B*Ho*Wo][C]
-  const float* g; int ldg;      // backward: grad of output (fp32)
+  GradSrcs g;                   // backward: grad of output = sum of fp32 sources (concat consumers)
   float* dx; int lddx;          // backward: grad of input (fp32)
   int B, H, W, C, Ho, Wo;
 };

@@ -26,15 +26,16 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restri
     for (int c = 0; c < 8; ++c) v[c] = c < Cin ? X[(src * Cin + c) * (int64_t)H * W + r] : 0.f;
     store8(out + p * 8, v);
   }
-  if (blockIdx.x == 0 && threadIdx.x < B * lab_w) {
-    const int b = threadIdx.x / lab_w, k = threadIdx.x - b * lab_w;
-    lab_out[threadIdx.x] = lab[idx[b] * lab_w + k];
-  }
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < B * lab_w; i += 256) {
+      const int b = i / lab_w, k = i - b * lab_w;
+      lab_out[i] = lab[idx[b] * lab_w + k];
+    }
 }
 
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
                         int64_t* lab_out, int B, int Cin, int H, int W, hipStream_t st) {
-  if (Cin > 8 || B * lab_w > 256) return -2;
+  if (Cin > 8) return -2;
   const int64_t M = (int64_t)B * H * W;
   int blocks = (int)std::min<int64_t>((M + 255) / 256, 2048);
   hipLaunchKernelGGL(gather_batch_kernel, dim3(blocks), dim3(256), 0, st, X, idx, lab, lab_w, out, lab_out, B, Cin, H, W);
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {
             }
           const int me = (ih - 2 * oh) * 3 + (iw - 2 * ow);
           float g[8];
-          load8f(a.g + ((int64_t)(b * a.Ho + oh) * a.Wo + ow) * a.ldg + cg * 8, g);
+          gsum8(a.g, 0, (int64_t)(b * a.Ho + oh) * a.Wo + ow, cg * 8, g);
 #pragma unroll
           for (int j = 0; j < 8; ++j) if (am[j] == me) acc[j] += g[j];
         }
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {
       for (int oh = max(0, ih - 1); oh <= min(a.Ho - 1, ih + 1); ++oh)
         for (int ow = max(0, iw - 1); ow <= min(a.Wo - 1, iw + 1); ++ow) {
           float g[8];
-          load8f(a.g + ((int64_t)(b * a.Ho + oh) * a.Wo + ow) * a.ldg + cg * 8, g);
+          gsum8(a.g, 0, (int64_t)(b * a.Ho + oh) * a.Wo + ow, cg * 8, g);
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[j] += g[j] * (1.f / 9.f);
         }

@@ -176,22 +176,24 @@ class TorchBackend(Backend):
 
 
 class EngineBackend(Backend):
-    """The MI355X HIP engine (Models A and B)."""
+    """The MI355X HIP engine: Models A/B lowered by engine/mtl.py, Model C by engine/inception.py."""
 
     def __init__(self, model: nn.Module, model_type: str, X: torch.Tensor, labels: torch.Tensor,
                  X_eval: torch.Tensor, labels_eval: torch.Tensor, ctx: DistContext, batch: int, lr: float,
                  weight_decay: float, loss_weights: Sequence[float] = (1.0, 1.0), use_graph: bool = True,
                  tune: bool = False):
+        from .inception import InceptionProgram
         from .mtl import MTLProgram
         from .step import StepRunner
         from .tune import autotune_program
-        if model_type == "multi_classifier":
-            raise NotImplementedError("Model C is served by the torch backend in this round")
         self.model_type = model_type
         self.ctx = ctx
         self.names, self.ncls = _report_tasks(model_type)
-        w = list(loss_weights) if model_type == "MTL" else [1.0]
-        self.prog = MTLProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), loss_weights=w)
+        if model_type == "multi_classifier":
+            self.prog = InceptionProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]))
+        else:
+            w = list(loss_weights) if model_type == "MTL" else [1.0]
+            self.prog = MTLProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), loss_weights=w)
         self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world)
         autotune_program(self.prog, measure=tune)
         f = self.prog.flat
@@ -220,6 +222,13 @@ class EngineBackend(Backend):
         met = self.prog.metrics.detach().double().cpu().numpy()
         conf = self.prog.confusion.detach().cpu().numpy().astype(np.int64)
         m = Metrics(self.names, self.ncls)
+        if self.model_type == "multi_classifier":
+            # rows: joint, distance, event; the joint CE loss is reported for both decoded tasks
+            for t in range(2):
+                m.loss[t], m.correct[t], m.count[t] = met[0, 0], met[1 + t, 1], met[1 + t, 2]
+                n = self.ncls[t]
+                m.cm[t] = conf[t, :n, :n].copy()
+            return m
         for t in range(len(self.names)):
             m.loss[t], m.correct[t], m.count[t] = met[t, 0], met[t, 1], met[t, 2]
             n = self.ncls[t]

@@ -1,0 +1,277 @@
+"""Lowering of the Inception-v3 multi-classifier (reference Model C, modelC_multiClassifier.py:28-172).
+
+The network is lowered as a DAG of *values* (bf16 NHWC activations).  Every ``BasicConv2d`` becomes
+one MFMA implicit-GEMM conv (BN sums fused into its epilogue) plus one fused BN+ReLU tail; the Inception
+pools are the 3x3 pool kernels.  There is no concatenation: the branches of a block write their
+outputs straight into channel slices of the block's output buffer (the tail / pool output pitch is the
+concat width), and the next block's convs read that buffer in place.
+
+Backward walks the ops in reverse.  Each consumer of a value writes the gradient w.r.t. its input ONCE
+into its own fp32 buffer and registers it as a *gradient source* of the value; the producing kernel
+(the BN-tail backward, or the pool backward) sums the sources on load.  A branch output that lives in a
+slice of a concat buffer gets the matching channel slices of the concat value's sources, so the
+concat backward is free as well.  The classifier (GAP -> Dropout -> Linear -> CE) is the fused
+``cls_head`` kernel (csrc/head.hip) which also writes d(fc) into the flat gradient buffer.
+
+Launch counts per training step (B fixed): forward 94 conv + 94 tails + 13 pools + head, backward
+94 tail-bwd + 94 wgrad + 93 dgrad + 13 pool-bwd + one finalize, one fused Adam.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from ..models.multi_classifier import (BasicConv2d, InceptionA, InceptionB, InceptionC, InceptionD, InceptionE,
+                                       Multi_Classifier)
+from .core import Act, Arena, BNLayer, ConvLayer, FlatState, P, grads_of, new_act, src_dict
+from .lowering import ACT_RELU, LoweredProgram
+from .program import Phase, k_cls_head, k_pool, k_wgfin
+
+
+class Val:
+    """A bf16 activation of the lowered graph and the fp32 gradient sources its consumers register.
+    ``parent``/``coff``: this value is channels [coff, coff+C) of a concat value."""
+
+    def __init__(self, act: Act, parent: "Val" = None, coff: int = 0, needs_grad: bool = True):
+        self.act = act
+        self.parent = parent
+        self.coff = coff
+        self.needs_grad = needs_grad
+        self.grads: List[Act] = []
+
+    def grad_sources(self) -> List[Act]:
+        g = list(self.grads)
+        if self.parent is not None:
+            g += [a.slice(self.coff, self.act.C) for a in self.parent.grad_sources()]
+        if not g or len(g) > 6:
+            raise RuntimeError(f"value has {len(g)} gradient sources (1..6 supported)")
+        return g
+
+
+class CBR:
+    """conv -> BN -> ReLU (one BasicConv2d)."""
+
+    def __init__(self, prog: "InceptionProgram", bc: BasicConv2d, src: Val, out: Val):
+        A, B, f = prog.arena, prog.B, prog.flat
+        self.src, self.out = src, out
+        s = src.act
+        self.conv = c = ConvLayer([bc.conv], f, A, B, s.H, s.W, cin_stored=s.C)
+        if (c.Ho, c.Wo, c.Co) != (out.act.H, out.act.W, out.act.C):
+            raise ValueError(f"shape mismatch lowering {bc}: conv gives {(c.Ho, c.Wo, c.Co)}, "
+                             f"destination {(out.act.H, out.act.W, out.act.C)}")
+        self.bn = BNLayer([bc.bn], f, A, B * c.Ho * c.Wo)
+        self.y = new_act(A, 1, B, c.Ho, c.Wo, c.Co)
+        self.dy = new_act(A, 1, B, c.Ho, c.Wo, c.Co)
+        self.dx = new_act(A, 1, B, s.H, s.W, s.C, torch.float32) if src.needs_grad else None
+
+    def forward(self, prog, ph: Phase, training: bool):
+        prog._conv_fwd(ph, self.conv, src_dict(self.src.act), self.y, self.bn, training)
+        prog._tail(ph, ACT_RELU, 1, self.y, self.bn, self.out.act, training)
+
+    def backward(self, prog, ph: Phase):
+        prog._tail_bwd(ph, ACT_RELU, 1, self.y, self.bn, grads_of(self.out.grad_sources()), self.dy)
+        prog._conv_bwd(ph, self.conv, src_dict(self.src.act), self.dy, self.dx)
+        if self.dx is not None:
+            self.src.grads.append(self.dx)
+
+
+class Pool:
+    """maxpool 3x3/s2 (valid) or avgpool 3x3/s1/p1 (count_include_pad)."""
+
+    def __init__(self, prog: "InceptionProgram", is_max: bool, src: Val, out: Val):
+        self.is_max, self.src, self.out = int(is_max), src, out
+        s = src.act
+        Ho, Wo = ((s.H - 3) // 2 + 1, (s.W - 3) // 2 + 1) if is_max else (s.H, s.W)
+        if (Ho, Wo, s.C) != (out.act.H, out.act.W, out.act.C):
+            raise ValueError("pool output shape mismatch")
+        self.dx = new_act(prog.arena, 1, prog.B, s.H, s.W, s.C, torch.float32) if src.needs_grad else None
+
+    def _geom(self, B):
+        s, o = self.src.act, self.out.act
+        return {"x": s.p, "ldx": s.ld, "B": B, "H": s.H, "W": s.W, "C": s.C, "Ho": o.H, "Wo": o.W}
+
+    def forward(self, prog, ph: Phase, training: bool):
+        d = dict(self._geom(prog.B), y=self.out.act.p, ldy=self.out.act.ld)
+        ph.add("pool_fwd", k_pool, self.is_max, 0, d)
+
+    def backward(self, prog, ph: Phase):
+        if self.dx is None:
+            return
+        d = dict(self._geom(prog.B), g=grads_of(self.out.grad_sources()), dx=self.dx.p, lddx=self.dx.ld)
+        ph.add("pool_bwd", k_pool, self.is_max, 1, d)
+        self.src.grads.append(self.dx)
+
+
+class InceptionProgram(LoweredProgram):
+    """Static train/eval programs of a :class:`Multi_Classifier` for a fixed per-GPU batch size."""
+
+    label_width = 1  # joint label (distance + 16 * event)
+
+    def __init__(self, model: Multi_Classifier, batch: int, device, in_hw=(100, 250), p_drop: float = 0.5):
+        if model.aux_logits:
+            raise NotImplementedError("aux_logits=True is not lowered (the reference trains without it)")
+        if model.transform_input:
+            raise NotImplementedError("transform_input is not lowered")
+        if model.num_classes > 64:
+            raise ValueError("the fused classifier head supports at most 64 classes")
+        self.model = model
+        self.B = batch
+        self.device = torch.device(device)
+        self.H0, self.W0 = in_hw
+        self.cin = model.Conv2d_1a_3x3.conv.in_channels
+        if self.cin > 8:
+            raise ValueError("in_channels > 8 not supported by the gather kernel")
+        self.p_drop = float(p_drop)
+        model.to(self.device)
+        self.flat = FlatState(model, self.device)
+        self.arena = Arena(self.device)
+        self._alloc()
+        self.arena.finalize()
+        self._emit()
+
+    # -------------------------------------------------------------------------------------------
+    def _val(self, H, W, C) -> Val:
+        return Val(new_act(self.arena, 1, self.B, H, W, C))
+
+    def _cbr(self, bc: BasicConv2d, src: Val, out: Optional[Val] = None) -> Val:
+        if out is None:
+            kh, kw = bc.conv.kernel_size
+            sh, sw = bc.conv.stride
+            ph, pw = bc.conv.padding
+            H = (src.act.H + 2 * ph - kh) // sh + 1
+            W = (src.act.W + 2 * pw - kw) // sw + 1
+            out = self._val(H, W, bc.conv.out_channels)
+        self.ops.append(CBR(self, bc, src, out))
+        return out
+
+    def _pool(self, is_max: bool, src: Val, out: Optional[Val] = None) -> Val:
+        if out is None:
+            s = src.act
+            H, W = ((s.H - 3) // 2 + 1, (s.W - 3) // 2 + 1) if is_max else (s.H, s.W)
+            out = self._val(H, W, s.C)
+        self.ops.append(Pool(self, is_max, src, out))
+        return out
+
+    def _concat(self, H, W, widths) -> tuple:
+        cat = self._val(H, W, sum(widths))
+        parts, o = [], 0
+        for w in widths:
+            parts.append(Val(cat.act.slice(o, w), parent=cat, coff=o))
+            o += w
+        return cat, parts
+
+    def _block(self, blk, x: Val) -> Val:
+        """Lower one Inception block; returns its concat output value."""
+        H, W = x.act.H, x.act.W
+        if isinstance(blk, InceptionA):
+            pf = blk.branch_pool.conv.out_channels
+            cat, (o1, o5, o3, op) = self._concat(H, W, [64, 64, 96, pf])
+            self._cbr(blk.branch1x1, x, o1)
+            self._cbr(blk.branch5x5_2, self._cbr(blk.branch5x5_1, x), o5)
+            self._cbr(blk.branch3x3dbl_3, self._cbr(blk.branch3x3dbl_2, self._cbr(blk.branch3x3dbl_1, x)), o3)
+            self._cbr(blk.branch_pool, self._pool(False, x), op)
+        elif isinstance(blk, InceptionB):
+            Ho, Wo = (H - 3) // 2 + 1, (W - 3) // 2 + 1
+            cat, (o3, od, om) = self._concat(Ho, Wo, [384, 96, x.act.C])
+            self._cbr(blk.branch3x3, x, o3)
+            self._cbr(blk.branch3x3dbl_3, self._cbr(blk.branch3x3dbl_2, self._cbr(blk.branch3x3dbl_1, x)), od)
+            self._pool(True, x, om)
+        elif isinstance(blk, InceptionC):
+            cat, (o1, o7, od, op) = self._concat(H, W, [192, 192, 192, 192])
+            self._cbr(blk.branch1x1, x, o1)
+            self._cbr(blk.branch7x7_3, self._cbr(blk.branch7x7_2, self._cbr(blk.branch7x7_1, x)), o7)
+            v = x
+            for i in range(1, 5):
+                v = self._cbr(getattr(blk, f"branch7x7dbl_{i}"), v)
+            self._cbr(blk.branch7x7dbl_5, v, od)
+            self._cbr(blk.branch_pool, self._pool(False, x), op)
+        elif isinstance(blk, InceptionD):
+            Ho, Wo = (H - 3) // 2 + 1, (W - 3) // 2 + 1
+            cat, (o3, o7, om) = self._concat(Ho, Wo, [320, 192, x.act.C])
+            self._cbr(blk.branch3x3_2, self._cbr(blk.branch3x3_1, x), o3)
+            v = x
+            for i in range(1, 4):
+                v = self._cbr(getattr(blk, f"branch7x7x3_{i}"), v)
+            self._cbr(blk.branch7x7x3_4, v, o7)
+            self._pool(True, x, om)
+        elif isinstance(blk, InceptionE):
+            cat, (o1, o3a, o3b, oda, odb, op) = self._concat(H, W, [320, 384, 384, 384, 384, 192])
+            self._cbr(blk.branch1x1, x, o1)
+            s = self._cbr(blk.branch3x3_1, x)
+            self._cbr(blk.branch3x3_2a, s, o3a)
+            self._cbr(blk.branch3x3_2b, s, o3b)
+            d = self._cbr(blk.branch3x3dbl_2, self._cbr(blk.branch3x3dbl_1, x))
+            self._cbr(blk.branch3x3dbl_3a, d, oda)
+            self._cbr(blk.branch3x3dbl_3b, d, odb)
+            self._cbr(blk.branch_pool, self._pool(False, x), op)
+        else:
+            raise TypeError(f"cannot lower block {type(blk).__name__}")
+        return cat
+
+    def _alloc(self):
+        m, A, B = self.model, self.arena, self.B
+        self.x = A.zeros((B, self.H0, self.W0, 8))
+        self.labels = torch.zeros((B,), dtype=torch.int64, device=self.device)
+        self.ops = []
+        v = Val(Act(self.x, 0, 8, 8, 0, B, self.H0, self.W0), needs_grad=False)
+        v = self._cbr(m.Conv2d_1a_3x3, v)
+        v = self._cbr(m.Conv2d_2a_3x3, v)
+        v = self._cbr(m.Conv2d_2b_3x3, v)
+        v = self._pool(True, v)
+        v = self._cbr(m.Conv2d_3b_1x1, v)
+        v = self._cbr(m.Conv2d_4a_3x3, v)
+        v = self._pool(True, v)
+        for blk in m.mixed:
+            v = self._block(blk, v)
+        self.feat = v
+        a = v.act
+        if a.C != m.fc.in_features:
+            raise ValueError("feature width does not match fc")
+        self.HWf = a.H * a.W
+        N = m.num_classes
+        self.dfeat = new_act(A, 1, B, a.H, a.W, a.C, torch.float32)
+        v.grads.append(self.dfeat)
+        self.fc_feat = A.empty((B, a.C), torch.float32)
+        self.logp = torch.zeros((B, N), device=self.device)   # logits of the last batch
+        self.dlogits = A.empty((B, N), torch.float32)
+        self.seed = torch.zeros(1, dtype=torch.int64, device=self.device)  # dropout RNG counter
+        self.extra_state = [self.seed]
+        # metrics [joint, distance, event] x [loss, correct, count, abs_err]; confusion: distance, event
+        self.metrics = torch.zeros((3, 4), device=self.device)
+        self.confusion = torch.zeros((2, 16, 16), device=self.device, dtype=torch.int32)
+        self.nvalid = torch.full((1,), B, device=self.device, dtype=torch.int64)
+        self.convs: List[ConvLayer] = [op.conv for op in self.ops if isinstance(op, CBR)]
+
+    # -------------------------------------------------------------------------------------------
+    def _head_args(self, training: bool) -> dict:
+        m, f, a = self.model, self.flat, self.feat.act
+        d = {"x": a.p, "ldx": a.ld, "W": P(f.params, f.off(m.fc.weight)), "bias": P(f.params, f.off(m.fc.bias)),
+             "labels": P(self.labels), "B": self.B, "HW": self.HWf, "C": a.C, "N": m.num_classes,
+             "p_drop": self.p_drop if training else 0.0, "seed": P(self.seed), "feat": P(self.fc_feat),
+             "logits": P(self.logp), "dlogits": P(self.dlogits), "metrics": P(self.metrics),
+             "confusion": P(self.confusion), "nvalid": P(self.nvalid)}
+        if training:
+            d.update({"dx": self.dfeat.p, "dW": P(f.grads, f.off(m.fc.weight)), "db": P(f.grads, f.off(m.fc.bias))})
+        return d
+
+    def _emit(self):
+        self.fwd_train = self._emit_forward(True)
+        self.fwd_eval = self._emit_forward(False)
+        self.bwd = self._emit_backward()
+        self.opt = self._emit_optimizer()
+
+    def _emit_forward(self, training: bool) -> Phase:
+        ph = Phase("forward_train" if training else "forward_eval")
+        for op in self.ops:
+            op.forward(self, ph, training)
+        ph.add("cls_head", k_cls_head, self._head_args(training))
+        return ph
+
+    def _emit_backward(self) -> Phase:
+        ph = Phase("backward")
+        for op in reversed(self.ops):
+            op.backward(self, ph)
+        ph.launches[self._last_wgrad].record = "wgrads"
+        ph.add("wgrad_finalize", k_wgfin, *self._wgfin_args(), waits=("wgrads",))
+        return ph

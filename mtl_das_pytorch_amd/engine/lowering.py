@@ -1,0 +1,112 @@
+"""Shared lowering machinery: the emit helpers every model program uses (conv forward / backward,
+fused BN tails and their backward, wgrad finalize, fused Adam + weight packing, batch gather)."""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+
+from .core import Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table
+from .program import Phase, k_adam, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad
+
+ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
+
+
+def _blocks(M: int, C: int, cap: int = 1024, per_thread: int = 4) -> int:
+    cg = max(1, C // 8)
+    pl = max(1, 256 // cg)
+    return int(max(1, min(cap, math.ceil(M / (pl * per_thread)))))
+
+
+class LoweredProgram:
+    """Base class: subclasses allocate buffers / layers, then emit ``fwd_train``, ``fwd_eval``, ``bwd``
+    and ``opt`` phases with these helpers.  ``self.convs`` lists every ConvLayer (for the finalize and
+    packing descriptor tables) and ``self.label_width`` the columns of the stored label tensor."""
+
+    label_width = 2
+
+    # -------------------------------------------------------------------------------------------
+    def _tail(self, ph: Phase, kind: int, G: int, y: Act, bn: BNLayer, out: Act, training: bool, r: Act = None,
+              bn2: BNLayer = None, H=None, W=None):
+        d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(training), "out": out.p, "ogs": out.gs, "ldo": out.ld,
+             "B": self.B, "H": y.H if H is None else H, "W": y.W if W is None else W, "C": y.C}
+        if r is not None:
+            d.update({"r": r.p, "rgs": r.gs, "ldr": r.ld})
+        if bn2 is not None:
+            d["bn2"] = bn2.args(training)
+        M = self.B * d["H"] * d["W"]
+        ph.add(f"tail{kind}", k_tail_fwd, kind, G, _blocks(M, y.C, per_thread=2), d)
+
+    def _tail_bwd(self, ph: Phase, kind: int, G: int, y: Act, bn: BNLayer, g: list, dy: Act, r: Act = None,
+                  bn2: BNLayer = None, side: Act = None, dy2: Act = None):
+        d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(True), "B": self.B, "H": y.H, "W": y.W, "C": y.C,
+             "g": g, "ws": P(bn.ws), "dy": dy.p, "dgs": dy.gs, "ldd": dy.ld}
+        d.update(bn.grad_ptrs())
+        if r is not None:
+            d.update({"r": r.p, "rgs": r.gs, "ldr": r.ld})
+        if bn2 is not None:
+            d["bn2"] = bn2.args(True)
+            d["ws2"] = P(bn.ws2)
+            gp = bn2.grad_ptrs()
+            d.update({"dgamma2": gp["dgamma"], "dbeta2": gp["dbeta"], "dy2": dy2.p, "d2gs": dy2.gs, "ldd2": dy2.ld})
+        if side is not None:
+            d.update({"side": side.p, "sgs": side.gs, "lds": side.ld})
+        ph.add(f"tailbwd{kind}", k_tail_bwd, kind, G, _blocks(y.M, y.C, cap=1024, per_thread=2), d)
+
+    def _conv_fwd(self, ph: Phase, c: ConvLayer, src: dict, out: Act, bn: BNLayer, training: bool):
+        mode, cfg, G, d = c.fwd_args(src, out, bn, training)
+        ph.add("conv_fwd", k_conv, mode, cfg, G, d, owner=c)
+
+    def _conv_bwd(self, ph: Phase, c: ConvLayer, src: dict, dy: Act, dx: Optional[Act]):
+        # the weight gradient is off the critical path: it runs on side stream 2 as soon as its dy exists
+        tag = f"dy{len(ph.launches)}"
+        ph.mark(tag)
+        cfg, G, d = c.wgrad_args(src, dy)
+        ph.add("conv_wgrad", k_wgrad, cfg, G, d, owner=c, stream=2, waits=(tag,))
+        self._last_wgrad = len(ph.launches) - 1
+        if dx is not None:
+            mode, cfg, G, d = c.dgrad_args(dy, dx)
+            ph.add("conv_dgrad", k_conv, mode, cfg, G, d, owner=c)
+
+    def set_source(self, X: torch.Tensor, labels: torch.Tensor, idx: torch.Tensor):
+        """Bind the dataset tensors the gather launch reads (X [N,C,H,W] fp32, labels [N,2], idx [B])."""
+        self.src = (X, labels, idx)
+
+    def gather_phase(self, X, labels, idx) -> Phase:
+        ph = Phase("gather")
+        ph.add("gather", k_gather, X, idx, labels, self.label_width, self.x, self.labels, self.B, X.shape[1], self.H0, self.W0)
+        return ph
+
+    def _wgfin_args(self):
+        self.wgfin_table, nd, nblocks = build_wgfin_table([c.finalize_desc() for c in self.convs], self.device)
+        return self.wgfin_table, nd, nblocks
+
+    def refresh_wgrad_finalize(self):
+        """Rebuild the finalize descriptor table after wgrad configs (split counts) changed."""
+        for l in self.bwd.launches:
+            if l.name == "wgrad_finalize":
+                l.args = self._wgfin_args()
+
+    def _emit_optimizer(self, grad_scale: float = 1.0) -> Dict[str, Phase]:
+        segs = [s for c in self.convs for s in c.opt_segments()]
+        self.optseg_table, ns, nblocks = build_optseg_table(segs, self.device)
+        f = self.flat
+        base = {"p": P(f.params), "g": P(f.grads), "m": P(f.exp_avg), "v": P(f.exp_avg_sq), "n": f.numel,
+                "lr": P(f.lr), "step": P(f.step), "segs": P(self.optseg_table), "nsegs": ns, "nblocks": nblocks}
+        self._opt_base = base
+        upd = Phase("adam")
+        upd.add("adam_pack", k_adam, dict(base, update=1, b1=0.9, b2=0.999, eps=1e-8, wd=0.0, grad_scale=grad_scale))
+        pack = Phase("pack")
+        pack.add("pack", k_adam, dict(base, update=0))
+        return {"adam": upd, "pack": pack}
+
+    def set_optimizer(self, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, grad_scale: float = 1.0):
+        d = dict(self._opt_base, update=1, b1=betas[0], b2=betas[1], eps=eps, wd=weight_decay, grad_scale=grad_scale)
+        upd = Phase("adam")
+        upd.add("adam_pack", k_adam, d)
+        self.opt["adam"] = upd
+
+    # -------------------------------------------------------------------------------------------
+    def num_launches(self) -> dict:
+        return {"forward_train": len(self.fwd_train), "backward": len(self.bwd), "adam": len(self.opt["adam"]) + 1}

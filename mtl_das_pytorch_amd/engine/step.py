@@ -54,7 +54,7 @@ class StepRunner:
     def _mutable_state(self) -> List[torch.Tensor]:
         f = self.p.flat
         return [f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step, self.p.metrics,
-                self.p.confusion, self.p.logp]
+                self.p.confusion, self.p.logp] + list(getattr(self.p, "extra_state", []))
 
     def pack_weights(self):
         """(Re)build the bf16 MFMA weight images from the fp32 masters (after init / load_state_dict)."""

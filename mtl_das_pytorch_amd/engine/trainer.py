@@ -111,7 +111,7 @@ class Trainer:
             return "torch"
         if c.backend == "engine":
             return "engine"
-        return "torch" if c.model == "multi_classifier" else "engine"
+        return "engine"
 
     def print(self, *a, **k):
         if self.is_main:
