@@ -1,11 +1,19 @@
 """Summarise a rocprofv3 kernel trace: per-kernel totals per step and the per-step span/gap breakdown."""
 import collections
 import csv
+import glob
+import os
+import sqlite3
 import sys
 
 d = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 24
-rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+if os.path.exists(f"{d}/run_kernel_trace.csv"):
+    rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+else:  # rocprofv3's default rocpd (SQLite) output
+    db = sqlite3.connect(glob.glob(f"{d}/**/*.db", recursive=True)[0])
+    rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+            for n, s, e in db.execute("select name, start, end from kernels")]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 tot = collections.defaultdict(float)
 cnt = collections.Counter()
