@@ -68,7 +68,7 @@ GradSrcs parse_grads(const py::list& l) {
 
 BNArgs parse_bn(const py::dict& d) {
   BNArgs b{};
-  b.stats = P<const float>(d, "stats");
+  b.stats = P<const double>(d, "stats");
   b.gamma = P<const float>(d, "gamma");
   b.beta = P<const float>(d, "beta");
   b.run_mean = P<float>(d, "run_mean");
@@ -93,7 +93,7 @@ void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
   a.out = P<void>(d, "out");
   a.ogs = I(d, "ogs");
   a.ldo = (int)I(d, "ldo");
-  a.stats = P<float>(d, "stats");
+  a.stats = P<double>(d, "stats");
   a.B = (int)I(d, "B"); a.Hs = (int)I(d, "Hs"); a.Ws = (int)I(d, "Ws"); a.Ho = (int)I(d, "Ho"); a.Wo = (int)I(d, "Wo");
   a.N = (int)I(d, "N"); a.Npad = (int)I(d, "Npad"); a.Cs = (int)I(d, "Cs");
   a.KH = (int)I(d, "KH"); a.KW = (int)I(d, "KW"); a.sh = (int)I(d, "sh"); a.sw = (int)I(d, "sw");
@@ -132,13 +132,14 @@ TailArgs parse_tail(const py::dict& d) {
   a.out = P<bf16_t>(d, "out"); a.ogs = I(d, "ogs"); a.ldo = (int)I(d, "ldo");
   a.B = (int)I(d, "B"); a.H = (int)I(d, "H"); a.W = (int)I(d, "W"); a.C = (int)I(d, "C");
   if (d.contains("g")) a.g = parse_grads(d["g"].cast<py::list>());
-  a.ws = P<float>(d, "ws"); a.ws2 = P<float>(d, "ws2");
+  a.ws = P<double>(d, "ws"); a.ws2 = P<double>(d, "ws2");
   a.side = P<float>(d, "side"); a.sgs = I(d, "sgs"); a.lds = (int)I(d, "lds");
   a.dy = P<bf16_t>(d, "dy"); a.dgs = I(d, "dgs"); a.ldd = (int)I(d, "ldd");
   a.dy2 = P<bf16_t>(d, "dy2"); a.d2gs = I(d, "d2gs"); a.ldd2 = (int)I(d, "ldd2");
   a.dgamma = P<float>(d, "dgamma"); a.dbeta = P<float>(d, "dbeta");
   a.dgamma2 = P<float>(d, "dgamma2"); a.dbeta2 = P<float>(d, "dbeta2");
   a.pgs = I(d, "pgs");
+  a.tsc = P<uint64_t>(d, "tsc");
   if (a.C % 8 || a.C > 2048) throw std::runtime_error("tail: C must be a multiple of 8 and <= 2048");
   return a;
 }
@@ -147,7 +148,7 @@ void tail_fwd(int kind, int G, int blocks, int64_t stream, py::dict d) {
   check(launch_tail_fwd(kind, parse_tail(d), G, blocks, S(stream)), "tail_fwd");
 }
 void tail_bwd(int kind, int G, int blocks, int64_t stream, py::dict d) {
-  check(launch_tail_bwd(kind, parse_tail(d), G, blocks, S(stream)), "tail_bwd");
+  check(launch_tail_bwd(kind, parse_tail(d), G, blocks, (int)I(d, "fused", 0), S(stream)), "tail_bwd");
 }
 
 void mtl_head(int64_t stream, py::dict d) {

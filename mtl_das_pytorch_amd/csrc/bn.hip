@@ -292,11 +292,11 @@ __global__ __launch_bounds__(256) void tail_bwd_reduce_kernel(TailArgs a) {
     float t = 0.f;
     for (int seg = 0; seg < S; ++seg) t += s_seg[seg * NI + item];
     const int k = item / C, ch = item - k * C;
-    if (k < 2) atomicAdd(a.ws + ((int64_t)z * NREP + rep) * 2 * C + k * C + ch, t);
+    if (k < 2) atomicAdd(a.ws + ((int64_t)z * NREP + rep) * 2 * C + k * C + ch, (double)t);
     if (two) {
-      float* w2 = a.ws2 + ((int64_t)z * NREP + rep) * 2 * C;
-      if (k == 0) atomicAdd(w2 + ch, t);
-      if (k == 2) atomicAdd(w2 + C + ch, t);
+      double* w2 = a.ws2 + ((int64_t)z * NREP + rep) * 2 * C;
+      if (k == 0) atomicAdd(w2 + ch, (double)t);
+      if (k == 2) atomicAdd(w2 + C + ch, (double)t);
     }
   }
 }
@@ -316,10 +316,11 @@ __global__ __launch_bounds__(256) void tail_bwd_apply_kernel(TailArgs a) {
   const float inv_n = 1.f / (float)a.bn.count;
   for (int ch = threadIdx.x; ch < C; ch += blockDim.x) {
     for (int k = 0; k < (two ? 2 : 1); ++k) {
-      const float* w = (k == 0 ? a.ws : a.ws2) + (int64_t)z * NREP * 2 * C;
-      float sdz = 0.f, sdx = 0.f;
+      const double* w = (k == 0 ? a.ws : a.ws2) + (int64_t)z * NREP * 2 * C;
+      double sdz_d = 0.0, sdx_d = 0.0;
 #pragma unroll
-      for (int r = 0; r < NREP; ++r) { sdz += w[r * 2 * C + ch]; sdx += w[r * 2 * C + C + ch]; }
+      for (int r = 0; r < NREP; ++r) { sdz_d += w[r * 2 * C + ch]; sdx_d += w[r * 2 * C + C + ch]; }
+      const float sdz = (float)sdz_d, sdx = (float)sdx_d;
       const float g = (k == 0 ? a.bn.gamma[a.bn.pstride * z + ch] : a.bn2.gamma[a.bn2.pstride * z + ch]);
       const float inv = s_inv[4 * C * k + ch], mu = s_mean[4 * C * k + ch];
       const float mdz = sdz * inv_n, mdx = sdx * inv_n;
@@ -366,6 +367,115 @@ __global__ __launch_bounds__(256) void tail_bwd_apply_kernel(TailArgs a) {
   }
 }
 
+// Single-launch BN backward for small maps: block (cg, -, z) owns channels [8cg, 8cg+8) for ALL M
+// pixels, so the batch reduction is a block reduction (no global atomics, no second launch, exact and
+// deterministic).  Each of the 1024 threads keeps the dz / xhat of its R <= 4 pixels in registers, so
+// the kernel is just: statistics + gamma (one round trip) -> pixel loads -> block reduction -> stores.
+// The autotuner picks it per layer against reduce+apply; it wins where launch and memory latency
+// dominate (deep Model A levels, most of Inception-v3 at 100x250).
+constexpr int FUSED_T = 1024;
+template <int KIND, int R>
+__global__ __launch_bounds__(FUSED_T) void tail_bwd_fused_kernel(TailArgs a) {
+  __shared__ float s_x[2][5][8];                // BN1/BN2 x (scale, shift, mean, invstd, gamma) x 8 ch
+  __shared__ float s_part[FUSED_T / 64][3][8];  // per-wave partial sums
+  __shared__ float s_coef[2][3][8];             // dy = A*dz + Bx*xhat + Cc (BN1, BN2)
+  const int z = blockIdx.z;
+  const int c = blockIdx.x * 8;
+  const bool two = (KIND == ADD_RELU && a.r_bn);
+  const bool tick = a.tsc && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0;
+#define TICK(i) if (tick) a.tsc[i] = wall_clock64()
+  TICK(0);
+  if (threadIdx.x < (two ? 16 : 8)) {
+    const int k = threadIdx.x >> 3, j = threadIdx.x & 7;
+    const BNArgs& bk = k ? a.bn2 : a.bn;
+    float sc, sh, mu, inv;
+    bn_channel(bk, z, c + j, false, sc, sh, mu, inv);
+    s_x[k][0][j] = sc; s_x[k][1][j] = sh; s_x[k][2][j] = mu; s_x[k][3][j] = inv;
+    s_x[k][4][j] = bk.gamma[bk.pstride * z + c + j];
+  }
+  __syncthreads();
+  TICK(1);
+  BwdCtx X;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    X.sc[j] = s_x[0][0][j]; X.sh[j] = s_x[0][1][j]; X.mean[j] = s_x[0][2][j]; X.inv[j] = s_x[0][3][j];
+    X.sc2[j] = s_x[1][0][j]; X.sh2[j] = s_x[1][1][j]; X.mean2[j] = s_x[1][2][j]; X.inv2[j] = s_x[1][3][j];
+  }
+  const int M = a.B * a.H * a.W;
+  float sdz[8], sdx[8], sdx2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sdz[j] = 0.f; sdx[j] = 0.f; sdx2[j] = 0.f; }
+  float dzc[R][8], xhc[R][8], xh2c[R][8];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int p = threadIdx.x + r * FUSED_T;
+    float side[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { dzc[r][j] = 0.f; xhc[r][j] = 0.f; xh2c[r][j] = 0.f; }
+    if (p < M) {
+      compute_dz<KIND>(a, X, z, p, c, dzc[r], xhc[r], xh2c[r], side);
+      if ((KIND == SIGMUL || (KIND == ADD_RELU && !a.r_bn)) && a.side)
+        store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sdz[j] += dzc[r][j];
+      sdx[j] += dzc[r][j] * xhc[r][j];
+      if (two) sdx2[j] += dzc[r][j] * xh2c[r][j];
+    }
+  }
+  TICK(2);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t0 = wave_sum(sdz[j]), t1 = wave_sum(sdx[j]);
+    float t2 = two ? wave_sum(sdx2[j]) : 0.f;
+    if (lane == 0) { s_part[wid][0][j] = t0; s_part[wid][1][j] = t1; s_part[wid][2][j] = t2; }
+  }
+  __syncthreads();
+  TICK(3);
+  if (threadIdx.x < (two ? 16 : 8)) {
+    const int k = threadIdx.x >> 3, j = threadIdx.x & 7;
+    float sd = 0.f, sx = 0.f;
+#pragma unroll
+    for (int w = 0; w < FUSED_T / 64; ++w) { sd += s_part[w][0][j]; sx += s_part[w][k ? 2 : 1][j]; }
+    const BNArgs& bk = k ? a.bn2 : a.bn;
+    const float inv_n = 1.f / (float)bk.count;
+    const float ginv = s_x[k][4][j] * s_x[k][3][j];
+    s_coef[k][0][j] = ginv;                  // dy = g*inv*(dz - mean(dz) - xhat*mean(dz*xhat))
+    s_coef[k][1][j] = -ginv * sx * inv_n;
+    s_coef[k][2][j] = -ginv * sd * inv_n;
+    float* dg = k ? a.dgamma2 : a.dgamma;
+    float* db = k ? a.dbeta2 : a.dbeta;
+    if (dg) dg[a.pgs * z + c + j] = sx;
+    if (db) db[a.pgs * z + c + j] = sd;
+  }
+  __syncthreads();
+  TICK(4);
+  float A1[8], B1[8], C1[8], A2[8], B2[8], C2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    A1[j] = s_coef[0][0][j]; B1[j] = s_coef[0][1][j]; C1[j] = s_coef[0][2][j];
+    A2[j] = s_coef[1][0][j]; B2[j] = s_coef[1][1][j]; C2[j] = s_coef[1][2][j];
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int p = threadIdx.x + r * FUSED_T;
+    if (p >= M) break;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = A1[j] * dzc[r][j] + B1[j] * xhc[r][j] + C1[j];
+    store8(a.dy + a.dgs * z + (int64_t)p * a.ldd + c, o);
+    if (two) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = A2[j] * dzc[r][j] + B2[j] * xh2c[r][j] + C2[j];
+      store8(a.dy2 + a.d2gs * z + (int64_t)p * a.ldd2 + c, o);
+    }
+  }
+  TICK(5);
+#undef TICK
+}
+
 // ------------------------------------------------------------------------------------------------
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st) {
   size_t lds = (size_t)4 * a.C * sizeof(float);
@@ -379,7 +489,28 @@ int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t 
   return (int)hipGetLastError();
 }
 
-int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st) {
+int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, int fused, hipStream_t st) {
+  if (fused) {
+    const int M = a.B * a.H * a.W;
+    const int R = (M + FUSED_T - 1) / FUSED_T;
+    // register-cached pixels per thread: up to 4 (2 for the two-BN residual tail) without spilling
+    if (R > (kind == ADD_RELU ? 2 : 4)) return -3;  // too large: use reduce + apply
+    dim3 grid(a.C / 8, 1, G);
+#define KR(X, RR) hipLaunchKernelGGL((tail_bwd_fused_kernel<X, RR>), grid, dim3(FUSED_T), 0, st, a)
+#define K(X)                                \
+  case X:                                   \
+    if (R <= 1) KR(X, 1);                   \
+    else if (R <= 2) KR(X, 2);              \
+    else KR(X, 4);                          \
+    break;
+    switch (kind) {
+      K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(ADD_RELU) K(POOL_RELU)
+      default: return -1;
+    }
+#undef K
+#undef KR
+    return (int)hipGetLastError();
+  }
   const int CG = a.C / 8;
   const int PL = 256 / CG;
   size_t lds_r = (size_t)(8 * a.C + 3 * PL * a.C + 3 * a.C + 256) * sizeof(float);

@@ -60,10 +60,29 @@ DEV void store8f(float* p, const float* v) {
 
 DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
-DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Cross-lane sums with DPP (data-parallel primitives): one VALU op per step instead of a ds_bpermute
+// round trip through the LDS unit per __shfl_xor (measured: 24 six-step shuffle reductions took
+// 4-7 us in the BN backward; DPP makes them negligible).  gfx9-family row operations: a row is 16
+// lanes; bound_ctrl zero-fills lanes shifted in from outside the row.
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
+DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK,
+                                                               BANK_MASK, true));
+}
+// Sum over each row of 16 lanes; the result is valid in lane 15 of the row.
+DEV float row16_sum(float v) {
+  v += dpp_f<0x111>(v);  // row_shr:1
+  v += dpp_f<0x112>(v);  // row_shr:2
+  v += dpp_f<0x114>(v);  // row_shr:4
+  v += dpp_f<0x118>(v);  // row_shr:8
   return v;
+}
+// Sum over the wave, returned in every lane.
+DEV float wave_sum(float v) {
+  v = row16_sum(v);
+  v += dpp_f<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -101,7 +120,10 @@ DEV void gsum8(const GradSrcs& g, int z, int64_t pix, int c, float* v) {
 
 // Per-BN-layer state. Everything is indexed by group z with the given strides (0 = shared).
 struct BNArgs {
-  const float* stats;    // [G][NREP][2][C] sums of y and y^2 (training) -- zeroed every step
+  const double* stats;   // [G][NREP][2][C] sums of y and y^2 (training) -- zeroed every step.  fp64: the
+                         // atomic summation order then perturbs results by ~1e-16 instead of ~1e-7,
+                         // which the (chaotic at init) networks amplified into run-to-run gradient
+                         // differences of up to 10% (tools/dbg_race.py)
   const float* gamma;    // [C] (+ z * pstride)
   const float* beta;
   float* run_mean;       // running stats (+ z * pstride)
@@ -114,36 +136,47 @@ struct BNArgs {
   int training;          // 1: batch statistics (and update running), 0: running statistics
 };
 
-// Computes per-channel scale/shift into LDS: out = y * scale + shift == gamma * (y - mean) / std + beta
-// Also returns mean and invstd arrays when requested (needed by backward kernels).
+// BN constants of channel c of group z: out = y * scale + shift == gamma * (y - mean) * invstd + beta.
+// Training: batch statistics from the NREP replicas of the conv-epilogue sums (and, when requested,
+// the running-statistics update -- done by exactly one block per launch); eval: running statistics.
+DEV void bn_channel(const BNArgs& a, int z, int c, bool update_running, float& scale, float& shift, float& mean,
+                    float& inv) {
+  float var;
+  if (a.training) {
+    const double* st = a.stats + (int64_t)z * NREP * 2 * a.C;
+    double s = 0.0, ss = 0.0;
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) { s += st[r * 2 * a.C + c]; ss += st[r * 2 * a.C + a.C + c]; }
+    const double inv_n = 1.0 / (double)a.count;
+    const double md = s * inv_n;
+    mean = (float)md;
+    var = (float)fmax(ss * inv_n - md * md, 0.0);
+    if (update_running) {
+      const float unb = a.count > 1 ? var * (float)a.count / (float)(a.count - 1) : var;
+      float* rm = a.run_mean + a.pstride * z;
+      float* rv = a.run_var + a.pstride * z;
+      rm[c] = (1.f - a.momentum) * rm[c] + a.momentum * mean;
+      rv[c] = (1.f - a.momentum) * rv[c] + a.momentum * unb;
+    }
+  } else {
+    mean = a.run_mean[a.pstride * z + c];
+    var = a.run_var[a.pstride * z + c];
+  }
+  inv = rsqrtf(var + a.eps);
+  const float g = a.gamma[a.pstride * z + c], b = a.beta[a.pstride * z + c];
+  scale = g * inv;
+  shift = b - mean * g * inv;
+}
+
+// All C channels into LDS (mean / invstd arrays optional -- needed by backward kernels).
 DEV void bn_prepare(const BNArgs& a, int z, float* s_scale, float* s_shift, float* s_mean, float* s_invstd,
                     bool update_running) {
-  const float* st = a.stats + (int64_t)z * NREP * 2 * a.C;
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    float mean, var;
-    if (a.training) {
-      float s = 0.f, ss = 0.f;
-#pragma unroll
-      for (int r = 0; r < NREP; ++r) { s += st[r * 2 * a.C + c]; ss += st[r * 2 * a.C + a.C + c]; }
-      float inv_n = 1.f / (float)a.count;
-      mean = s * inv_n;
-      var = fmaxf(ss * inv_n - mean * mean, 0.f);
-      if (update_running) {
-        float unb = a.count > 1 ? var * (float)a.count / (float)(a.count - 1) : var;
-        float* rm = a.run_mean + a.pstride * z;
-        float* rv = a.run_var + a.pstride * z;
-        rm[c] = (1.f - a.momentum) * rm[c] + a.momentum * mean;
-        rv[c] = (1.f - a.momentum) * rv[c] + a.momentum * unb;
-      }
-    } else {
-      mean = a.run_mean[a.pstride * z + c];
-      var = a.run_var[a.pstride * z + c];
-    }
-    float inv = rsqrtf(var + a.eps);
-    float g = a.gamma[a.pstride * z + c], b = a.beta[a.pstride * z + c];
-    s_scale[c] = g * inv;
-    s_shift[c] = b - mean * g * inv;
-    if (s_mean) s_mean[c] = mean;
+    float sc, sh, mu, inv;
+    bn_channel(a, z, c, update_running, sc, sh, mu, inv);
+    s_scale[c] = sc;
+    s_shift[c] = sh;
+    if (s_mean) s_mean[c] = mu;
     if (s_invstd) s_invstd[c] = inv;
   }
   if (update_running && a.training && threadIdx.x == 0 && a.nbt) a.nbt[z] += 1;

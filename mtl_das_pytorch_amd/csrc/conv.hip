@@ -210,14 +210,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       }
       if (want_stats) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            s[r] += __shfl_xor(s[r], o, 64);
-            ss[r] += __shfl_xor(ss[r], o, 64);
-          }
+        for (int r = 0; r < 4; ++r) {  // pixels of a 16-lane row -> lane 15 (DPP, common.h)
+          s[r] = row16_sum(s[r]);
+          ss[r] = row16_sum(ss[r]);
         }
-        if (l16 == 0) {
+        if (l16 == 15) {
           const int cl = wn * WN + i * 16 + 4 * kgl;  // channel within the block tile
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -238,7 +235,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         float v = 0.f;
 #pragma unroll
         for (int w2 = 0; w2 < WAVES_M; ++w2) v += s_st[(w2 * BN_T + cl) * 2 + which];
-        atomicAdd(a.stats + ((int64_t)z * NREP + rep) * 2 * a.N + which * a.N + n, v);
+        atomicAdd(a.stats + ((int64_t)z * NREP + rep) * 2 * a.N + which * a.N + n, (double)v);
       }
     }
   }

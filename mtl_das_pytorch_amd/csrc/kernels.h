@@ -17,7 +17,7 @@ struct ConvArgs {
   void* out;  // FWD: bf16, DGRAD: fp32; [M][ldo] (+ z * ogs)
   int64_t ogs;
   int ldo;
-  float* stats;  // FWD: [G][NREP][2][N] (may be null)
+  double* stats;  // FWD: [G][NREP][2][N] fp64 (may be null)
   int B, Hs, Ws, Ho, Wo;
   int N, Npad, Cs;
   int KH, KW, sh, sw, ph, pw;
@@ -62,11 +62,12 @@ struct TailArgs {
   int B, H, W, C;
   // backward only
   GradSrcs g;                       // upstream fp32 gradient(s) on the tail's output grid
-  float* ws; float* ws2;            // [G][NREP][2][C]
+  double* ws; double* ws2;          // [G][NREP][2][C] fp64 (see BNArgs::stats)
   float* side; int64_t sgs; int lds;
   bf16_t* dy; int64_t dgs; int ldd;
   bf16_t* dy2; int64_t d2gs; int ldd2;
   float* dgamma; float* dbeta; float* dgamma2; float* dbeta2; int64_t pgs;
+  uint64_t* tsc;                    // optional phase timestamps (profiling; null in production)
 };
 
 struct HeadArgs {
@@ -130,7 +131,7 @@ int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st);
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);
-int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);
+int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, int fused, hipStream_t st);
 int launch_mtl_head(const HeadArgs& a, hipStream_t st);
 int launch_cls_head(const ClsArgs& a, int64_t* seed_mut, hipStream_t st);
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,

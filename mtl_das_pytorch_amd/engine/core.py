@@ -147,8 +147,7 @@ class Arena:
     def __init__(self, device):
         self.device = torch.device(device)
         self._zero_specs: List[tuple] = []
-        self._zero_f32: Optional[torch.Tensor] = None
-        self._zero_i32: Optional[torch.Tensor] = None
+        self._zero: Dict[torch.dtype, torch.Tensor] = {}
         self.views: List[torch.Tensor] = []
 
     def empty(self, shape, dtype=torch.bfloat16) -> torch.Tensor:
@@ -163,23 +162,21 @@ class Arena:
         return lv
 
     def finalize(self):
-        nf = sum(pad_to(int(np.prod(v.shape)), 64) for v in self._zero_specs if v.dtype == torch.float32)
-        ni = sum(pad_to(int(np.prod(v.shape)), 64) for v in self._zero_specs if v.dtype == torch.int32)
-        self._zero_f32 = torch.zeros(max(nf, 64), device=self.device, dtype=torch.float32)
-        self._zero_i32 = torch.zeros(max(ni, 64), device=self.device, dtype=torch.int32)
-        of = oi = 0
-        for v in self._zero_specs:
-            n = int(np.prod(v.shape))
-            if v.dtype == torch.float32:
-                v.bind(self._zero_f32[of:of + n].view(v.shape))
-                of += pad_to(n, 64)
-            else:
-                v.bind(self._zero_i32[oi:oi + n].view(v.shape))
-                oi += pad_to(n, 64)
+        # one backing buffer per dtype (fp64 BN replica sums, fp32 workspaces, int32 counters)
+        for dt in sorted({v.dtype for v in self._zero_specs}, key=str):
+            specs = [v for v in self._zero_specs if v.dtype == dt]
+            n_tot = sum(pad_to(int(np.prod(v.shape)), 64) for v in specs)
+            buf = torch.zeros(max(n_tot, 64), device=self.device, dtype=dt)
+            self._zero[dt] = buf
+            o = 0
+            for v in specs:
+                n = int(np.prod(v.shape))
+                v.bind(buf[o:o + n].view(v.shape))
+                o += pad_to(n, 64)
 
     def clear(self):
-        self._zero_f32.zero_()
-        self._zero_i32.zero_()
+        for buf in self._zero.values():
+            buf.zero_()
 
 
 class LazyView:
@@ -269,8 +266,9 @@ class BNLayer:
         rs = flat.bn_stride(mods)
         if self.G > 1 and rs != self.pstride:
             raise ValueError("BN running-stat stride must equal the affine-parameter stride")
-        self.stats = arena.zeroed((self.G, NREP, 2, self.C))
-        self.ws = arena.zeroed((self.G, NREP, 2, self.C))
+        # fp64 replica sums: summation order no longer perturbs results (csrc/common.h BNArgs::stats)
+        self.stats = arena.zeroed((self.G, NREP, 2, self.C), torch.float64)
+        self.ws = arena.zeroed((self.G, NREP, 2, self.C), torch.float64)
         self.ws2 = None  # allocated on demand (second BN of a residual tail shares the dz)
 
     def args(self, training: bool) -> dict:

@@ -18,6 +18,11 @@ import torch
 from ..ops.hip import lib
 
 CONV_CFGS = list(range(14))
+
+
+def fused_max_m(kind: int) -> int:
+    """csrc/bn.hip tail_bwd_fused_kernel: 1024 threads x <= 4 register-cached pixels (2 for ADD_RELU)."""
+    return 1024 * (2 if kind == 4 else 4)
 WGRAD_CFGS = list(range(8))
 _CACHE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_cfgs.json")
 
@@ -106,7 +111,31 @@ def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, ve
                     print(f"tuned {sig}: cfg {best} ({best_t * 1e3:.1f} us)", flush=True)
             conv.set_wgrad_cfg(cache[sig])
             launch.args = (cache[sig], G, d)
+    # BN backward: reduce + apply (grid over pixels, replica atomics) vs the single-launch variant
+    # (one block per 8 channels over all pixels) -- the crossover depends on M, C and the sources
+    for ph in phases:
+        for launch in ph.launches:
+            if not launch.name.startswith("tailbwd"):
+                continue
+            kind, G, blocks, d = launch.args
+            sig = tail_bwd_signature(kind, G, d)
+            if sig not in cache and not measure:
+                continue
+            if sig not in cache:
+                fusable = d["B"] * d["H"] * d["W"] <= fused_max_m(kind)
+                ts = [_time(lambda: L.tail_bwd(kind, G, blocks, torch.cuda.current_stream().cuda_stream,
+                                                dict(d, fused=f))) if (f == 0 or fusable) else float("inf")
+                      for f in (0, 1)]
+                cache[sig] = int(ts[1] < ts[0])
+                if verbose:
+                    print(f"tuned {sig}: fused={cache[sig]} ({ts[0] * 1e3:.1f} / {ts[1] * 1e3:.1f} us)", flush=True)
+            d["fused"] = cache[sig]
     return cache
+
+
+def tail_bwd_signature(kind: int, G: int, d: dict) -> str:
+    return (f"tailbwd|k{kind}|G{G}|{d['B']},{d['H']},{d['W']},{d['C']}|src{len(d['g'])}"
+            f"|bn2{int('bn2' in d)}|side{int(bool(d.get('side')))}")
 
 
 def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False, measure: bool = True) -> Dict[str, int]:

@@ -92,6 +92,8 @@ class WgradCall:
 
 
 def prepare_conv2d(x, w, bias=None, stride=1, padding=0, stats=None, x2=None, cfg=None) -> ConvCall:
+    if stats is not None and stats.dtype != torch.float64:
+        raise TypeError("BN statistic replicas are fp64 ([NREP, 2, Co])")
     _check(x, torch.bfloat16)
     C1 = x2.shape[-1] if x2 is not None else 0
     Cs = x.shape[-1] + C1
@@ -113,7 +115,7 @@ def prepare_conv2d(x, w, bias=None, stride=1, padding=0, stats=None, x2=None, cf
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0,
            stats: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
     """NHWC bf16 convolution.  ``x2`` (optional) is a second input whose channels are concatenated after
-    ``x``'s (the kernel reads both without materialising the concat).  ``stats`` ([NREP, 2, Co] fp32,
+    ``x``'s (the kernel reads both without materialising the concat).  ``stats`` ([NREP, 2, Co] fp64,
     zero-initialised by the caller) receives per-channel sums of the output and its square."""
     return prepare_conv2d(x, w, bias, stride, padding, stats, x2, cfg).run()
 
@@ -196,6 +198,8 @@ ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
 def bn_args(stats, gamma, beta, run_mean, run_var, nbt, count, eps=1e-5, momentum=0.1, training=True):
     """Kernel BN descriptor.  The dict keeps references to the tensors it points at (``_keep``) so that
     they cannot be freed while a launch may still use them."""
+    if stats.dtype != torch.float64:
+        raise TypeError("BN statistic replicas are fp64 ([NREP, 2, C])")
     return {"_keep": (stats, gamma, beta, run_mean, run_var, nbt),"stats": ptr(stats), "gamma": ptr(gamma), "beta": ptr(beta), "run_mean": ptr(run_mean),
             "run_var": ptr(run_var), "nbt": ptr(nbt) if nbt is not None else 0, "pstride": 0, "C": gamma.numel(),
             "count": count, "eps": eps, "momentum": momentum, "training": 1 if training else 0}
@@ -220,14 +224,15 @@ def bn_tail(kind: int, y: torch.Tensor, bn: dict, r: Optional[torch.Tensor] = No
 
 def bn_tail_backward(kind: int, y: torch.Tensor, bn: dict, grads: Sequence[torch.Tensor], dgamma, dbeta,
                      r: Optional[torch.Tensor] = None, bn2: Optional[dict] = None, dgamma2=None, dbeta2=None,
-                     blocks: int = 64):
-    """Returns ``(dy bf16, side fp32 | None, dy2 bf16 | None)``; writes dgamma/dbeta (and 2) in place."""
+                     blocks: int = 64, fused: bool = False):
+    """Returns ``(dy bf16, side fp32 | None, dy2 bf16 | None)``; writes dgamma/dbeta (and 2) in place.
+    ``fused``: single-launch variant (block per 8 channels over all pixels) instead of reduce + apply."""
     B, H, W, C = y.shape
-    ws = torch.zeros(1, NREP, 2, C, device=y.device)
+    ws = torch.zeros(1, NREP, 2, C, device=y.device, dtype=torch.float64)
     dy = torch.empty_like(y)
     d = {"y": ptr(y), "ldy": C, "bn": bn, "B": B, "H": H, "W": W, "C": C,
          "g": [(ptr(g), 0, g.shape[-1]) for g in grads], "ws": ptr(ws), "dy": ptr(dy), "ldd": C,
-         "dgamma": ptr(dgamma), "dbeta": ptr(dbeta)}
+         "dgamma": ptr(dgamma), "dbeta": ptr(dbeta), "fused": int(fused)}
     side = dy2 = None
     if r is not None:
         d.update({"r": ptr(r), "ldr": r.shape[-1]})
@@ -235,7 +240,7 @@ def bn_tail_backward(kind: int, y: torch.Tensor, bn: dict, grads: Sequence[torch
         side = torch.empty(B, H, W, C, device=y.device, dtype=torch.float32)
         d.update({"side": ptr(side), "lds": C})
     if bn2 is not None:
-        ws2 = torch.zeros(1, NREP, 2, C, device=y.device)
+        ws2 = torch.zeros(1, NREP, 2, C, device=y.device, dtype=torch.float64)
         dy2 = torch.empty_like(y)
         d.update({"bn2": bn2, "ws2": ptr(ws2), "dy2": ptr(dy2), "ldd2": C, "dgamma2": ptr(dgamma2),
                   "dbeta2": ptr(dbeta2)})

@@ -139,9 +139,10 @@ def test_adam_matches_torch():
 
 
 def test_graph_replay_matches_eager():
-    """HIP-graph replay must reproduce eager execution.  BN statistics use fp32 atomics (order-dependent in
-    the last bit), so one step's gradients are compared against the run-to-run spread of two eager runs;
-    over several steps Adam amplifies that noise, so the multi-step check is loose."""
+    """HIP-graph replay must reproduce eager execution BITWISE, and so must two eager runs: the only
+    cross-block reductions are the BN replica sums, accumulated in fp64 so their atomic order cannot
+    change a rounded result (with fp32 sums the chaotic-at-init network turned order noise into run-to-run
+    gradient differences of up to 12%)."""
     from mtl_das_pytorch_amd.engine.step import StepRunner
     from mtl_das_pytorch_amd.models import MTL_Net
     model, ref, prog, X, labels = _setup(MTL_Net)
@@ -170,6 +171,6 @@ def test_graph_replay_matches_eager():
     base = rel(grads[1], grads[0])
     d = rel(grads[2], grads[0])
     print(f"one-step gradients: eager-vs-eager {base:.3e}  graph-vs-eager {d:.3e}")
-    assert d < 5 * base + 2e-3
+    assert torch.equal(grads[1], grads[0]) and torch.equal(grads[2], grads[0])
     assert params[2][1] == 3.0
-    assert rel(params[2][0], params[0][0]) < 0.05
+    assert torch.equal(params[2][0], params[0][0]) and torch.equal(params[1][0], params[0][0])

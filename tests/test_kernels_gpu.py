@@ -64,7 +64,7 @@ def _mk(case, dev="cuda", seed=0):
 def test_conv_forward_and_stats(fn, case):
     x, w, b, s, p = _mk(case)
     ref = F.conv2d(x, w, b, stride=s, padding=p)
-    stats = torch.zeros(NREP, 2, w.shape[0], device="cuda")
+    stats = torch.zeros(NREP, 2, w.shape[0], device="cuda", dtype=torch.float64)
     y = fn.conv2d(nhwc(x).bfloat16(), w, b, stride=s, padding=p, stats=stats)
     assert y.shape == nhwc(ref).shape
     assert rel(nchw(y), ref) < 6e-3
@@ -134,7 +134,7 @@ def _bn_setup(fn, y_ref, C, eps=1e-5, seed=0):
     beta = (0.2 * torch.randn(C, generator=g)).cuda()
     rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
     nbt = torch.zeros(1, device="cuda", dtype=torch.int64)
-    stats = torch.zeros(NREP, 2, C, device="cuda")
+    stats = torch.zeros(NREP, 2, C, device="cuda", dtype=torch.float64)
     stats[0, 0] = y_ref.sum((0, 2, 3))
     stats[0, 1] = (y_ref * y_ref).sum((0, 2, 3))
     cnt = y_ref.numel() // C
@@ -147,9 +147,10 @@ def _torch_bn(y, gamma, beta, eps=1e-5):
     return F.batch_norm(y, None, None, gamma, beta, training=True, eps=eps)
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("C", [8, 16, 48, 128])
-def test_bn_tail_forward_backward(fn, kind, C):
+def test_bn_tail_forward_backward(fn, kind, C, fused):
     g = torch.Generator().manual_seed(10 + kind)
     B, H, W = 4, 9, 21
     y = (torch.randn(B, C, H, W, generator=g) * 2 + 0.5).bfloat16().float().cuda()
@@ -184,7 +185,7 @@ def test_bn_tail_forward_backward(fn, kind, C):
     out.backward(go)
     dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
     dy, side, _ = fn.bn_tail_backward(kind, nhwc(y).bfloat16(), bn, [nhwc(go).contiguous()], dg, db,
-                                      r=nhwc(r).bfloat16() if kind in (3, 4) else None)
+                                      r=nhwc(r).bfloat16() if kind in (3, 4) else None, fused=fused)
     assert rel(nchw(dy), yr.grad) < 1e-2
     assert rel(dg, gam.grad) < 1e-2
     assert rel(db, bet.grad) < 1e-2
@@ -192,9 +193,10 @@ def test_bn_tail_forward_backward(fn, kind, C):
         assert rel(nchw(side), rr.grad) < 1e-2
 
 
-def test_bn_residual_projection(fn):
+@pytest.mark.parametrize("fused", [False, True])
+def test_bn_residual_projection(fn, fused):
     g = torch.Generator().manual_seed(20)
-    B, C, H, W = 4, 32, 17, 42
+    B, C, H, W = (4, 32, 9, 21) if fused else (4, 32, 17, 42)  # single launch: <= 2048 pixels
     y = torch.randn(B, C, H, W, generator=g).bfloat16().float().cuda()
     y2 = (torch.randn(B, C, H, W, generator=g) + 1).bfloat16().float().cuda()
     bn, gamma, beta, *_ = _bn_setup(fn, y, C, seed=1)
@@ -208,7 +210,7 @@ def test_bn_residual_projection(fn):
     out.backward(go)
     d = [torch.zeros(C, device="cuda") for _ in range(4)]
     dy, _, dy2 = fn.bn_tail_backward(4, nhwc(y).bfloat16(), bn, [nhwc(go)], d[0], d[1], r=nhwc(y2).bfloat16(),
-                                     bn2=bn2, dgamma2=d[2], dbeta2=d[3])
+                                     bn2=bn2, dgamma2=d[2], dbeta2=d[3], fused=fused)
     assert rel(nchw(dy), yr.grad) < 1e-2
     assert rel(nchw(dy2), y2r.grad) < 1e-2
     for a, b in zip(d, gs):
@@ -221,7 +223,7 @@ def test_bn_eval_mode(fn):
     y = torch.randn(2, C, 9, 21, generator=g).bfloat16().float().cuda()
     gamma, beta = torch.rand(C).cuda() + 0.5, torch.randn(C).cuda()
     rm, rv = torch.randn(C).cuda(), torch.rand(C).cuda() + 0.5
-    st = torch.zeros(NREP, 2, C, device="cuda")
+    st = torch.zeros(NREP, 2, C, device="cuda", dtype=torch.float64)
     bn = fn.bn_args(st, gamma, beta, rm, rv, None, 1, training=False)
     out = fn.bn_tail(1, nhwc(y).bfloat16(), bn)
     ref = F.relu(F.batch_norm(y, rm, rv, gamma, beta, training=False))

@@ -48,7 +48,7 @@ for name, (H, W, Ci, Co, k, s, p) in SHAPES.items():
     w = torch.randn(Co, Ci, k, k, device="cuda") * 0.1
     Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
     dy = torch.randn(B, Ho, Wo, Co, device="cuda").bfloat16()
-    stats = torch.zeros(32, 2, Co, device="cuda")
+    stats = torch.zeros(32, 2, Co, device="cuda", dtype=torch.float64)
     r = {}
     for cfg in range(int(os.environ.get("NCFG", 5))):
         try:

@@ -3,7 +3,7 @@ sys.path.insert(0, '.')
 from mtl_das_pytorch_amd.ops import functional as fn
 C=8; B,H,W=4,9,21
 y = (torch.randn(B, C, H, W) * 2 + 0.5).bfloat16().float().cuda()
-stats = torch.zeros(8, 2, C, device="cuda")
+stats = torch.zeros(8, 2, C, device="cuda", dtype=torch.float64)
 stats[0, 0] = y.sum((0, 2, 3)); stats[0, 1] = (y * y).sum((0, 2, 3))
 gamma = torch.ones(C, device="cuda"); beta = torch.zeros(C, device="cuda")
 rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")

@@ -1,0 +1,8 @@
+source tools/gpu_round.sh
+export TAILN=8
+step ph timeout -k 10 200 python tools/bench_tails.py phases
+step gputests timeout -k 10 900 python -m pytest tests -m gpu -x -q
+rm -f gpurun_out/tuned_cfgs.json
+step benchA timeout -k 10 300 python bench.py --steps 200 --warmup 20
+cp gpurun_out/tuned_cfgs.json mtl_das_pytorch_amd/engine/tuned_cfgs.json || true
+step benchC timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 10

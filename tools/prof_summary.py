@@ -21,6 +21,23 @@ for r in rows:
     n = r["Kernel_Name"].split("(")[0][:70]
     tot[n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     cnt[n] += 1
+# steady state: the last 10 complete steps (windows between consecutive gather launches)
+gi = [i for i, r in enumerate(rows) if "gather_batch" in r["Kernel_Name"]]
+if len(gi) >= 12:
+    win = rows[gi[-11]:gi[-1]]
+    wt = collections.defaultdict(float)
+    wc = collections.Counter()
+    for r in win:
+        n = r["Kernel_Name"].split("(")[0][:70]
+        wt[n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        wc[n] += 1
+    WS = sum(wt.values())
+    span = (int(win[-1]["End_Timestamp"]) - int(win[0]["Start_Timestamp"])) / 1e3
+    print(f"steady state (last 10 steps): {len(win) / 10:.0f} kernels/step, busy {WS / 10:.1f} us/step, "
+          f"span {span / 10:.1f} us/step")
+    for n, t in sorted(wt.items(), key=lambda x: -x[1])[:30]:
+        print(f"{t / 10:8.1f} us/step {100 * t / WS:5.1f}%  {wc[n] / 10:5.1f} calls/step  {t / wc[n]:6.1f} us/call  {n}")
+    print()
 S = sum(tot.values())
 print(f"kernel time total {S/1e3:.2f} ms over {steps} steps -> {S/steps:.1f} us/step")
 for n, t in sorted(tot.items(), key=lambda x: -x[1])[:25]:
