@@ -41,6 +41,7 @@ from ..utils.config import TrainConfig
 from ..utils.logger import Logger
 from ..utils.metrics import format_task_report, mae_from_confusion, metrics_from_confusion
 from ..utils.plots import plot_confusion_files, plot_curves
+from ..utils.profiling import phase_range
 from .backends import EngineBackend, Metrics, TorchBackend, reduce_metrics
 
 
@@ -97,9 +98,18 @@ class Trainer:
             self.ctx.broadcast_(t)
             stamp = datetime.datetime.fromtimestamp(float(t.item())).strftime("%m-%d-%H_%M_%S")
         self.save_dir = os.path.join(cfg.output_savedir, "{} {}".format(stamp, note)) + "/"
+        self.resume_path = None
+        if cfg.resume == "auto":
+            # elastic restart: continue the newest run of this model type in the same directory
+            self.resume_path = find_latest_resume(cfg.output_savedir, cfg.model)
+            if self.resume_path:
+                self.save_dir = os.path.dirname(self.resume_path) + "/"
+        elif cfg.resume:
+            self.resume_path = cfg.resume
         if self.is_main:
             os.makedirs(self.save_dir, exist_ok=True)
-        self.logger = Logger("console output.log", self.save_dir, enabled=self.is_main)
+        self.logger = Logger("console output.log", self.save_dir, enabled=self.is_main,
+                             append=self.resume_path is not None)
         if cfg.model_path and cfg.is_test:
             sd = torch.load(cfg.model_path, map_location="cpu", weights_only=True)
             self.model.load_state_dict(sd, strict=True)
@@ -109,8 +119,10 @@ class Trainer:
         c = self.cfg
         if c.backend == "torch" or self.device.type != "cuda":
             return "torch"
-        if c.backend == "engine":
-            return "engine"
+        if c.sync_bn:
+            if c.backend == "engine":
+                raise ValueError("--sync_bn is implemented by the torch backend (--dtype fp32)")
+            return "torch"
         return "engine"
 
     def print(self, *a, **k):
@@ -130,36 +142,40 @@ class Trainer:
             self.model.to(self.device)
             self.backend = EngineBackend(self.model, cfg.model, X, Y, Xv, Yv, use_graph=cfg.graph, tune=cfg.tune, **kw)
         else:
+            if cfg.sync_bn and self.ctx.enabled:
+                self.model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(self.model)
             self.model.to(self.device)
             self.backend = TorchBackend(self.model, cfg.model, X, Y, Xv, Yv, **kw)
         self.n_train, self.n_val = len(X), len(Xv)
         self.print(f"backend: {self.backend_name}  device: {self.device}  world: {self.ctx.world}  "
                    f"train samples: {0 if cfg.is_test else self.n_train}  val samples: {self.n_val}")
-        start_epoch, lr = 0, cfg.lr
-        if cfg.resume:
-            start_epoch, lr = self._load_resume(cfg.resume)
-        self.lr = lr
-        self.backend.set_lr(lr)
+        start_epoch, lr, val_done = 0, cfg.lr, False
         self.curves = {"trainAccLine": [[], []], "trainLossLine": [[], []], "testAccLine": [[], []],
                        "testLossLine": [[], []]}
+        if self.resume_path:
+            start_epoch, lr, val_done = self._load_resume(self.resume_path)
+        self.lr = lr
+        self.backend.set_lr(lr)
+        self.global_step = 0
+        self.fault = parse_fault_injection(self.ctx.rank)
         self.start_time = datetime.datetime.now()
         if cfg.model == "multi_classifier":
             self.print("{}：{}".format("Start Test" if cfg.is_test else "Start Training", self.start_time))
         sampler = ShardedIndexSampler(self.n_train, cfg.batch_size, self.ctx, shuffle=True, seed=cfg.seed)
         E = cfg.epoch_num
         for epoch in range(start_epoch, E + 1):
-            if epoch % cfg.val_every == 0:
-                resumed_here = cfg.resume and epoch == start_epoch
-                if not resumed_here and (cfg.model != "multi_classifier" or epoch != 0):
+            if epoch % cfg.val_every == 0 and not (epoch == start_epoch and val_done):
+                if cfg.model != "multi_classifier" or epoch != 0:
                     self.lr /= cfg.lr_decay
                     self.backend.set_lr(self.lr)
                 self.validate(epoch)
-                self._save_resume(epoch)
+                self._save_resume(epoch, val_done=True)
                 if cfg.is_test:
                     break
             if epoch < E:
                 self.train_epoch(epoch, sampler)
                 self.print("Epoch {} finished！".format(epoch + 1))
+                self._save_resume(epoch + 1, val_done=False)
         if self.is_main:
             if cfg.is_test:
                 plot_confusion_files(self.save_dir)
@@ -186,8 +202,23 @@ class Trainer:
         batches = sampler.epoch(epoch, self.device)
         be.reset_metrics()
         last = be.read_metrics()
+        prof = self._maybe_profiler(epoch)
+        t_log = time.perf_counter()
         for bi, idx in enumerate(batches):
-            be.train_batch(idx)
+            if self.fault is not None and self.global_step == self.fault:
+                print(f"fault injection: rank {self.ctx.rank} exits at global step {self.global_step}",
+                      file=sys.stderr, flush=True)
+                self.logger.flush()
+                os._exit(13)
+            with phase_range("train_step"):
+                be.train_batch(idx)
+            self.global_step += 1
+            if prof is not None:
+                prof.step()
+                if bi + 1 >= cfg.profile_steps:
+                    prof.stop()
+                    prof = None
+                    self.print(f"profiler trace written to {self.save_dir}")
             if (bi + 1) % cfg.log_every == 0:
                 now = be.read_metrics()
                 delta = reduce_metrics(self.ctx, now - last)
@@ -200,6 +231,12 @@ class Trainer:
                     loss = [loss[0], loss[0]]
                 self.print("epoch-iteration:{}-{}, loss:{}, accuracy:{}".format(epoch + 1, bi + 1, loss, acc))
                 self.print("time:{}".format(datetime.datetime.now() - self.start_time))
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize()
+                dt = time.perf_counter() - t_log
+                t_log = time.perf_counter()
+                self.print("throughput: {:.1f} samples/s ({} GPU(s), {:.3f} ms/step)".format(
+                    cfg.log_every * cfg.batch_size * self.ctx.world / dt, self.ctx.world, 1e3 * dt / cfg.log_every))
                 for t in range(2):
                     self.curves["trainLossLine"][t].append(loss[min(t, nt - 1)])
                     self.curves["trainAccLine"][t].append(acc[min(t, nt - 1)])
@@ -268,27 +305,76 @@ class Trainer:
         self.ctx.barrier()
 
     # --------------------------------------------------------------------------------------------
-    def _save_resume(self, epoch: int):
-        """Resumable sidecar (never inside the reference-format .pth): weights, optimizer moments, epoch,
-        LR and RNG state, written by rank 0 after every validation."""
+    def _maybe_profiler(self, epoch: int):
+        """--profile_steps N: torch.profiler (Kineto/roctracer on ROCm) over the first N train steps of
+        the first trained epoch, exported as a chrome trace into the run directory (rank 0)."""
+        n = self.cfg.profile_steps
+        if n <= 0 or not self.is_main or getattr(self, "_profiled", False):
+            return None
+        self._profiled = True
+        acts = [torch.profiler.ProfilerActivity.CPU]
+        if self.device.type == "cuda":
+            acts.append(torch.profiler.ProfilerActivity.CUDA)
+        path = os.path.join(self.save_dir, f"trace_epoch{epoch}.json")
+        prof = torch.profiler.profile(activities=acts, on_trace_ready=lambda p: p.export_chrome_trace(path))
+        prof.start()
+        return prof
+
+    def _save_resume(self, epoch: int, val_done: bool):
+        """Resumable sidecar (never inside the reference-format .pth): weights, optimizer moments, next
+        epoch, whether that epoch's validation (and LR decay) already ran, LR, RNG state and curves.
+        Written atomically by rank 0 after every validation and every training epoch."""
         if not self.is_main or self.cfg.is_test:
             return
-        st = {"epoch": epoch, "lr": self.lr, "model": {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()},
+        st = {"epoch": epoch, "val_done": val_done, "lr": self.lr,
+              "model": {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()},
               "optimizer": self.backend.optimizer_state(), "rng": torch.get_rng_state(),
-              "curves": self.curves, "model_type": self.cfg.model}
+              "curves": self.curves, "model_type": self.cfg.model, "global_step": self.global_step}
         tmp = os.path.join(self.save_dir, "last.resume.pt.tmp")
         torch.save(st, tmp)
-        os.replace(tmp, os.path.join(self.save_dir, "last.resume.pt"))
+        os.replace(tmp, os.path.join(self.save_dir, RESUME_NAME))
 
     def _load_resume(self, path: str):
         st = torch.load(path, map_location="cpu", weights_only=True)
+        if st.get("model_type", self.cfg.model) != self.cfg.model:
+            raise ValueError(f"{path} holds a {st['model_type']} run, not {self.cfg.model}")
         self.model.load_state_dict(st["model"], strict=True)
         self.backend.load_optimizer_state(st["optimizer"])
         if hasattr(self.backend, "after_load"):
             self.backend.after_load()
         torch.set_rng_state(st["rng"])
+        if "curves" in st:
+            self.curves = st["curves"]
         self.print(f"resumed from {path} at epoch {st['epoch']} (lr {st['lr']})")
-        return int(st["epoch"]), float(st["lr"])
+        return int(st["epoch"]), float(st["lr"]), bool(st.get("val_done", True))
+
+
+RESUME_NAME = "last.resume.pt"
+
+
+def find_latest_resume(root: str, model_type: str) -> Optional[str]:
+    """Newest ``last.resume.pt`` of a ``model_type`` run directly under ``root`` (training runs only)."""
+    best, best_t = None, -1.0
+    if not os.path.isdir(root):
+        return None
+    for d in os.listdir(root):
+        p = os.path.join(root, d, RESUME_NAME)
+        if f"model_type={model_type} is_test=False" in d and os.path.isfile(p):
+            t = os.path.getmtime(p)
+            if t > best_t:
+                best, best_t = p, t
+    return best
+
+
+def parse_fault_injection(rank: int) -> Optional[int]:
+    """MDA_FAULT_INJECT="rank=R,step=S": rank R exits (status 13) before global train step S -- only in
+    the first attempt of an elastic job (TORCHELASTIC_RESTART_COUNT 0), so a restarted job runs through
+    (SURVEY 5.3)."""
+    spec = os.environ.get("MDA_FAULT_INJECT")
+    if not spec or int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) > 0:
+        return None
+    kv = dict(item.split("=") for item in spec.split(","))
+    return int(kv["step"]) if int(kv.get("rank", 0)) == rank else None
 
 
 def main_process(cfg: TrainConfig) -> str:

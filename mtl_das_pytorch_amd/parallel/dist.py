@@ -68,8 +68,14 @@ class DistContext:
         return float(t.item())
 
 
-def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> DistContext:
-    """Initialise from torchrun's environment (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*)."""
+def init_distributed(backend: Optional[str] = None, timeout_s: Optional[int] = None) -> DistContext:
+    """Initialise from torchrun's environment (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*).
+
+    Failure detection: collectives time out after ``timeout_s`` (env ``MDA_PG_TIMEOUT``, default 600 s)
+    instead of hanging when a peer dies, so the rank errors out and torchrun's elastic agent
+    (``--max-restarts``) can restart the worker group, which resumes with ``--resume auto``."""
+    if timeout_s is None:
+        timeout_s = int(os.environ.get("MDA_PG_TIMEOUT", "600"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -82,6 +88,10 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600) -> Dis
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     backend = backend or ("nccl" if use_gpu else "gloo")
+    if backend == "gloo" and os.environ["MASTER_ADDR"] in ("127.0.0.1", "localhost"):
+        # single-node gloo over loopback: the host name may not resolve (containers), and gloo's
+        # interface guess then makes a restarted group's full-mesh connect fail intermittently
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
     if not dist.is_initialized():
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":

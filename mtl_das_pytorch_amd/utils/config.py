@@ -57,7 +57,11 @@ class TrainConfig:
     seed: int = 0
     graph: bool = True
     tune: bool = False
-    resume: Optional[str] = None
+    resume: Optional[str] = None          # path to a *.resume.pt sidecar, or "auto" (newest under output_savedir)
+    dtype: Optional[str] = None           # bf16 -> HIP engine, fp32 -> plain PyTorch (alias of --backend)
+    sync_bn: bool = False                 # all-reduce BN batch statistics across ranks (torch backend)
+    profile_steps: int = 0                # >0: torch.profiler trace of that many train steps (rank 0)
+    debug: bool = False                   # serialised kernels + blocking launches, no HIP graphs
     is_test: bool = False
 
     @property
@@ -107,7 +111,16 @@ def build_parser(is_test: bool) -> argparse.ArgumentParser:
     g.add_argument("--seed", type=int, default=0)
     g.add_argument("--graph", type=str2bool, default=True, help="capture each step into a HIP graph")
     g.add_argument("--tune", type=str2bool, default=False, help="autotune kernel configs at start-up")
-    g.add_argument("--resume", type=str, default=None, help="resume from a *.resume.pt sidecar")
+    g.add_argument("--resume", type=str, default=None,
+                   help="resume from a *.resume.pt sidecar; 'auto' = newest sidecar of this model under "
+                        "--output_savedir (elastic restarts), fresh start if none")
+    g.add_argument("--dtype", choices=["bf16", "fp32"], default=None,
+                   help="compute dtype: bf16 = HIP engine, fp32 = plain PyTorch (overrides --backend)")
+    g.add_argument("--sync_bn", type=str2bool, default=False,
+                   help="synchronise BN batch statistics across ranks (torch backend, GPU process groups)")
+    g.add_argument("--profile_steps", type=int, default=0, help="write a torch.profiler trace of N train steps")
+    g.add_argument("--debug", type=str2bool, default=False,
+                   help="debug mode: AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING=1, no HIP graphs")
     return ap
 
 
@@ -119,4 +132,22 @@ def config_from_args(args: argparse.Namespace, is_test: bool) -> TrainConfig:
     if not is_test:
         d["model_path"] = None  # reference train.py passes pth_file=None (train.py:35)
     d["is_test"] = is_test
+    if d.get("dtype") == "bf16":
+        d["backend"] = "engine"
+    elif d.get("dtype") == "fp32":
+        d["backend"] = "torch"
+    if d.get("debug"):
+        d["graph"] = False
     return TrainConfig(**d)
+
+
+def apply_debug_env(argv) -> None:
+    """--debug must take effect before the HIP runtime initialises: called by train.py / test.py before
+    importing torch.  Serialised kernels + blocking launches make a faulting kernel report at its own
+    launch."""
+    import os
+    for i, a in enumerate(argv):
+        val = a.split("=", 1)[1] if a.startswith("--debug=") else (argv[i + 1] if a == "--debug" and i + 1 < len(argv) else None)
+        if val is not None and str2bool(val):
+            os.environ.setdefault("AMD_SERIALIZE_KERNEL", "3")
+            os.environ.setdefault("HIP_LAUNCH_BLOCKING", "1")

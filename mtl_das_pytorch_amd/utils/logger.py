@@ -12,7 +12,10 @@ import sys
 
 
 class Logger:
-    def __init__(self, filename: str = "Default.log", path: str = "./", terminal=None, enabled: bool = True):
+    def __init__(self, filename: str = "Default.log", path: str = "./", terminal=None, enabled: bool = True,
+                 append: bool = True):
+        """The log file is written incrementally (the reference keeps it in memory until the end and
+        loses it on a crash); an elastic restart (``append``) continues the same file."""
         self.terminal = terminal if terminal is not None else sys.stdout
         self.filename = filename
         self.path = path
@@ -20,7 +23,7 @@ class Logger:
         self._fh = None
         if enabled:
             os.makedirs(path, exist_ok=True)
-            self._fh = open(os.path.join(path, filename), "a", encoding="utf-8")
+            self._fh = open(os.path.join(path, filename), "a" if append else "w", encoding="utf-8")
 
     def write(self, message: str):
         self.terminal.write(message)

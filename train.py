@@ -11,8 +11,11 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+from mtl_das_pytorch_amd.utils.config import apply_debug_env, build_parser, config_from_args  # noqa: E402
+
+apply_debug_env(sys.argv)  # before anything initialises the HIP runtime
+
 from mtl_das_pytorch_amd.engine.trainer import main_process  # noqa: E402
-from mtl_das_pytorch_amd.utils.config import build_parser, config_from_args  # noqa: E402
 
 if __name__ == "__main__":
     args = build_parser(is_test=False).parse_args()
