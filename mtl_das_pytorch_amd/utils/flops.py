@@ -81,3 +81,33 @@ def complexity_report(input_res=(1, 100, 250)) -> dict:
     return {"macs": {"A": a, "B_distance": bd, "B_event": be, "C": c},
             "params": {"A": pa, "B_distance": pbd, "B_event": pbe, "C": pc},
             "ratio_A_over_2B": a / (bd + be), "ratio_A_over_C": a / c}
+
+
+def main(argv=None):
+    """``python -m mtl_das_pytorch_amd.utils.flops [--model M] [--per_layer]``: the ptflops-style report the
+    reference prints (commented out at utils.py:127-131), plus the README's 67.8 % / 19.8 % ratios."""
+    import argparse
+    import json
+    ap = argparse.ArgumentParser(description=main.__doc__)
+    ap.add_argument("--model", default=None, help="MTL | single_distance | single_event | multi_classifier")
+    ap.add_argument("--input_res", default="1,100,250")
+    ap.add_argument("--per_layer", action="store_true")
+    args = ap.parse_args(argv)
+    res = tuple(int(x) for x in args.input_res.split(","))
+    if args.model is None:
+        print(json.dumps(complexity_report(res), indent=1))
+        return
+    from ..models import build_model
+    m = build_model(args.model, in_channels=res[0])
+    if args.per_layer:
+        macs, params, per = count_macs(m, res, per_layer=True)
+        for name, v in per.items():
+            print(f"{name:60s} {v / 1e6:10.3f} MMac")
+    else:
+        macs, params = count_macs(m, res)
+    print(f"Computational complexity: {macs / 1e9:.3f} GMac")
+    print(f"Number of parameters: {params / 1e6:.3f} M")
+
+
+if __name__ == "__main__":
+    main()
