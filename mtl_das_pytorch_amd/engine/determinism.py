@@ -18,7 +18,8 @@ def check_step(prog, X: torch.Tensor, labels: torch.Tensor, idx: torch.Tensor, u
                runs: int = 2) -> Dict[str, object]:
     from .step import StepRunner
     f = prog.flat
-    state = [f.params, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step]
+    state = [f.params, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step] + \
+        list(getattr(prog, "extra_state", []))  # e.g. Model C's dropout RNG counter
     saved = [t.clone() for t in state]
     grads, outs = [], []
     for _ in range(runs):
