@@ -102,7 +102,37 @@ void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
   check(launch_conv(mode, a, G, cfg, S(stream)), "conv");
 }
 
+WgradArgs parse_wgrad(const py::dict& d);
+
 void wgrad(int cfg, int G, int64_t stream, py::dict d) {
+  check(launch_wgrad(parse_wgrad(d), G, cfg, S(stream)), "wgrad");
+}
+
+// Packs the WgradJob table of a batched weight-gradient launch; returns (bytes, total blocks).
+py::tuple wgrad_table(int cfg, py::list dicts, py::list groups) {
+  int TN, TK;
+  if (wgrad_tile_shape(cfg, TN, TK)) throw std::runtime_error("wgrad_table: bad cfg");
+  std::vector<WgradJob> jobs(dicts.size());
+  int64_t b0 = 0;
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    WgradJob& j = jobs[i];
+    j = WgradJob{};
+    j.a = parse_wgrad(dicts[i].cast<py::dict>());
+    j.G = groups[i].cast<int>();
+    j.ntiles = ((j.a.Npad + TN - 1) / TN) * (j.a.Kpad / TK);
+    if (j.a.Kpad % TK) throw std::runtime_error("wgrad_table: Kpad not a multiple of the tile");
+    j.block0 = b0;
+    b0 += (int64_t)j.ntiles * j.a.splits * j.G;
+  }
+  return py::make_tuple(py::bytes(reinterpret_cast<const char*>(jobs.data()), jobs.size() * sizeof(WgradJob)), b0);
+}
+
+void wgrad_batched(int cfg, int64_t table, int nj, int64_t nblocks, int64_t stream) {
+  check(launch_wgrad_batched(cfg, reinterpret_cast<const WgradJob*>(static_cast<intptr_t>(table)), nj, nblocks,
+                             S(stream)), "wgrad_batched");
+}
+
+WgradArgs parse_wgrad(const py::dict& d) {
   WgradArgs a{};
   a.src = parse_src(d["src"].cast<py::dict>());
   a.dy = P<const bf16_t>(d, "dy");
@@ -115,7 +145,7 @@ void wgrad(int cfg, int G, int64_t stream, py::dict d) {
   a.KH = (int)I(d, "KH"); a.KW = (int)I(d, "KW"); a.sh = (int)I(d, "sh"); a.sw = (int)I(d, "sw");
   a.ph = (int)I(d, "ph"); a.pw = (int)I(d, "pw"); a.Kpad = (int)I(d, "Kpad");
   if (a.Cs % 8 || a.Co % 8 || a.Kpad % 64) throw std::runtime_error("wgrad: bad geometry");
-  check(launch_wgrad(a, G, cfg, S(stream)), "wgrad");
+  return a;
 }
 
 void wgrad_finalize(int64_t descs, int nd, int64_t nblocks, double scale, int64_t stream) {
@@ -235,6 +265,8 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("cls_head", &cls_head);
   m.def("gather_batch", &gather_batch);
   m.def("pool3", &pool3);
+  m.def("wgrad_table", &wgrad_table);
+  m.def("wgrad_batched", &wgrad_batched);
   m.def("grad_sum", &grad_sum);
   m.def("adam_pack", &adam_pack);
   m.def("hip_device_sync", []() { return (int)hipDeviceSynchronize(); });

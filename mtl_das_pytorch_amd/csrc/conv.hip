@@ -260,7 +260,7 @@ DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
 // Global loads of chunk c+1 are issued into registers before the MFMAs of chunk c (which read LDS), so
 // the load latency overlaps compute; one LDS image per operand, two barriers per chunk.
 template <int TN, int TK, int MCH>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const int z) {
   constexpr int PAD = 8;  // rows stay 16-byte aligned (ds_write_b128 staging, 8-byte tr-read addresses)
   constexpr int LDY = TN + PAD, LDX = TK + PAD;
   __shared__ __attribute__((aligned(16))) bf16_t s_dy[MCH * LDY];
@@ -271,10 +271,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   constexpr int VY = MCH * (TN / 8), VX = MCH * (TK / 8);
   constexpr int NY = (VY + 255) / 256, NX = (VX + 255) / 256;
 
-  const int z = blockIdx.z;
-  const int split = blockIdx.y;
   const int ntk = a.Kpad / TK;
-  const int tn = blockIdx.x / ntk, tk = blockIdx.x - tn * ntk;
+  const int tn = tile / ntk, tk = tile - tn * ntk;
   const int n0 = tn * TN, k0 = tk * TK;
   const int Ktot = a.KH * a.KW * a.Cs;
   if (threadIdx.x < TK / 8) s_tab[threadIdx.x] = encode_kg(k0 / 8 + threadIdx.x, Ktot, a.Cs >> 3, a.KW, a.src.C0);
@@ -382,6 +380,27 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
+template <int TN, int TK, int MCH>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+  wgrad_block<TN, TK, MCH>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Horizontally batched weight gradients: every conv of a backward pass that uses this tile config, in
+// ONE launch.  The weight gradient of a layer only needs its dy and forward input, both resident until
+// the step ends, so all of them are deferred to the end of the backward pass; the ~40 (Model A) / ~90
+// (Model C) small launches become <= 8 large ones that fill the 256 CUs (the deep, small-M layers run
+// side by side instead of one after another).  Block -> job by binary search over the jobs' first blocks.
+template <int TN, int TK, int MCH>
+__global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob* __restrict__ jobs, int nj) {
+  int lo = 0, hi = nj - 1;
+  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
+  const WgradJob& J = jobs[lo];
+  const int local = (int)((int64_t)blockIdx.x - J.block0);
+  const int per_z = J.ntiles * J.a.splits;
+  const int z = local / per_z, r = local - z * per_z;
+  wgrad_block<TN, TK, MCH>(J.a, r % J.ntiles, r / J.ntiles, z);
+}
+
 // Sums the split-M partial slabs of many convolutions into the flat fp32 gradient buffer (deterministic,
 // one launch per backward), reference weight layout [Cout][Cin][KH][KW].
 __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale) {
@@ -478,6 +497,34 @@ int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st) {
     default: return -1;
   }
 #undef LAUNCH_WG
+  return (int)hipGetLastError();
+}
+
+int wgrad_tile_shape(int cfg, int& TN, int& TK) {
+  static const int tn[8] = {16, 32, 32, 64, 16, 16, 32, 64}, tk[8] = {32, 32, 64, 64, 64, 32, 32, 32};
+  if (cfg < 0 || cfg > 7) return -1;
+  TN = tn[cfg]; TK = tk[cfg];
+  return 0;
+}
+
+int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st) {
+  if (nblocks <= 0) return 0;
+  dim3 grid((unsigned)nblocks);
+#define LAUNCH_WGB(TN, TK, MCH)                                                                      \
+  hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, d_jobs, nj); \
+  break;
+  switch (cfg) {
+    case 0: LAUNCH_WGB(16, 32, 128)
+    case 1: LAUNCH_WGB(32, 32, 128)
+    case 2: LAUNCH_WGB(32, 64, 64)
+    case 3: LAUNCH_WGB(64, 64, 64)
+    case 4: LAUNCH_WGB(16, 64, 128)
+    case 5: LAUNCH_WGB(16, 32, 256)
+    case 6: LAUNCH_WGB(32, 32, 256)
+    case 7: LAUNCH_WGB(64, 32, 64)
+    default: return -1;
+  }
+#undef LAUNCH_WGB
   return (int)hipGetLastError();
 }
 

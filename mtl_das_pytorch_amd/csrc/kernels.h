@@ -40,6 +40,14 @@ struct WgradArgs {
   int Kpad;
 };
 
+// One conv of a horizontally batched weight-gradient launch (device table, built by wgrad_table).
+struct WgradJob {
+  WgradArgs a;
+  int ntiles;      // (Npad / TN) * (Kpad / TK)
+  int G;
+  int64_t block0;  // first block of this job in the batched grid
+};
+
 // Sums the split-M partial slabs of many convolutions and scatters them into the flat fp32 gradient
 // buffer in the reference weight layout [Cout][Cin][KH][KW] (deterministic, one launch per backward).
 struct WgFinDesc {
@@ -129,6 +137,8 @@ struct AdamArgs {
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st);
+int wgrad_tile_shape(int cfg, int& TN, int& TK);
+int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st);
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);
 int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, int fused, hipStream_t st);

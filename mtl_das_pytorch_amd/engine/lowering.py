@@ -7,8 +7,9 @@ from typing import Dict, List, Optional
 
 import torch
 
+from ..ops.hip import lib
 from .core import Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table
-from .program import Phase, k_adam, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad
+from .program import Launch, Phase, k_adam, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad, k_wgrad_batched
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
 
@@ -87,6 +88,31 @@ class LoweredProgram:
         for l in self.bwd.launches:
             if l.name == "wgrad_finalize":
                 l.args = self._wgfin_args()
+
+    def batch_wgrads(self):
+        """Replace the per-conv weight-gradient launches by one batched launch per tile config, placed
+        right before the finalize (csrc/conv.hip conv_wgrad_batched_kernel).  Called after the autotuner
+        has fixed every conv's wgrad config and split count."""
+        ls = self.bwd.launches
+        wg = [l for l in ls if l.name == "conv_wgrad"]
+        if not wg:
+            return
+        fin = next(i for i, l in enumerate(ls) if l.name == "wgrad_finalize")
+        keep = [l for l in ls[:fin] if l.name != "conv_wgrad"]
+        self.wgrad_tables = []
+        batched = []
+        for cfg in sorted({l.args[0] for l in wg}):
+            group = [l for l in wg if l.args[0] == cfg]
+            raw, nblocks = lib().wgrad_table(cfg, [l.args[2] for l in group], [l.args[1] for l in group])
+            table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+            self.wgrad_tables.append(table)
+            batched.append(Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks))
+        batched[-1].record = "wgrads"
+        for l in keep:  # the per-conv "wgrads" event is gone; the finalize now follows the batch in order
+            if l.record == "wgrads":
+                l.record = None
+        self.bwd.launches = keep + batched + ls[fin:]
+        self.wgrads_batched = True
 
     def _emit_optimizer(self, grad_scale: float = 1.0) -> Dict[str, Phase]:
         segs = [s for c in self.convs for s in c.opt_segments()]

@@ -138,14 +138,18 @@ def tail_bwd_signature(kind: int, G: int, d: dict) -> str:
             f"|bn2{int('bn2' in d)}|side{int(bool(d.get('side')))}")
 
 
-def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False, measure: bool = True) -> Dict[str, int]:
-    """Tune every conv launch of a lowered program (train forward, eval forward, backward)."""
+def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False, measure: bool = True,
+                     batch_wgrads: bool = True) -> Dict[str, int]:
+    """Tune every conv launch of a lowered program (train forward, eval forward, backward), then batch the
+    weight-gradient launches per tile config (``batch_wgrads``)."""
     if prog.device.type != "cuda":
         return {}
     cache = load_cache()
     n0 = len(cache)
     autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose, measure)
     prog.refresh_wgrad_finalize()
+    if batch_wgrads:
+        prog.batch_wgrads()
     if out_path and len(cache) != n0:
         save_cache(cache, out_path)
     return cache

@@ -174,3 +174,27 @@ def test_graph_replay_matches_eager():
     assert torch.equal(grads[1], grads[0]) and torch.equal(grads[2], grads[0])
     assert params[2][1] == 3.0
     assert torch.equal(params[2][0], params[0][0]) and torch.equal(params[1][0], params[0][0])
+
+
+@pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
+def test_batched_wgrad_bitwise_equal(model_name):
+    """One launch per tile config computes exactly what the per-conv launches compute."""
+    from mtl_das_pytorch_amd.models import build_model, encode_joint
+    from mtl_das_pytorch_amd.data.synthetic import generate
+    grads = []
+    for batched in (False, True):
+        torch.manual_seed(0)
+        m = build_model(model_name)
+        if model_name == "multi_classifier":
+            from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+            prog = InceptionProgram(m, 8, "cuda", p_drop=0.0)
+        else:
+            from mtl_das_pytorch_amd.engine.mtl import MTLProgram
+            prog = MTLProgram(m, 8, "cuda")
+        if batched:
+            prog.batch_wgrads()
+        X, d, e = generate(16, seed=1, device="cuda")
+        lab = encode_joint(d, e) if model_name == "multi_classifier" else torch.stack([d, e], 1)
+        _engine_step(prog, X, lab, torch.arange(8, device="cuda"))
+        grads.append(prog.flat.grads.clone())
+    assert torch.equal(grads[0], grads[1])

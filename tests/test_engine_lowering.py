@@ -68,3 +68,17 @@ def test_inception_program_structure():
     # every parameter has a gradient producer: conv weights (finalize), BN (tails), fc (head)
     assert p.wgfin_table.numel() == 94 * 80
     assert len(p.model.state_dict()) == 566
+
+
+def test_wgrad_batching_structure():
+    """All per-conv weight-gradient launches collapse into one launch per tile config, just before the
+    finalize; every conv appears in exactly one job table."""
+    p = MTLProgram(MTL_Net(), 32, "cpu")
+    n_wg = sum(1 for l in p.bwd.launches if l.name == "conv_wgrad")
+    cfgs = {l.args[0] for l in p.bwd.launches if l.name == "conv_wgrad"}
+    p.batch_wgrads()
+    names = [l.name for l in p.bwd.launches]
+    assert "conv_wgrad" not in names
+    b = [l for l in p.bwd.launches if l.name == "wgrad_batched"]
+    assert len(b) == len(cfgs) and sum(l.args[2] for l in b) == n_wg
+    assert names.index("wgrad_finalize") == len(names) - 1 and names[-1 - len(b):-1] == ["wgrad_batched"] * len(b)
