@@ -80,14 +80,18 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[int] = N
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available()
-    device = torch.device(f"cuda:{local_rank}") if use_gpu else torch.device("cpu")
+    # MDA_SINGLE_DEVICE=1 puts every rank on cuda:0 and MDA_DIST_BACKEND overrides the backend: together
+    # they rehearse the multi-rank GPU path (split graphs around the all-reduce, sharded sampler, metric
+    # reduction) on a one-GPU machine with gloo (RCCL refuses two ranks on one device)
+    dev_index = 0 if os.environ.get("MDA_SINGLE_DEVICE") == "1" else local_rank
+    device = torch.device(f"cuda:{dev_index}") if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
     if world <= 1:
         return DistContext(0, 1, 0, device, None)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
-    backend = backend or ("nccl" if use_gpu else "gloo")
+    backend = backend or os.environ.get("MDA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     if backend == "gloo" and os.environ["MASTER_ADDR"] in ("127.0.0.1", "localhost"):
         # single-node gloo over loopback: the host name may not resolve (containers), and gloo's
         # interface guess then makes a restarted group's full-mesh connect fail intermittently
