@@ -162,7 +162,8 @@ TailArgs parse_tail(const py::dict& d) {
   a.out = P<bf16_t>(d, "out"); a.ogs = I(d, "ogs"); a.ldo = (int)I(d, "ldo");
   a.B = (int)I(d, "B"); a.H = (int)I(d, "H"); a.W = (int)I(d, "W"); a.C = (int)I(d, "C");
   if (d.contains("g")) a.g = parse_grads(d["g"].cast<py::list>());
-  a.ws = P<double>(d, "ws"); a.ws2 = P<double>(d, "ws2");
+  a.part = P<double>(d, "part"); a.chunk_px = (int)I(d, "chunk_px");
+  a.dzbuf = P<float>(d, "dzbuf"); a.dzgs = I(d, "dzgs"); a.lddz = (int)I(d, "lddz");
   a.side = P<float>(d, "side"); a.sgs = I(d, "sgs"); a.lds = (int)I(d, "lds");
   a.dy = P<bf16_t>(d, "dy"); a.dgs = I(d, "dgs"); a.ldd = (int)I(d, "ldd");
   a.dy2 = P<bf16_t>(d, "dy2"); a.d2gs = I(d, "d2gs"); a.ldd2 = (int)I(d, "ldd2");

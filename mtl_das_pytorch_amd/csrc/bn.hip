@@ -228,131 +228,170 @@ DEV void load_ctx(const TailArgs& a, BwdCtx& X, const float* s_sc, const float* 
   }
 }
 
-template <int KIND>
-__global__ __launch_bounds__(256) void tail_bwd_reduce_kernel(TailArgs a) {
-  extern __shared__ float sm[];
-  const int C = a.C;
-  // [0..4C): sc, sh, mean, inv of BN1; [4C..8C): BN2; then partial sums [PL][3][C]
-  float* s_sc = sm; float* s_sh = sm + C; float* s_mean = sm + 2 * C; float* s_inv = sm + 3 * C;
-  float* s_part = sm + 8 * C;
-  const int z = blockIdx.z;
-  bn_prepare(a.bn, z, s_sc, s_sh, s_mean, s_inv, false);
+// ------------------------------------------------------------------------------------------------
+// Two-launch BN backward, 2-D tiled: block (chunk, cb, z) owns 8*CGB channels [8*CGB*cb, ...) of group z
+// over the pixel chunk [chunk*P, (chunk+1)*P); thread = (channel group cgl = tid % CGB, pixel lane
+// tid / CGB), so a wave reads whole NHWC pixel rows (coalesced) for C <= 64 and 64-channel slices above.
+// Block partials go into NREP fp64 replicas (atomics on rows chunk % NREP; fp64 makes the summation
+// order immaterial after rounding, as for the forward statistics) and the apply sums the NREP replicas of
+// its channels.  Per-block cross-lane reductions are strided DPP
+// row shifts (lanes of the same channel group are CGB apart), finished in LDS over the block's 16 rows.
+// Optionally the reduce stores dz (fp32) so the apply does not re-read multi-source gradients or
+// re-evaluate 2x2 pool windows.
+constexpr int BNB_T = 256;
+
+// channel groups of 8 per block: whole rows for C <= 64 (C/8 must be divisible), 64-channel slices above
+int bnb_cgb(int C) {
+  const int cg = C / 8;
+  for (int g = 8; g > 1; g >>= 1)
+    if (cg % g == 0) return g;
+  return 1;
+}
+
+// Row-strided sum: lanes i, i-S, i-2S ... of each 16-lane row; the row totals of the S lane classes end
+// up in lanes 16-S .. 15 of the row.
+template <int S>
+DEV float row_stride_sum(float v) {
+  if (S <= 1) v += dpp_f<0x111>(v);
+  if (S <= 2) v += dpp_f<0x112>(v);
+  if (S <= 4) v += dpp_f<0x114>(v);
+  if (S <= 8) v += dpp_f<0x118>(v);
+  return v;
+}
+
+// BN constants of the thread's 8 channels (BN1 and, for the residual projection, BN2)
+template <int KIND, int CGB>
+DEV void bnb_ctx(const TailArgs& a, int z, int cblk, int cgl, BwdCtx& X, float (*s_x)[5][8 * CGB]) {
   const bool two = (KIND == ADD_RELU && a.r_bn);
-  if (two) bn_prepare(a.bn2, z, s_sc + 4 * C, s_sh + 4 * C, s_mean + 4 * C, s_inv + 4 * C, false);
-  __syncthreads();
-  Lanes L(C);
-  const int c = L.cg * 8;
-  float sdz[8], sdx[8], sdx2[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { sdz[j] = 0.f; sdx[j] = 0.f; sdx2[j] = 0.f; }
-  if (L.active) {
-    BwdCtx X;
-    load_ctx<KIND>(a, X, s_sc, s_sh, s_mean, s_inv, c);
-    const int M = a.B * a.H * a.W;
-    for (int p = blockIdx.x * L.PL + L.pl; p < M; p += gridDim.x * L.PL) {
-      float dz[8], xh[8], xh2[8], side[8];
-      compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sdz[j] += dz[j];
-        sdx[j] += dz[j] * xh[j];
-        if (two) sdx2[j] += dz[j] * xh2[j];
-      }
-      if ((KIND == SIGMUL || (KIND == ADD_RELU && !a.r_bn)) && a.side)
-        store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
-    }
-  }
-  // block reduction over pixel lanes: partials -> LDS [PL][3][C], then all 256 threads reduce
-  // (item, segment) pairs and a second short pass combines segments; one atomic per item per block.
-  const int PL = L.PL;
-  const int NI = (two ? 3 : 2) * C;  // items: (statistic, channel)
-  if (L.active) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      s_part[(L.pl * 3 + 0) * C + c + j] = sdz[j];
-      s_part[(L.pl * 3 + 1) * C + c + j] = sdx[j];
-      if (two) s_part[(L.pl * 3 + 2) * C + c + j] = sdx2[j];
-    }
+  for (int t = threadIdx.x; t < (two ? 2 : 1) * 8 * CGB; t += BNB_T) {
+    const int k = t / (8 * CGB), j = t - k * 8 * CGB;
+    const BNArgs& bk = k ? a.bn2 : a.bn;
+    float sc, sh, mu, inv;
+    bn_channel(bk, z, cblk + j, false, sc, sh, mu, inv);
+    s_x[k][0][j] = sc; s_x[k][1][j] = sh; s_x[k][2][j] = mu; s_x[k][3][j] = inv;
+    s_x[k][4][j] = bk.gamma[bk.pstride * z + cblk + j];
   }
   __syncthreads();
-  float* s_seg = s_part + PL * 3 * C;  // [S][NI]
-  const int S = NI >= 256 ? 1 : min(PL, 256 / NI);
-  const int rows = (PL + S - 1) / S;
-  for (int q = threadIdx.x; q < NI * S; q += blockDim.x) {
-    const int item = q % NI, seg = q / NI;
-    const int k = item / C, ch = item - k * C;
-    float t = 0.f;
-    const int r0 = seg * rows, r1 = min(PL, r0 + rows);
-    for (int r = r0; r < r1; ++r) t += s_part[(r * 3 + k) * C + ch];
-    s_seg[seg * NI + item] = t;
-  }
-  __syncthreads();
-  const int rep = blockIdx.x % NREP;
-  for (int item = threadIdx.x; item < NI; item += blockDim.x) {
-    float t = 0.f;
-    for (int seg = 0; seg < S; ++seg) t += s_seg[seg * NI + item];
-    const int k = item / C, ch = item - k * C;
-    if (k < 2) atomicAdd(a.ws + ((int64_t)z * NREP + rep) * 2 * C + k * C + ch, (double)t);
-    if (two) {
-      double* w2 = a.ws2 + ((int64_t)z * NREP + rep) * 2 * C;
-      if (k == 0) atomicAdd(w2 + ch, (double)t);
-      if (k == 2) atomicAdd(w2 + C + ch, (double)t);
-    }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int q = cgl * 8 + j;
+    X.sc[j] = s_x[0][0][q]; X.sh[j] = s_x[0][1][q]; X.mean[j] = s_x[0][2][q]; X.inv[j] = s_x[0][3][q];
+    X.sc2[j] = s_x[1][0][q]; X.sh2[j] = s_x[1][1][q]; X.mean2[j] = s_x[1][2][q]; X.inv2[j] = s_x[1][3][q];
   }
 }
 
-template <int KIND>
-__global__ __launch_bounds__(256) void tail_bwd_apply_kernel(TailArgs a) {
-  extern __shared__ float sm[];
-  const int C = a.C;
-  float* s_sc = sm; float* s_sh = sm + C; float* s_mean = sm + 2 * C; float* s_inv = sm + 3 * C;
-  // coefficient arrays: dy = A*dz + Bc*y + Cc  (BN1 at [8C..11C), BN2 at [11C..14C))
-  float* s_A = sm + 8 * C; float* s_B = sm + 9 * C; float* s_Cc = sm + 10 * C;
-  const int z = blockIdx.z;
+template <int KIND, int CGB>
+__global__ __launch_bounds__(BNB_T) void bnb_reduce_kernel(TailArgs a) {
+  constexpr int PL = BNB_T / CGB, CB = 8 * CGB;
+  __shared__ float s_x[2][5][CB];
+  __shared__ float s_part[16][3][CB];  // 16 rows of 16 lanes per block
+  const int z = blockIdx.z, chunk = blockIdx.x;
+  const int cgl = threadIdx.x % CGB, pl = threadIdx.x / CGB;
+  const int cblk = blockIdx.y * CB, c = cblk + cgl * 8;
   const bool two = (KIND == ADD_RELU && a.r_bn);
-  bn_prepare(a.bn, z, s_sc, s_sh, s_mean, s_inv, false);
-  if (two) bn_prepare(a.bn2, z, s_sc + 4 * C, s_sh + 4 * C, s_mean + 4 * C, s_inv + 4 * C, false);
-  __syncthreads();
-  const float inv_n = 1.f / (float)a.bn.count;
-  for (int ch = threadIdx.x; ch < C; ch += blockDim.x) {
-    for (int k = 0; k < (two ? 2 : 1); ++k) {
-      const double* w = (k == 0 ? a.ws : a.ws2) + (int64_t)z * NREP * 2 * C;
-      double sdz_d = 0.0, sdx_d = 0.0;
+  BwdCtx X;
+  bnb_ctx<KIND, CGB>(a, z, cblk, cgl, X, s_x);
+  const int M = a.B * a.H * a.W;
+  const int p0 = chunk * a.chunk_px, p1 = min(M, p0 + a.chunk_px);
+  float sdz[8], sdx[8], sdx2[8];
 #pragma unroll
-      for (int r = 0; r < NREP; ++r) { sdz_d += w[r * 2 * C + ch]; sdx_d += w[r * 2 * C + C + ch]; }
-      const float sdz = (float)sdz_d, sdx = (float)sdx_d;
-      const float g = (k == 0 ? a.bn.gamma[a.bn.pstride * z + ch] : a.bn2.gamma[a.bn2.pstride * z + ch]);
-      const float inv = s_inv[4 * C * k + ch], mu = s_mean[4 * C * k + ch];
-      const float mdz = sdz * inv_n, mdx = sdx * inv_n;
-      s_A[3 * C * k + ch] = g * inv;
-      s_B[3 * C * k + ch] = -g * inv * inv * mdx;
-      s_Cc[3 * C * k + ch] = g * inv * (mu * inv * mdx - mdz);
-      if (blockIdx.x == 0) {
-        float* dg = (k == 0 ? a.dgamma : a.dgamma2);
-        float* db = (k == 0 ? a.dbeta : a.dbeta2);
-        if (dg) dg[a.pgs * z + ch] = sdx;
-        if (db) db[a.pgs * z + ch] = sdz;
-      }
+  for (int j = 0; j < 8; ++j) { sdz[j] = 0.f; sdx[j] = 0.f; sdx2[j] = 0.f; }
+  float* dzz = a.dzbuf ? a.dzbuf + a.dzgs * z : nullptr;
+  for (int p = p0 + pl; p < p1; p += PL) {
+    float dz[8], xh[8], xh2[8], side[8];
+    compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sdz[j] += dz[j];
+      sdx[j] += dz[j] * xh[j];
+      if (two) sdx2[j] += dz[j] * xh2[j];
+    }
+    if ((KIND == SIGMUL || (KIND == ADD_RELU && !a.r_bn)) && a.side)
+      store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
+    if (dzz) store8f(dzz + (int64_t)p * a.lddz + c, dz);
+  }
+  const int lane = threadIdx.x & 63, row = threadIdx.x >> 4;
+  const bool top = (lane & 15) >= 16 - CGB;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float t0 = row_stride_sum<CGB>(sdz[j]), t1 = row_stride_sum<CGB>(sdx[j]);
+    const float t2 = two ? row_stride_sum<CGB>(sdx2[j]) : 0.f;
+    if (top) { s_part[row][0][cgl * 8 + j] = t0; s_part[row][1][cgl * 8 + j] = t1; s_part[row][2][cgl * 8 + j] = t2; }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 3 * CB; t += BNB_T) {
+    const int k = t / CB, q = t - k * CB;
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v += s_part[r][k][q];
+    atomicAdd(a.part + (((int64_t)z * NREP + chunk % NREP) * 3 + k) * a.C + cblk + q, (double)v);
+  }
+}
+
+template <int KIND, int CGB>
+__global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
+  constexpr int PL = BNB_T / CGB, CB = 8 * CGB;
+  __shared__ float s_x[2][5][CB];
+  __shared__ float s_red[BNB_T];
+  __shared__ float s_coef[2][3][CB];
+  const int z = blockIdx.z, chunk = blockIdx.x;
+  const int cgl = threadIdx.x % CGB, pl = threadIdx.x / CGB;
+  const int cblk = blockIdx.y * CB, c = cblk + cgl * 8;
+  const bool two = (KIND == ADD_RELU && a.r_bn);
+  BwdCtx X;
+  bnb_ctx<KIND, CGB>(a, z, cblk, cgl, X, s_x);
+  // the NREP replicas of this block's channels: item = (stat, channel), Q threads per item
+  constexpr int NI = 3 * CB;
+  constexpr int Q = BNB_T / NI > 0 ? BNB_T / NI : 1;
+  {
+    const double* base = a.part + (int64_t)z * NREP * 3 * a.C + cblk;
+    for (int t = threadIdx.x; t < NI * Q; t += BNB_T) {
+      const int item = t % NI, q = t / NI;
+      const int k = item / CB, j = item - k * CB;
+      double v = 0.0;
+      for (int r = q; r < NREP; r += Q) v += base[((int64_t)r * 3 + k) * a.C + j];
+      s_red[q * NI + item] = (float)v;
     }
   }
   __syncthreads();
-  Lanes L(C);
-  if (!L.active) return;
-  const int c = L.cg * 8;
-  BwdCtx X;
-  load_ctx<KIND>(a, X, s_sc, s_sh, s_mean, s_inv, c);
+  for (int t = threadIdx.x; t < (two ? 2 : 1) * CB; t += BNB_T) {
+    const int k = t / CB, j = t - k * CB;  // k: BN1 / BN2
+    float sd = 0.f, sx = 0.f;
+    for (int q = 0; q < Q; ++q) { sd += s_red[q * NI + j]; sx += s_red[q * NI + (k ? 2 : 1) * CB + j]; }
+    const BNArgs& bk = k ? a.bn2 : a.bn;
+    const float inv_n = 1.f / (float)bk.count;
+    const float g = s_x[k][4][j], inv = s_x[k][3][j], mu = s_x[k][2][j];
+    const float mdz = sd * inv_n, mdx = sx * inv_n;
+    s_coef[k][0][j] = g * inv;                            // dy = A*dz + B*y + C
+    s_coef[k][1][j] = -g * inv * inv * mdx;
+    s_coef[k][2][j] = g * inv * (mu * inv * mdx - mdz);
+    if (chunk == 0) {
+      float* dg = k ? a.dgamma2 : a.dgamma;
+      float* db = k ? a.dbeta2 : a.dbeta;
+      if (dg) dg[a.pgs * z + cblk + j] = sx;
+      if (db) db[a.pgs * z + cblk + j] = sd;
+    }
+  }
+  __syncthreads();
   float A1[8], B1[8], C1[8], A2[8], B2[8], C2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    A1[j] = s_A[c + j]; B1[j] = s_B[c + j]; C1[j] = s_Cc[c + j];
-    if (two) { A2[j] = s_A[3 * C + c + j]; B2[j] = s_B[3 * C + c + j]; C2[j] = s_Cc[3 * C + c + j]; }
+    const int q = cgl * 8 + j;
+    A1[j] = s_coef[0][0][q]; B1[j] = s_coef[0][1][q]; C1[j] = s_coef[0][2][q];
+    A2[j] = s_coef[1][0][q]; B2[j] = s_coef[1][1][q]; C2[j] = s_coef[1][2][q];
   }
   const int M = a.B * a.H * a.W;
+  const int p0 = chunk * a.chunk_px, p1 = min(M, p0 + a.chunk_px);
   const bf16_t* yz = a.y + a.ygs * z;
-  for (int p = blockIdx.x * L.PL + L.pl; p < M; p += gridDim.x * L.PL) {
-    float dz[8], xh[8], xh2[8], side[8];
-    compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
-    float y[8], o[8];
+  const float* dzz = a.dzbuf ? a.dzbuf + a.dzgs * z : nullptr;
+  for (int p = p0 + pl; p < p1; p += PL) {
+    float dz[8], y[8], o[8];
+    if (dzz) {
+      load8f(dzz + (int64_t)p * a.lddz + c, dz);
+    } else {
+      float xh[8], xh2[8], side[8];
+      compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
+    }
     load8(yz + (int64_t)p * a.ldy + c, y);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = A1[j] * dz[j] + B1[j] * y[j] + C1[j];
@@ -489,7 +528,7 @@ int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t 
   return (int)hipGetLastError();
 }
 
-int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, int fused, hipStream_t st) {
+int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, hipStream_t st) {
   if (fused) {
     const int M = a.B * a.H * a.W;
     const int R = (M + FUSED_T - 1) / FUSED_T;
@@ -511,21 +550,23 @@ int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, int fused, h
 #undef KR
     return (int)hipGetLastError();
   }
-  const int CG = a.C / 8;
-  const int PL = 256 / CG;
-  size_t lds_r = (size_t)(8 * a.C + 3 * PL * a.C + 3 * a.C + 256) * sizeof(float);
-  size_t lds_a = (size_t)(14 * a.C) * sizeof(float);
-  dim3 grid(blocks, 1, G);
-  switch (kind) {
-#define K(X)                                                                                 \
-  case X:                                                                                    \
-    hipLaunchKernelGGL(tail_bwd_reduce_kernel<X>, grid, dim3(256), lds_r, st, a);            \
-    hipLaunchKernelGGL(tail_bwd_apply_kernel<X>, grid, dim3(256), lds_a, st, a);             \
+  if (!a.part || a.chunk_px <= 0 || nchunk <= 0) return -4;
+  const int cgb = bnb_cgb(a.C);
+  dim3 grid(nchunk, a.C / (8 * cgb), G);
+#define KC(X, CG)                                                                      \
+  hipLaunchKernelGGL((bnb_reduce_kernel<X, CG>), grid, dim3(BNB_T), 0, st, a);         \
+  hipLaunchKernelGGL((bnb_apply_kernel<X, CG>), grid, dim3(BNB_T), 0, st, a);
+#define K(X)                                                   \
+  case X:                                                      \
+    if (cgb == 1) { KC(X, 1) } else if (cgb == 2) { KC(X, 2) } \
+    else if (cgb == 4) { KC(X, 4) } else { KC(X, 8) }          \
     break;
+  switch (kind) {
     K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(ADD_RELU) K(POOL_RELU)
-#undef K
     default: return -1;
   }
+#undef K
+#undef KC
   return (int)hipGetLastError();
 }
 

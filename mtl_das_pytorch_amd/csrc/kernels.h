@@ -70,7 +70,8 @@ struct TailArgs {
   int B, H, W, C;
   // backward only
   GradSrcs g;                       // upstream fp32 gradient(s) on the tail's output grid
-  double* ws; double* ws2;          // [G][NREP][2][C] fp64 (see BNArgs::stats)
+  double* part; int chunk_px;       // [G][NREP][3][C] fp64 replica sums (zeroed per step); pixels per chunk
+  float* dzbuf; int64_t dzgs; int lddz;  // optional dz store (reduce) / load (apply), fp32
   float* side; int64_t sgs; int lds;
   bf16_t* dy; int64_t dgs; int ldd;
   bf16_t* dy2; int64_t d2gs; int ldd2;

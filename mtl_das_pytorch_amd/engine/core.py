@@ -23,7 +23,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..ops.functional import WGRAD_TILES, wgrad_cfg
+from ..ops.functional import WGRAD_TILES, bnb_plan, wgrad_cfg
 from ..ops.hip import lib, ptr
 
 NREP = 32  # must match csrc/common.h
@@ -268,8 +268,11 @@ class BNLayer:
             raise ValueError("BN running-stat stride must equal the affine-parameter stride")
         # fp64 replica sums: summation order no longer perturbs results (csrc/common.h BNArgs::stats)
         self.stats = arena.zeroed((self.G, NREP, 2, self.C), torch.float64)
-        self.ws = arena.zeroed((self.G, NREP, 2, self.C), torch.float64)
-        self.ws2 = None  # allocated on demand (second BN of a residual tail shares the dz)
+        # backward: fp64 replica sums of the 2-D tiled BN backward (csrc/bn.hip bnb_*), zeroed per step
+        self.nchunk, self.chunk_px = bnb_plan(count, self.C, self.G)
+        self.part = arena.zeroed((self.G, NREP, 3, self.C), torch.float64)
+        self.arena = arena
+        self.dzbuf = None
 
     def args(self, training: bool) -> dict:
         f = self.flat

@@ -42,18 +42,25 @@ class LoweredProgram:
     def _tail_bwd(self, ph: Phase, kind: int, G: int, y: Act, bn: BNLayer, g: list, dy: Act, r: Act = None,
                   bn2: BNLayer = None, side: Act = None, dy2: Act = None):
         d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(True), "B": self.B, "H": y.H, "W": y.W, "C": y.C,
-             "g": g, "ws": P(bn.ws), "dy": dy.p, "dgs": dy.gs, "ldd": dy.ld}
+             "g": g, "part": P(bn.part), "chunk_px": bn.chunk_px, "dy": dy.p, "dgs": dy.gs, "ldd": dy.ld}
+        if kind in (SIGMUL, POOL_RELU) or len(g) > 1:
+            # the apply pass reads the stored dz instead of re-reading several gradient sources /
+            # re-evaluating the pool window
+            if bn.dzbuf is None:
+                bn.dzbuf = self.arena.empty((G, y.M, y.C), torch.float32)
+            d.update({"dzbuf": P(bn.dzbuf), "dzgs": y.M * y.C if G > 1 else 0, "lddz": y.C})
         d.update(bn.grad_ptrs())
         if r is not None:
             d.update({"r": r.p, "rgs": r.gs, "ldr": r.ld})
         if bn2 is not None:
             d["bn2"] = bn2.args(True)
-            d["ws2"] = P(bn.ws2)
             gp = bn2.grad_ptrs()
             d.update({"dgamma2": gp["dgamma"], "dbeta2": gp["dbeta"], "dy2": dy2.p, "d2gs": dy2.gs, "ldd2": dy2.ld})
         if side is not None:
             d.update({"side": side.p, "sgs": side.gs, "lds": side.ld})
-        ph.add(f"tailbwd{kind}", k_tail_bwd, kind, G, _blocks(y.M, y.C, cap=1024, per_thread=2), d)
+        if bn.count != y.M:
+            raise ValueError("BN backward chunking assumes the BN count equals the tail's pixel count")
+        ph.add(f"tailbwd{kind}", k_tail_bwd, kind, G, bn.nchunk, d)
 
     def _conv_fwd(self, ph: Phase, c: ConvLayer, src: dict, out: Act, bn: BNLayer, training: bool):
         mode, cfg, G, d = c.fwd_args(src, out, bn, training)

@@ -100,7 +100,6 @@ class MTLProgram(LoweredProgram):
             if rb.has_projection:
                 L["cs"] = ConvLayer([rb.shortcut[0]], f, A, B, prev.H, prev.W)
                 L["bns"] = BNLayer([rb.shortcut[1]], f, A, B * Ho * Wo)
-                L["bnb"].ws2 = A.zeroed((1, NREP, 2, C), torch.float64)
                 L["ys"] = new_act(A, 1, B, Ho, Wo, C)
                 L["dys"] = new_act(A, 1, B, Ho, Wo, C)
                 L["dxs"] = new_act(A, 1, B, prev.H, prev.W, prev.C, torch.float32)

@@ -222,17 +222,45 @@ def bn_tail(kind: int, y: torch.Tensor, bn: dict, r: Optional[torch.Tensor] = No
     return out
 
 
+def bnb_cgb(C: int) -> int:
+    """Channel groups of 8 per block of the 2-D tiled BN backward (csrc/bn.hip bnb_cgb)."""
+    cg = C // 8
+    for g in (8, 4, 2):
+        if cg % g == 0:
+            return g
+    return 1
+
+
+def bnb_plan(M: int, C: int, G: int = 1, target_blocks: int = 1024):
+    """Chunking of the 2-D tiled BN backward (csrc/bn.hip bnb_*): blocks of 256 threads cover 8*CGB
+    channels x 256/CGB pixel lanes; chunks are sized so that chunks x channel blocks x G ~ target_blocks
+    (at most 8 pixel steps per thread).  Returns (nchunk, pixels per chunk)."""
+    cgb = bnb_cgb(C)
+    pl = 256 // cgb
+    steps = max(1, math.ceil(M / pl))
+    cblocks = (C // (8 * cgb)) * G
+    per = max(1, min(8, math.ceil(steps * cblocks / target_blocks)))
+    chunk_px = pl * per
+    return math.ceil(M / chunk_px), chunk_px
+
+
 def bn_tail_backward(kind: int, y: torch.Tensor, bn: dict, grads: Sequence[torch.Tensor], dgamma, dbeta,
                      r: Optional[torch.Tensor] = None, bn2: Optional[dict] = None, dgamma2=None, dbeta2=None,
-                     blocks: int = 64, fused: bool = False):
+                     fused: bool = False, store_dz: bool = False):
     """Returns ``(dy bf16, side fp32 | None, dy2 bf16 | None)``; writes dgamma/dbeta (and 2) in place.
-    ``fused``: single-launch variant (block per 8 channels over all pixels) instead of reduce + apply."""
+    ``fused``: single-launch variant (block per 8 channels over all pixels) instead of reduce + apply;
+    ``store_dz``: the reduce stores dz and the apply reads it instead of recomputing it."""
     B, H, W, C = y.shape
-    ws = torch.zeros(1, NREP, 2, C, device=y.device, dtype=torch.float64)
+    nchunk, chunk_px = bnb_plan(B * H * W, C)
+    part = torch.zeros(NREP, 3, C, device=y.device, dtype=torch.float64)
     dy = torch.empty_like(y)
     d = {"y": ptr(y), "ldy": C, "bn": bn, "B": B, "H": H, "W": W, "C": C,
-         "g": [(ptr(g), 0, g.shape[-1]) for g in grads], "ws": ptr(ws), "dy": ptr(dy), "ldd": C,
-         "dgamma": ptr(dgamma), "dbeta": ptr(dbeta), "fused": int(fused)}
+         "g": [(ptr(g), 0, g.shape[-1]) for g in grads], "part": ptr(part), "chunk_px": chunk_px,
+         "dy": ptr(dy), "ldd": C, "dgamma": ptr(dgamma), "dbeta": ptr(dbeta), "fused": int(fused)}
+    dzbuf = None
+    if store_dz:
+        dzbuf = torch.empty(B, H, W, C, device=y.device)
+        d.update({"dzbuf": ptr(dzbuf), "lddz": C})
     side = dy2 = None
     if r is not None:
         d.update({"r": ptr(r), "ldr": r.shape[-1]})
@@ -240,11 +268,10 @@ def bn_tail_backward(kind: int, y: torch.Tensor, bn: dict, grads: Sequence[torch
         side = torch.empty(B, H, W, C, device=y.device, dtype=torch.float32)
         d.update({"side": ptr(side), "lds": C})
     if bn2 is not None:
-        ws2 = torch.zeros(1, NREP, 2, C, device=y.device, dtype=torch.float64)
         dy2 = torch.empty_like(y)
-        d.update({"bn2": bn2, "ws2": ptr(ws2), "dy2": ptr(dy2), "ldd2": C, "dgamma2": ptr(dgamma2),
+        d.update({"bn2": bn2, "dy2": ptr(dy2), "ldd2": C, "dgamma2": ptr(dgamma2),
                   "dbeta2": ptr(dbeta2)})
-    lib().tail_bwd(kind, 1, blocks, stream(), d)
+    lib().tail_bwd(kind, 1, nchunk, stream(), d)
     return dy, side, dy2
 
 

@@ -62,7 +62,9 @@ def main():
         nbt = torch.zeros(1, dtype=torch.int64, device="cuda")
         g = torch.randn(M, C, device="cuda")
         dy = torch.empty_like(y)
-        ws = torch.zeros(NREP, 2, C, device="cuda", dtype=torch.float64)
+        from mtl_das_pytorch_amd.ops.functional import bnb_plan
+        nchunk, chunk_px = bnb_plan(M, C)
+        part = torch.empty(nchunk, 3, C, device="cuda")
         dgam, dbet = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
 
         def bn(with_fin):
@@ -82,9 +84,9 @@ def main():
                      "B": 1, "H": M, "W": 1, "C": C}
                 r[f"fwd_pt{pt}_fin{wf}"] = timeit(lambda: L.tail_fwd(1, 1, nb, torch.cuda.current_stream().cuda_stream, d))
                 db = {"y": y.data_ptr(), "ygs": 0, "ldy": C, "bn": bn(wf), "B": 1, "H": M, "W": 1, "C": C,
-                      "g": [(g.data_ptr(), 0, C)], "ws": ws.data_ptr(), "dy": dy.data_ptr(), "dgs": 0, "ldd": C,
+                      "g": [(g.data_ptr(), 0, C)], "part": part.data_ptr(), "chunk_px": chunk_px, "dy": dy.data_ptr(), "dgs": 0, "ldd": C,
                       "dgamma": dgam.data_ptr(), "dbeta": dbet.data_ptr(), "pgs": 0}
-                r[f"bwd_pt{pt}_fin{wf}"] = timeit(lambda: L.tail_bwd(1, 1, nb, torch.cuda.current_stream().cuda_stream, db))
+                r[f"bwd_pt{pt}_fin{wf}"] = timeit(lambda: L.tail_bwd(1, 1, nchunk, torch.cuda.current_stream().cuda_stream, db))
                 if pt == 2 and wf == 0 and M <= 4096:
                     dbf = dict(db, fused=1)
                     r["bwd_fused"] = timeit(lambda: L.tail_bwd(1, 1, nb, torch.cuda.current_stream().cuda_stream, dbf))

@@ -12,7 +12,7 @@ from mtl_das_pytorch_amd.engine.core import Act, LazyView  # noqa: E402
 from mtl_das_pytorch_amd.models import build_model, encode_joint  # noqa: E402
 from mtl_das_pytorch_amd.ops.hip import stream  # noqa: E402
 
-OUT_KEYS = ("out", "dy", "dy2", "side", "slab", "stats", "dfeat", "logp", "ws", "ws2", "dx", "y", "dlogits")
+OUT_KEYS = ("out", "dy", "dy2", "side", "slab", "stats", "dfeat", "logp", "part", "dzbuf", "dx", "y", "dlogits")
 
 
 def collect(obj, seen, acc):
@@ -102,9 +102,9 @@ def main():
     b = run()
     for i, ((ph, l), sa, sb) in enumerate(zip(launches, a, b)):
         for (k, x), (_, y) in zip(sa, sb):
-            if k in ("stats", "ws", "ws2"):
+            if k == "stats":
                 xf, yf = x.view(torch.float64), y.view(torch.float64)
-            elif x.numel() % 4 == 0 and k in ("slab", "dfeat", "logp", "dx", "grads", "side", "dlogits"):
+            elif x.numel() % 4 == 0 and k in ("slab", "part", "dzbuf", "dfeat", "logp", "dx", "grads", "side", "dlogits"):
                 xf, yf = x.view(torch.float32), y.view(torch.float32)
             else:
                 xf, yf = x.view(torch.bfloat16).float(), y.view(torch.bfloat16).float()
