@@ -331,10 +331,17 @@ class ConvLayer:
         self.slab = arena.empty((self.G, max_splits, self.Npad, self.Kpad_w), torch.float32)
         self.set_wgrad_cfg(wgrad_cfg(self.Co, self.Kpad_w))
 
+    # every split-M block reduces at least this many output pixels: with the weight gradients of all
+    # convs batched into one launch (csrc/conv.hip conv_wgrad_batched_kernel) the grid no longer has to
+    # be filled by one conv's splits, and each extra split costs a full Npad x Kpad slab read in the
+    # finalize (Model C: ~0.9 GB/step of slab traffic with grid-filling splits)
+    MIN_SPLIT_PX = 1024
+
     def wgrad_plan(self, cfg: int):
         TN, TK, MCH = WGRAD_TILES[cfg]
         tiles = math.ceil(self.Npad / TN) * (self.Kpad_w // TK) * self.G
-        splits = max(1, min(math.ceil(self.M_out / MCH), math.ceil(512 / tiles)))
+        splits = max(1, min(math.ceil(self.M_out / MCH), math.ceil(512 / tiles),
+                            math.ceil(self.M_out / self.MIN_SPLIT_PX)))
         mps = pad_to(math.ceil(self.M_out / splits), MCH)
         return math.ceil(self.M_out / mps), mps
 

@@ -1,0 +1,4 @@
+source tools/gpu_round.sh
+export TAILN=2
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+step profC timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profC3 -o run -- python3 bench.py --model multi_classifier --steps 30 --warmup 3 --no-tune
