@@ -134,6 +134,14 @@ class InceptionProgram(LoweredProgram):
     def _val(self, H, W, C) -> Val:
         return Val(new_act(self.arena, 1, self.B, H, W, C))
 
+    def _at(self, branch: Optional[int]):
+        """Subsequent ops belong to ``branch`` of the current block (None: stem / head, stream 0)."""
+        self._cur = None if branch is None else (self._bi, branch)
+
+    def _push(self, op):
+        self.ops.append(op)
+        self.op_meta.append(self._cur)
+
     def _cbr(self, bc: BasicConv2d, src: Val, out: Optional[Val] = None) -> Val:
         if out is None:
             kh, kw = bc.conv.kernel_size
@@ -142,7 +150,7 @@ class InceptionProgram(LoweredProgram):
             H = (src.act.H + 2 * ph - kh) // sh + 1
             W = (src.act.W + 2 * pw - kw) // sw + 1
             out = self._val(H, W, bc.conv.out_channels)
-        self.ops.append(CBR(self, bc, src, out))
+        self._push(CBR(self, bc, src, out))
         return out
 
     def _pool(self, is_max: bool, src: Val, out: Optional[Val] = None) -> Val:
@@ -150,7 +158,7 @@ class InceptionProgram(LoweredProgram):
             s = src.act
             H, W = ((s.H - 3) // 2 + 1, (s.W - 3) // 2 + 1) if is_max else (s.H, s.W)
             out = self._val(H, W, s.C)
-        self.ops.append(Pool(self, is_max, src, out))
+        self._push(Pool(self, is_max, src, out))
         return out
 
     def _concat(self, H, W, widths) -> tuple:
@@ -167,46 +175,52 @@ class InceptionProgram(LoweredProgram):
         if isinstance(blk, InceptionA):
             pf = blk.branch_pool.conv.out_channels
             cat, (o1, o5, o3, op) = self._concat(H, W, [64, 64, 96, pf])
-            self._cbr(blk.branch1x1, x, o1)
-            self._cbr(blk.branch5x5_2, self._cbr(blk.branch5x5_1, x), o5)
-            self._cbr(blk.branch3x3dbl_3, self._cbr(blk.branch3x3dbl_2, self._cbr(blk.branch3x3dbl_1, x)), o3)
-            self._cbr(blk.branch_pool, self._pool(False, x), op)
+            self._at(0); self._cbr(blk.branch1x1, x, o1)
+            self._at(1); self._cbr(blk.branch5x5_2, self._cbr(blk.branch5x5_1, x), o5)
+            self._at(2); self._cbr(blk.branch3x3dbl_3, self._cbr(blk.branch3x3dbl_2, self._cbr(blk.branch3x3dbl_1, x)), o3)
+            self._at(3); self._cbr(blk.branch_pool, self._pool(False, x), op)
         elif isinstance(blk, InceptionB):
             Ho, Wo = (H - 3) // 2 + 1, (W - 3) // 2 + 1
             cat, (o3, od, om) = self._concat(Ho, Wo, [384, 96, x.act.C])
-            self._cbr(blk.branch3x3, x, o3)
-            self._cbr(blk.branch3x3dbl_3, self._cbr(blk.branch3x3dbl_2, self._cbr(blk.branch3x3dbl_1, x)), od)
-            self._pool(True, x, om)
+            self._at(0); self._cbr(blk.branch3x3, x, o3)
+            self._at(1); self._cbr(blk.branch3x3dbl_3, self._cbr(blk.branch3x3dbl_2, self._cbr(blk.branch3x3dbl_1, x)), od)
+            self._at(2); self._pool(True, x, om)
         elif isinstance(blk, InceptionC):
             cat, (o1, o7, od, op) = self._concat(H, W, [192, 192, 192, 192])
-            self._cbr(blk.branch1x1, x, o1)
-            self._cbr(blk.branch7x7_3, self._cbr(blk.branch7x7_2, self._cbr(blk.branch7x7_1, x)), o7)
+            self._at(0); self._cbr(blk.branch1x1, x, o1)
+            self._at(1); self._cbr(blk.branch7x7_3, self._cbr(blk.branch7x7_2, self._cbr(blk.branch7x7_1, x)), o7)
+            self._at(2)
             v = x
             for i in range(1, 5):
                 v = self._cbr(getattr(blk, f"branch7x7dbl_{i}"), v)
             self._cbr(blk.branch7x7dbl_5, v, od)
-            self._cbr(blk.branch_pool, self._pool(False, x), op)
+            self._at(3); self._cbr(blk.branch_pool, self._pool(False, x), op)
         elif isinstance(blk, InceptionD):
             Ho, Wo = (H - 3) // 2 + 1, (W - 3) // 2 + 1
             cat, (o3, o7, om) = self._concat(Ho, Wo, [320, 192, x.act.C])
-            self._cbr(blk.branch3x3_2, self._cbr(blk.branch3x3_1, x), o3)
+            self._at(0); self._cbr(blk.branch3x3_2, self._cbr(blk.branch3x3_1, x), o3)
+            self._at(1)
             v = x
             for i in range(1, 4):
                 v = self._cbr(getattr(blk, f"branch7x7x3_{i}"), v)
             self._cbr(blk.branch7x7x3_4, v, o7)
-            self._pool(True, x, om)
+            self._at(2); self._pool(True, x, om)
         elif isinstance(blk, InceptionE):
             cat, (o1, o3a, o3b, oda, odb, op) = self._concat(H, W, [320, 384, 384, 384, 384, 192])
-            self._cbr(blk.branch1x1, x, o1)
+            self._at(0); self._cbr(blk.branch1x1, x, o1)
+            self._at(1)
             s = self._cbr(blk.branch3x3_1, x)
             self._cbr(blk.branch3x3_2a, s, o3a)
             self._cbr(blk.branch3x3_2b, s, o3b)
+            self._at(2)
             d = self._cbr(blk.branch3x3dbl_2, self._cbr(blk.branch3x3dbl_1, x))
             self._cbr(blk.branch3x3dbl_3a, d, oda)
             self._cbr(blk.branch3x3dbl_3b, d, odb)
-            self._cbr(blk.branch_pool, self._pool(False, x), op)
+            self._at(3); self._cbr(blk.branch_pool, self._pool(False, x), op)
         else:
             raise TypeError(f"cannot lower block {type(blk).__name__}")
+        self._at(None)
+        self._bi += 1
         return cat
 
     def _alloc(self):
@@ -214,6 +228,8 @@ class InceptionProgram(LoweredProgram):
         self.x = A.zeros((B, self.H0, self.W0, 8))
         self.labels = torch.zeros((B,), dtype=torch.int64, device=self.device)
         self.ops = []
+        self.op_meta = []   # per op: None (stem, stream 0) or (block index, branch index)
+        self._bi, self._cur = 0, None
         v = Val(Act(self.x, 0, 8, 8, 0, B, self.H0, self.W0), needs_grad=False)
         v = self._cbr(m.Conv2d_1a_3x3, v)
         v = self._cbr(m.Conv2d_2a_3x3, v)
@@ -261,17 +277,64 @@ class InceptionProgram(LoweredProgram):
         self.bwd = self._emit_backward()
         self.opt = self._emit_optimizer()
 
+    def _emit_streamed(self, ph: Phase, order, run) -> List[str]:
+        """Emit ops in ``order``; the branches of an Inception block run on streams 0..3 (branch b on
+        stream b), join-then-fork per block: a kernel-free fork point on stream 0 waits for the previous
+        block's side streams and records one event, and every side branch waits only for that event
+        (the block input -- in backward the block output's gradient sources -- is then complete).
+        Returns the side-stream events the caller's next stream-0 launch must wait for.  With
+        MDA_STREAMS=0 the annotations are inert and the ops run in list order."""
+        owed0: List[str] = []       # last block's side-stream end events (joined at the next fork)
+        cur_block, used = None, set()
+
+        def close_block():
+            nonlocal owed0, cur_block, used
+            owed0 = []
+            for st in sorted(used - {0}):
+                ph.cur_stream = st
+                tag = f"{ph.name}_e{cur_block}_{st}"
+                ph.mark(tag)
+                owed0.append(tag)
+            cur_block, used = None, set()
+
+        for i in order:
+            meta = self.op_meta[i]
+            blk = None if meta is None else meta[0]
+            if blk != cur_block and cur_block is not None:
+                close_block()
+            if meta is None:
+                ph.cur_stream = 0
+                ph.pending_waits.extend(owed0)
+                owed0 = []
+                run(self.ops[i])
+                continue
+            if cur_block is None:
+                cur_block = blk
+                ph.cur_stream = 0
+                ph.fork_point(f"{ph.name}_f{blk}", waits=owed0)
+                owed0 = []
+            st = meta[1] % 4
+            ph.cur_stream = st
+            if st not in used:
+                used.add(st)
+                if st != 0:
+                    ph.pending_waits.append(f"{ph.name}_f{blk}")
+            run(self.ops[i])
+        if cur_block is not None:
+            close_block()
+        ph.cur_stream = 0
+        return owed0
+
     def _emit_forward(self, training: bool) -> Phase:
         ph = Phase("forward_train" if training else "forward_eval")
-        for op in self.ops:
-            op.forward(self, ph, training)
-        ph.add("cls_head", k_cls_head, self._head_args(training))
+        owed = self._emit_streamed(ph, range(len(self.ops)), lambda op: op.forward(self, ph, training))
+        ph.add("cls_head", k_cls_head, self._head_args(training), waits=owed)
         return ph
 
     def _emit_backward(self) -> Phase:
         ph = Phase("backward")
-        for op in reversed(self.ops):
-            op.backward(self, ph)
+        owed = self._emit_streamed(ph, reversed(range(len(self.ops))), lambda op: op.backward(self, ph))
+        assert not owed, "the stem's backward must have joined the first block's branches"
         ph.launches[self._last_wgrad].record = "wgrads"
         ph.add("wgrad_finalize", k_wgfin, *self._wgfin_args(), waits=("wgrads",))
         return ph

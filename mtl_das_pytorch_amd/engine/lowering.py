@@ -67,11 +67,10 @@ class LoweredProgram:
         ph.add("conv_fwd", k_conv, mode, cfg, G, d, owner=c)
 
     def _conv_bwd(self, ph: Phase, c: ConvLayer, src: dict, dy: Act, dx: Optional[Act]):
-        # the weight gradient is off the critical path: it runs on side stream 2 as soon as its dy exists
-        tag = f"dy{len(ph.launches)}"
-        ph.mark(tag)
+        # per-conv weight gradient on the producer's stream (production programs replace these by the
+        # batched launches at the end of the backward pass: batch_wgrads)
         cfg, G, d = c.wgrad_args(src, dy)
-        ph.add("conv_wgrad", k_wgrad, cfg, G, d, owner=c, stream=2, waits=(tag,))
+        ph.add("conv_wgrad", k_wgrad, cfg, G, d, owner=c)
         self._last_wgrad = len(ph.launches) - 1
         if dx is not None:
             mode, cfg, G, d = c.dgrad_args(dy, dx)
@@ -105,7 +104,20 @@ class LoweredProgram:
         if not wg:
             return
         fin = next(i for i, l in enumerate(ls) if l.name == "wgrad_finalize")
-        keep = [l for l in ls[:fin] if l.name != "conv_wgrad"]
+        keep = []
+        for l in ls[:fin]:
+            if l.name != "conv_wgrad":
+                keep.append(l)
+                continue
+            if l.record is not None and l.record != "wgrads":
+                # an event recorded on a removed launch now stands for the stream's previous kept launch
+                prev = next((k for k in reversed(keep) if k.stream == l.stream), None)
+                if prev is None:
+                    raise RuntimeError(f"cannot re-anchor event {l.record}")
+                if prev.record is None:
+                    prev.record = l.record
+                else:
+                    self.bwd.alias[l.record] = prev.record
         self.wgrad_tables = []
         batched = []
         for cfg in sorted({l.args[0] for l in wg}):

@@ -17,9 +17,15 @@ import os
 
 from ..ops.hip import lib, stream
 
-# Side-stream execution is opt-in: measured on MI355X (round 1) the replayed graph showed no kernel
-# overlap for this workload while adding event edges, so the default is the serial order of the list.
-MULTI_STREAM = os.environ.get("MDA_STREAMS", "0") == "1"
+# Side streams are on by default (MDA_STREAMS=0 runs the list serially on one stream).  Measured on
+# MI355X: independent branches captured on separate streams DO overlap in graph replay (two chains of
+# small convs: 253 vs 320 us, tools/graph_concurrency.py); Model A levels || backbone: 21.2k -> 25.0k
+# samples/s, Model C Inception branches on 4 streams: 5.7k -> 6.35k.  Cross-stream edges are kept few
+# (join-then-fork points, wgrads on their producer's stream): denser event patterns crashed
+# hipStreamEndCapture on ROCm 7.
+MULTI_STREAM = os.environ.get("MDA_STREAMS", "1") == "1"
+# streams used at most (ids above are folded onto the last one -- still a valid schedule)
+MAX_STREAMS = max(1, min(4, int(os.environ.get("MDA_MAX_STREAMS", "4"))))
 
 
 class Launch:
@@ -35,7 +41,8 @@ class Launch:
         self.record = record
 
     def __call__(self, st: int):
-        self.fn(*self.args, st)
+        if self.fn is not None:  # fn None: a pseudo-launch that only carries waits / a record (fork point)
+            self.fn(*self.args, st)
 
 
 class Phase:
@@ -45,12 +52,18 @@ class Phase:
         self._streams = None
         self.cur_stream = 0      # default stream id for add()
         self.pending_waits = []  # waits attached to the next add() on any stream
+        self.alias = {}          # event tag -> tag it is recorded under (after launches were removed)
 
     def add(self, name, fn, *args, owner=None, stream=None, waits=(), record=None):
         sid = self.cur_stream if stream is None else stream
         w = tuple(waits) + tuple(self.pending_waits)
         self.pending_waits = []
         self.launches.append(Launch(name, fn, *args, owner=owner, stream=sid, waits=w, record=record))
+
+    def fork_point(self, tag: str, waits=()):
+        """A kernel-free launch on the current stream that waits for ``waits`` and records ``tag``:
+        the join-then-fork point other streams wait on (eager: stream waits + an event record)."""
+        self.launches.append(Launch(f"fork:{tag}", None, stream=self.cur_stream, waits=tuple(waits), record=tag))
 
     def mark(self, tag: str):
         """Record event ``tag`` after the last launch added on the current stream."""
@@ -67,26 +80,31 @@ class Phase:
         if not MULTI_STREAM or all(l.stream == 0 and not l.waits for l in self.launches):
             st = stream() if st is None else st
             for l in self.launches:
-                l(st)
+                if l.fn is not None:
+                    l(st)
             return
         main = torch.cuda.current_stream()
         if self._streams is None or self._streams[0].device != main.device:
             self._streams = [torch.cuda.Stream(device=main.device) for _ in range(3)]
         streams = [main] + self._streams
-        used = {l.stream for l in self.launches}
+        sid_of = lambda l: min(l.stream, MAX_STREAMS - 1)
+        used = {sid_of(l) for l in self.launches}
         start = main.record_event()
         for sid in used - {0}:
             streams[sid].wait_event(start)
         events = {}
         for l in self.launches:
-            s = streams[l.stream]
+            s = streams[sid_of(l)]
             for tag in l.waits:
-                s.wait_event(events[tag])
+                s.wait_event(events[self.alias.get(tag, tag)])
             l(s.cuda_stream)
             if l.record is not None:
                 events[l.record] = s.record_event()
         for sid in used - {0}:
             main.wait_stream(streams[sid])
+        # keep the events alive past this call: under HIP-graph capture they must outlive the capture
+        # (destroying a recorded event while the capture is open crashed hipStreamEndCapture)
+        self._live_events = (start, events)
 
     def __len__(self):
         return len(self.launches)

@@ -56,9 +56,9 @@ def test_inception_program_structure():
     assert len(cbr) == sum(1 for x in m.modules() if isinstance(x, torch.nn.Conv2d)) == 94
     assert len(pools) == 13
     assert (p.feat.act.H, p.feat.act.W, p.feat.act.C) == (1, 6, 2048)
-    n = p.num_launches()
-    assert n["forward_train"] == 94 * 2 + 13 + 1
-    assert n["backward"] == 94 * 2 + 93 + 13 + 1   # the stem conv has no data gradient
+    kernels = lambda ph: sum(1 for l in ph.launches if l.fn is not None)  # not the fork points
+    assert kernels(p.fwd_train) == 94 * 2 + 13 + 1
+    assert kernels(p.bwd) == 94 * 2 + 93 + 13 + 1   # the stem conv has no data gradient
     # Mixed_5b's 1x1 branch writes channels [0, 64) of the 256-wide block buffer in place
     blk = [o for o in cbr if o.conv.mods[0] is m.Mixed_5b.branch1x1.conv][0]
     assert blk.out.act.ld == 256 and blk.out.coff == 0 and blk.out.parent is not None
@@ -82,3 +82,27 @@ def test_wgrad_batching_structure():
     b = [l for l in p.bwd.launches if l.name == "wgrad_batched"]
     assert len(b) == len(cfgs) and sum(l.args[2] for l in b) == n_wg
     assert names.index("wgrad_finalize") == len(names) - 1 and names[-1 - len(b):-1] == ["wgrad_batched"] * len(b)
+
+
+def _check_event_order(ph):
+    seen = set()
+    for l in ph.launches:
+        for w in l.waits:
+            assert ph.alias.get(w, w) in seen, (ph.name, l.name, w)
+        if l.record:
+            seen.add(l.record)
+
+
+def test_stream_events_are_recorded_before_they_are_awaited():
+    """Multi-stream programs (levels || backbone in A, Inception branches on streams 0..3 in C): every
+    event a launch waits on is recorded by an earlier launch, before and after wgrad batching."""
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.models import Multi_Classifier
+    for prog in (MTLProgram(MTL_Net(), 4, "cpu"), InceptionProgram(Multi_Classifier(), 4, "cpu")):
+        for batched in (False, True):
+            if batched:
+                prog.batch_wgrads()
+            for ph in (prog.fwd_train, prog.fwd_eval, prog.bwd):
+                _check_event_order(ph)
+    streams = {l.stream for l in prog.fwd_train.launches}
+    assert streams == {0, 1, 2, 3}  # Inception branches spread over four streams

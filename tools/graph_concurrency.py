@@ -36,6 +36,19 @@ def run(calls, streams):
     main.wait_stream(side)
 
 
+def bench_eager(streams, n=40, reps=20):
+    calls = make_calls(n)
+    run(calls, streams)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        run(calls, streams)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
 def bench(streams, n=40, reps=20):
     calls = make_calls(n)
     run(calls, streams)
@@ -55,4 +68,6 @@ def bench(streams, n=40, reps=20):
 
 
 for st in (1, 2, 1, 2):
-    print(f"{st} stream(s): {bench(st):.1f} us per 40 launches", flush=True)
+    print(f"graph {st} stream(s): {bench(st):.1f} us per 40 launches", flush=True)
+for st in (1, 2, 1, 2):
+    print(f"eager {st} stream(s): {bench_eager(st):.1f} us per 40 launches", flush=True)
