@@ -96,9 +96,11 @@ class LoweredProgram:
                 l.args = self._wgfin_args()
 
     def batch_wgrads(self):
-        """Replace the per-conv weight-gradient launches by one batched launch per tile config, placed
-        right before the finalize (csrc/conv.hip conv_wgrad_batched_kernel).  Called after the autotuner
-        has fixed every conv's wgrad config and split count."""
+        """Replace the per-conv weight-gradient launches by batched launches, one per (stream, tile
+        config) (csrc/conv.hip conv_wgrad_batched_kernel).  Each stream's batch goes after that stream's
+        last kernel -- after its join events, so nothing waits for the batch except the finalize, and e.g.
+        Model A's level-branch weight gradients overlap the backbone's backward.  Called after the
+        autotuner has fixed every conv's wgrad config and split count."""
         ls = self.bwd.launches
         wg = [l for l in ls if l.name == "conv_wgrad"]
         if not wg:
@@ -119,18 +121,27 @@ class LoweredProgram:
                 else:
                     self.bwd.alias[l.record] = prev.record
         self.wgrad_tables = []
-        batched = []
-        for cfg in sorted({l.args[0] for l in wg}):
-            group = [l for l in wg if l.args[0] == cfg]
-            raw, nblocks = lib().wgrad_table(cfg, [l.args[2] for l in group], [l.args[1] for l in group])
-            table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
-            self.wgrad_tables.append(table)
-            batched.append(Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks))
-        batched[-1].record = "wgrads"
-        for l in keep:  # the per-conv "wgrads" event is gone; the finalize now follows the batch in order
+        inserts, tags = [], []
+        for st in sorted({l.stream for l in wg}):
+            batched = []
+            for cfg in sorted({l.args[0] for l in wg if l.stream == st}):
+                group = [l for l in wg if l.stream == st and l.args[0] == cfg]
+                raw, nblocks = lib().wgrad_table(cfg, [l.args[2] for l in group], [l.args[1] for l in group])
+                table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+                self.wgrad_tables.append(table)
+                batched.append(Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, stream=st))
+            batched[-1].record = f"wgrads_s{st}"
+            tags.append(batched[-1].record)
+            pos = max((i for i, k in enumerate(keep) if k.stream == st), default=len(keep) - 1) + 1
+            inserts.append((pos, batched))
+        for pos, batched in sorted(inserts, key=lambda x: -x[0]):
+            keep[pos:pos] = batched
+        for l in keep:  # the per-conv "wgrads" event is gone
             if l.record == "wgrads":
                 l.record = None
-        self.bwd.launches = keep + batched + ls[fin:]
+        fin_l = ls[fin]
+        fin_l.waits = tuple(tags)
+        self.bwd.launches = keep + ls[fin:]
         self.wgrads_batched = True
 
     def _emit_optimizer(self, grad_scale: float = 1.0) -> Dict[str, Phase]:
