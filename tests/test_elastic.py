@@ -33,7 +33,16 @@ def test_fault_injection_elastic_restart_resumes(tmp_path):
            os.path.join(ROOT, "train.py"), "--model", "single_event", "--synthetic", "2", "--batch_size", "4",
            "--epoch_num", "3", "--val_every", "1", "--log_every", "2", "--output_savedir", str(out),
            "--GPU_device", "False", "--resume", "auto", "--save_threshold", "0"]
-    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+    for attempt in range(2):
+        r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+        if r.returncode == 0 or "connectFullMesh failed" not in r.stdout + r.stderr:
+            break
+        # gloo's full-mesh connect of a restarted group occasionally fails under host load (refused /
+        # timed-out TCP connect in gloo itself); that is not what this test checks: run the scenario again
+        import shutil
+        shutil.rmtree(out, ignore_errors=True)
+        port = _free_port()
+        cmd[cmd.index("--rdzv-endpoint") + 1] = f"127.0.0.1:{port}"
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     runs = glob.glob(str(out / "* model_type=single_event is_test=False"))
     assert len(runs) == 1, runs  # the restarted job continued in the same directory
