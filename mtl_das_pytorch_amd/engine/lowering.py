@@ -7,6 +7,7 @@ from typing import Dict, List, Optional
 
 import torch
 
+from ..ops.functional import WGRAD_TILES
 from ..ops.hip import lib
 from .core import Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table
 from .program import Launch, Phase, k_adam, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad, k_wgrad_batched
@@ -123,16 +124,26 @@ class LoweredProgram:
         self.wgrad_tables = []
         inserts, tags = [], []
         for st in sorted({l.stream for l in wg}):
-            batched = []
+            batched, costs = [], []
             for cfg in sorted({l.args[0] for l in wg if l.stream == st}):
                 group = [l for l in wg if l.stream == st and l.args[0] == cfg]
                 raw, nblocks = lib().wgrad_table(cfg, [l.args[2] for l in group], [l.args[1] for l in group])
                 table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
                 self.wgrad_tables.append(table)
                 batched.append(Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, stream=st))
-            batched[-1].record = f"wgrads_s{st}"
-            tags.append(batched[-1].record)
+                TN, TK, MCH = WGRAD_TILES[cfg]
+                costs.append(sum(l.args[2]["splits"] * l.args[2]["m_per_split"] * l.args[1] * TN * TK *
+                                 math.ceil(l.args[2]["Npad"] / TN) * (l.args[2]["Kpad"] // TK) for l in group))
             pos = max((i for i, k in enumerate(keep) if k.stream == st), default=len(keep) - 1) + 1
+            if st == 0 and len(batched) > 1 and pos > 0 and self._fan_out_wgrads():
+                # the main stream's batches form the step's tail (nothing else is left to overlap them):
+                # fan them out over the side streams from one fork point so the tile configs run side by
+                # side instead of back to back
+                batched = self._fan_out(keep, pos, batched, costs)
+                tags += [l.record for l in batched if l.record is not None]
+            else:
+                batched[-1].record = f"wgrads_s{st}"
+                tags.append(batched[-1].record)
             inserts.append((pos, batched))
         for pos, batched in sorted(inserts, key=lambda x: -x[0]):
             keep[pos:pos] = batched
@@ -143,6 +154,42 @@ class LoweredProgram:
         fin_l.waits = tuple(tags)
         self.bwd.launches = keep + ls[fin:]
         self.wgrads_batched = True
+
+    @staticmethod
+    def _fan_out_wgrads() -> bool:
+        # opt-in (MDA_WGRAD_FANOUT=1): measured on MI355X, Model A 25.8k -> 23.3k samples/s with the
+        # fan-out, Model C 6.47k -> 6.51k (docs/PERF.md "Rejected")
+        import os
+        return os.environ.get("MDA_WGRAD_FANOUT", "0") == "1"
+
+    def _fan_out(self, keep: List[Launch], pos: int, batched: List[Launch], costs: List[float]) -> List[Launch]:
+        """Spread the main stream's batched weight-gradient launches over streams 0, 2, 3, 1 (largest
+        first, then greedily onto the least-loaded stream).  Every side stream waits on one event recorded
+        after the main stream's last backward kernel; each stream's last batch records the tag the
+        finalize waits on."""
+        anchor = keep[pos - 1]
+        if anchor.record is None:
+            anchor.record = "wgfork"
+        else:
+            self.bwd.alias["wgfork"] = anchor.record
+        order = sorted(range(len(batched)), key=lambda i: -costs[i])
+        sids = [0, 2, 3, 1]
+        load = {s: 0.0 for s in sids}
+        out: Dict[int, List[Launch]] = {s: [] for s in sids}
+        for n, i in enumerate(order):
+            s = sids[n] if n < len(sids) else min(sids, key=lambda x: load[x])
+            l = batched[i]
+            l.stream = s
+            if s != 0 and not out[s]:
+                l.waits = ("wgfork",)
+            out[s].append(l)
+            load[s] += costs[i]
+        res = []
+        for s in sids:
+            if out[s]:
+                out[s][-1].record = f"wgrads_s0_{s}"
+                res += out[s]
+        return res
 
     def _emit_optimizer(self, grad_scale: float = 1.0) -> Dict[str, Phase]:
         segs = [s for c in self.convs for s in c.opt_segments()]

@@ -72,7 +72,23 @@ def test_inception_program_structure():
 
 def test_wgrad_batching_structure():
     """All per-conv weight-gradient launches collapse into one launch per tile config, just before the
-    finalize; every conv appears in exactly one job table."""
+    finalize; every conv appears in exactly one job table; the finalize waits for every stream's last
+    batch."""
+    p = MTLProgram(MTL_Net(), 32, "cpu")
+    n_wg = sum(1 for l in p.bwd.launches if l.name == "conv_wgrad")
+    p.batch_wgrads()
+    b = [l for l in p.bwd.launches if l.name == "wgrad_batched"]
+    assert sum(l.args[2] for l in b) == n_wg
+    fin = p.bwd.launches[-1]
+    assert fin.name == "wgrad_finalize"
+    assert set(fin.waits) == {f"wgrads_s{s}" for s in {l.stream for l in b}}
+    _check_event_order(p.bwd)
+
+
+def test_wgrad_fanout_structure(monkeypatch):
+    """Opt-in (MDA_WGRAD_FANOUT=1): the main stream's batches are fanned out over the side streams from
+    one fork point."""
+    monkeypatch.setenv("MDA_WGRAD_FANOUT", "1")
     p = MTLProgram(MTL_Net(), 32, "cpu")
     n_wg = sum(1 for l in p.bwd.launches if l.name == "conv_wgrad")
     cfgs = {l.args[0] for l in p.bwd.launches if l.name == "conv_wgrad"}
@@ -83,8 +99,14 @@ def test_wgrad_batching_structure():
     assert len(b) >= len(cfgs) and sum(l.args[2] for l in b) == n_wg
     fin = p.bwd.launches[-1]
     assert fin.name == "wgrad_finalize"
-    # one batch per (stream, config); the finalize waits for every stream's last batch
-    assert set(fin.waits) == {f"wgrads_s{s}" for s in {l.stream for l in b}}
+    # one batch per (stream, config); the finalize waits for every stream's last batch.  The main stream's
+    # batches (the step's tail) are fanned out over the streams from one fork point.
+    assert set(fin.waits) == {l.record for l in b if l.record}
+    assert len(fin.waits) == len({(l.stream, l.record.startswith("wgrads_s0_")) for l in b if l.record})
+    main_tail = [l for l in b if l.record and l.record.startswith("wgrads_s0_")]
+    assert len(main_tail) > 1
+    assert all(l.waits == ("wgfork",) for l in b if l.stream != 0 and l.waits)
+    _check_event_order(p.bwd)
 
 
 def _check_event_order(ph):
