@@ -80,6 +80,7 @@ BNArgs parse_bn(const py::dict& d) {
   b.eps = (float)F(d, "eps", 1e-5);
   b.momentum = (float)F(d, "momentum", 0.1);
   b.training = (int)I(d, "training", 1);
+  b.consts = P<float>(d, "consts");
   return b;
 }
 
@@ -99,6 +100,16 @@ void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
   a.KH = (int)I(d, "KH"); a.KW = (int)I(d, "KW"); a.sh = (int)I(d, "sh"); a.sw = (int)I(d, "sw");
   a.ph = (int)I(d, "ph"); a.pw = (int)I(d, "pw"); a.Kpad = (int)I(d, "Kpad");
   if (a.Cs % 8 || a.N % 4 || a.Kpad % 32 || a.src.C0 + a.src.C1 != a.Cs) throw std::runtime_error("conv: bad geometry");
+  if (d.contains("bnb") && !d["bnb"].is_none()) {  // fused BN-backward statistics (dgrad epilogue)
+    py::dict b = d["bnb"].cast<py::dict>();
+    a.by = P<const bf16_t>(b, "y"); a.bygs = I(b, "ygs"); a.ldby = (int)I(b, "ldy");
+    a.bbn = parse_bn(b["bn"].cast<py::dict>());
+    a.bpart = P<double>(b, "part");
+    a.bkind = (int)I(b, "kind");
+    if (mode != MODE_DGRAD || !a.bpart || !a.by || !a.bbn.stats || !a.bbn.training || a.bbn.C != a.N ||
+        a.ldby % 4 || a.bkind < ACT_NONE || a.bkind > ACT_SIGMOID)
+      throw std::runtime_error("conv: bad fused BN-backward statistics arguments");
+  }
   check(launch_conv(mode, a, G, cfg, S(stream)), "conv");
 }
 

@@ -267,7 +267,7 @@ DEV void bnb_ctx(const TailArgs& a, int z, int cblk, int cgl, BwdCtx& X, float (
     const int k = t / (8 * CGB), j = t - k * 8 * CGB;
     const BNArgs& bk = k ? a.bn2 : a.bn;
     float sc, sh, mu, inv;
-    bn_channel(bk, z, cblk + j, false, sc, sh, mu, inv);
+    bn_channel_bwd(bk, z, cblk + j, sc, sh, mu, inv);
     s_x[k][0][j] = sc; s_x[k][1][j] = sh; s_x[k][2][j] = mu; s_x[k][3][j] = inv;
     s_x[k][4][j] = bk.gamma[bk.pstride * z + cblk + j];
   }
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(FUSED_T) void tail_bwd_fused_kernel(TailArgs a) {
     const int k = threadIdx.x >> 3, j = threadIdx.x & 7;
     const BNArgs& bk = k ? a.bn2 : a.bn;
     float sc, sh, mu, inv;
-    bn_channel(bk, z, c + j, false, sc, sh, mu, inv);
+    bn_channel_bwd(bk, z, c + j, sc, sh, mu, inv);
     s_x[k][0][j] = sc; s_x[k][1][j] = sh; s_x[k][2][j] = mu; s_x[k][3][j] = inv;
     s_x[k][4][j] = bk.gamma[bk.pstride * z + c + j];
   }
@@ -528,8 +528,11 @@ int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t 
   return (int)hipGetLastError();
 }
 
+// fused: 0 = reduce + apply, 1 = single-launch kernel (small maps), 2 = apply only -- the statistics were
+// accumulated into `part` by the epilogue of the dgrad that produced the (single) gradient source.
 int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, hipStream_t st) {
-  if (fused) {
+  if (fused == 2 && (kind > ACT_SIGMOID || a.dzbuf || a.g.n != 1)) return -5;
+  if (fused == 1) {
     const int M = a.B * a.H * a.W;
     const int R = (M + FUSED_T - 1) / FUSED_T;
     // register-cached pixels per thread: up to 4 (2 for the two-BN residual tail) without spilling
@@ -553,8 +556,8 @@ int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, h
   if (!a.part || a.chunk_px <= 0 || nchunk <= 0) return -4;
   const int cgb = bnb_cgb(a.C);
   dim3 grid(nchunk, a.C / (8 * cgb), G);
-#define KC(X, CG)                                                                      \
-  hipLaunchKernelGGL((bnb_reduce_kernel<X, CG>), grid, dim3(BNB_T), 0, st, a);         \
+#define KC(X, CG)                                                                                    \
+  if (fused != 2) hipLaunchKernelGGL((bnb_reduce_kernel<X, CG>), grid, dim3(BNB_T), 0, st, a);       \
   hipLaunchKernelGGL((bnb_apply_kernel<X, CG>), grid, dim3(BNB_T), 0, st, a);
 #define K(X)                                                   \
   case X:                                                      \

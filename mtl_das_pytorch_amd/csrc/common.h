@@ -134,6 +134,9 @@ struct BNArgs {
   int count;             // number of elements per channel reduced into stats (B*H*W)
   float eps, momentum;
   int training;          // 1: batch statistics (and update running), 0: running statistics
+  float* consts;         // optional [G][4][C] (+ z * 4C): scale, shift, mean, invstd of the current batch,
+                         // written by the forward tail's block 0 (training) and read by every backward
+                         // kernel of this BN -- 4 floats per channel instead of 2 x NREP fp64 replicas
 };
 
 // BN constants of channel c of group z: out = y * scale + shift == gamma * (y - mean) * invstd + beta.
@@ -168,9 +171,21 @@ DEV void bn_channel(const BNArgs& a, int z, int c, bool update_running, float& s
   shift = b - mean * g * inv;
 }
 
-// All C channels into LDS (mean / invstd arrays optional -- needed by backward kernels).
+// Backward kernels: the constants the forward tail stored (consts), else recomputed from the replicas.
+DEV void bn_channel_bwd(const BNArgs& a, int z, int c, float& scale, float& shift, float& mean, float& inv) {
+  if (a.consts) {
+    const float* k = a.consts + (int64_t)z * 4 * a.C;
+    scale = k[c]; shift = k[a.C + c]; mean = k[2 * a.C + c]; inv = k[3 * a.C + c];
+  } else {
+    bn_channel(a, z, c, false, scale, shift, mean, inv);
+  }
+}
+
+// All C channels into LDS (mean / invstd arrays optional -- needed by backward kernels).  The block that
+// updates the running statistics also publishes the batch constants (BNArgs::consts) for the backward.
 DEV void bn_prepare(const BNArgs& a, int z, float* s_scale, float* s_shift, float* s_mean, float* s_invstd,
                     bool update_running) {
+  float* kz = (update_running && a.training && a.consts) ? a.consts + (int64_t)z * 4 * a.C : nullptr;
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
     float sc, sh, mu, inv;
     bn_channel(a, z, c, update_running, sc, sh, mu, inv);
@@ -178,6 +193,7 @@ DEV void bn_prepare(const BNArgs& a, int z, float* s_scale, float* s_shift, floa
     s_shift[c] = sh;
     if (s_mean) s_mean[c] = mu;
     if (s_invstd) s_invstd[c] = inv;
+    if (kz) { kz[c] = sc; kz[a.C + c] = sh; kz[2 * a.C + c] = mu; kz[3 * a.C + c] = inv; }
   }
   if (update_running && a.training && threadIdx.x == 0 && a.nbt) a.nbt[z] += 1;
 }

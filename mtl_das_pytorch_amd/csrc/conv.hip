@@ -82,13 +82,25 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   static_assert(WAVES_N * WAVES_M * KSPLIT == 4, "4 waves per block");
   constexpr int FN = WN / 16, FM = WM / 16;
   constexpr int BN_T = WN * WAVES_N, BM_T = WM * WAVES_M;
+  constexpr int TILE = FN * FM * 4 * 64;  // floats per wave accumulator tile
+  constexpr int RED = (KSPLIT - 1) * WAVES_N * WAVES_M * TILE, ST2 = WAVES_M * BN_T * 2;
   extern __shared__ __attribute__((aligned(16))) int s_dyn[];
   int* s_tab = s_dyn;  // [Kpad/8]
   const int nkg = a.Kpad >> 3;
   float* s_red = reinterpret_cast<float*>(s_dyn + ((nkg + 3) & ~3));  // KSPLIT partials, then stats
+  float* s_bn = s_red + (RED > ST2 ? RED : ST2);  // [4][BN_T] fused BN-backward: scale, shift, mean, invstd
   const int z = blockIdx.z;
   const int Ktot = a.KH * a.KW * a.Cs;
   for (int i = threadIdx.x; i < nkg; i += 256) s_tab[i] = encode_kg(i, Ktot, a.Cs >> 3, a.KW, a.src.C0);
+  const bool want_bnb = MODE == MODE_DGRAD && a.bpart != nullptr;
+  if (want_bnb) {
+    for (int i = threadIdx.x; i < BN_T; i += 256) {
+      const int n = blockIdx.y * BN_T + i;
+      float sc = 0.f, sh = 0.f, mu = 0.f, inv = 0.f;
+      if (n < a.N) bn_channel_bwd(a.bbn, z, n, sc, sh, mu, inv);
+      s_bn[i] = sc; s_bn[BN_T + i] = sh; s_bn[2 * BN_T + i] = mu; s_bn[3 * BN_T + i] = inv;
+    }
+  }
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -126,6 +138,17 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const int nks = a.Kpad >> 5;
   const int kchunk = (nks + KSPLIT - 1) / KSPLIT;
   const int kbeg = wk * kchunk, kend = min(nks, kbeg + kchunk);
+  // fused BN backward: the tail's pre-BN y at this lane's output elements, in flight during the K loop
+  uint2 ypre[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int f = 0; f < FM; ++f) {
+      ypre[i][f] = make_uint2(0, 0);
+      const int n0 = n_base + i * 16 + 4 * kgl;
+      if (want_bnb && wk == 0 && n0 < a.N && pv[f])
+        ypre[i][f] = *reinterpret_cast<const uint2*>(a.by + a.bygs * z + (int64_t)(m_base + f * 16 + l16) * a.ldby + n0);
+    }
   bf16x8 a0[FN], b0[FM], a1[FN], b1[FM];
 #define LOAD_STAGE(KS, AF, BF) \
   conv_load_stage<MODE, FN, FM>(a, s_tab, KS, kgl, l16, n_base, pb, py, px, pv, base0, base1, ld0, ld1, wz, AF, BF)
@@ -143,7 +166,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #undef LOAD_STAGE
 #undef MMA_STAGE
 
-  constexpr int TILE = FN * FM * 4 * 64;  // floats per wave accumulator tile
   if (KSPLIT > 1) {
     const int slot = wn + WAVES_N * wm;
     if (wk > 0) {
@@ -176,6 +198,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // (channel, statistic) per block into replica blockIdx.x % NREP.
   float* s_st = s_red;  // [WAVES_M][BN_T][2]
   const bool want_stats = MODE == MODE_FWD && a.stats != nullptr;
+  const bool want_red = want_stats || want_bnb;
   if (wk == 0) {
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
@@ -205,10 +228,30 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           } else {
             float* o = reinterpret_cast<float*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
             *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+            if (want_bnb) {  // dz of the BN tail whose output gradient this is, and its statistics
+              const uint2 u = ypre[i][f];
+              const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                   __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+              const int cl = wn * WN + i * 16 + 4 * kgl;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float t = yv[r] * s_bn[cl + r] + s_bn[BN_T + cl + r];
+                float dz = v[r];
+                if (a.bkind == ACT_RELU) {
+                  dz = t > 0.f ? dz : 0.f;
+                } else if (a.bkind == ACT_SIGMOID) {
+                  const float sg = sigmoidf_(t);
+                  dz *= sg * (1.f - sg);
+                }
+                const float xh = (yv[r] - s_bn[2 * BN_T + cl + r]) * s_bn[3 * BN_T + cl + r];
+                s[r] += dz;
+                ss[r] += dz * xh;
+              }
+            }
           }
         }
       }
-      if (want_stats) {
+      if (want_red) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {  // pixels of a 16-lane row -> lane 15 (DPP, common.h)
           s[r] = row16_sum(s[r]);
@@ -225,9 +268,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       }
     }
   }
-  if (want_stats) {
+  if (want_red) {
     __syncthreads();
     const int rep = blockIdx.x % NREP;
+    // forward: [G][NREP][2][N] (sum y, sum y^2); fused BN backward: rows 0/1 of [G][NREP][3][N]
+    double* dst = want_bnb ? a.bpart : a.stats;
+    const int rows = want_bnb ? 3 : 2;
     for (int q = threadIdx.x; q < BN_T * 2; q += 256) {
       const int cl = q >> 1, which = q & 1;
       const int n = blockIdx.y * BN_T + cl;
@@ -235,7 +281,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         float v = 0.f;
 #pragma unroll
         for (int w2 = 0; w2 < WAVES_M; ++w2) v += s_st[(w2 * BN_T + cl) * 2 + which];
-        atomicAdd(a.stats + ((int64_t)z * NREP + rep) * 2 * a.N + which * a.N + n, (double)v);
+        atomicAdd(dst + ((int64_t)z * NREP + rep) * rows * a.N + which * a.N + n, (double)v);
       }
     }
   }
@@ -446,7 +492,7 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
     constexpr int TILE = (WN / 16) * (WM / 16) * 4 * 64;                                                \
     size_t red = (size_t)(KS - 1) * WAN * WAM * TILE;                                                   \
     size_t st2 = (size_t)WAM * WN * WAN * 2;                                                            \
-    size_t lds = (size_t)nkg4 * 4 + (red > st2 ? red : st2) * 4;                                        \
+    size_t lds = (size_t)nkg4 * 4 + (red > st2 ? red : st2) * 4 + (a.bpart ? 4 * WN * WAN * 4 : 0);     \
     dim3 grid((M + WM * WAM - 1) / (WM * WAM), (a.N + WN * WAN - 1) / (WN * WAN), G);                    \
     hipLaunchKernelGGL((conv_igemm_kernel<MODE, WN, WM, WAN, WAM, KS>), grid, dim3(256), lds, st, a);   \
     break;                                                                                              \

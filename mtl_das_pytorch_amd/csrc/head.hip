@@ -15,13 +15,17 @@
 namespace mda {
 
 
+// One block per (sample, task): the tasks' dependent chains (GAP -> group mean -> softmax -> gradient)
+// run side by side instead of one after the other, and the label is fetched before the GAP.
 __global__ __launch_bounds__(256) void mtl_head_kernel(HeadArgs a) {
-  __shared__ float s_gap[4][256];  // up to 4 tasks x 256 channels
+  __shared__ float s_gap[256];
   __shared__ float s_part[256];
   __shared__ float s_logit[16], s_prob[16];
-  const int b = blockIdx.x;
+  __shared__ int s_lab;
+  const int b = blockIdx.x, t = blockIdx.y;
+  if (threadIdx.x == 0) s_lab = (int)a.labels[(int64_t)b * a.lab_stride + a.lab_off + t];
   const bool valid = a.nvalid == nullptr || b < *a.nvalid;
-  for (int t = 0; t < a.T; ++t) {
+  {
     const bf16_t* f = a.feat + a.fgs * t + (int64_t)b * a.HW * a.ldf;
     // GAP: thread -> (channel, pixel-lane)
     const int lanes = 256 / a.C;  // C in {.., 64, 128, 256}
@@ -34,13 +38,13 @@ __global__ __launch_bounds__(256) void mtl_head_kernel(HeadArgs a) {
     if (threadIdx.x < a.C) {
       float acc = 0.f;
       for (int q = 0; q < lanes; ++q) acc += s_part[q * a.C + threadIdx.x];
-      s_gap[t][threadIdx.x] = acc / (float)a.HW;
+      s_gap[threadIdx.x] = acc / (float)a.HW;
     }
     __syncthreads();
     const int K = a.ncls[t], gsz = a.C / K;
     if (threadIdx.x < K) {
       float acc = 0.f;
-      for (int q = 0; q < gsz; ++q) acc += s_gap[t][threadIdx.x * gsz + q];
+      for (int q = 0; q < gsz; ++q) acc += s_gap[threadIdx.x * gsz + q];
       s_logit[threadIdx.x] = acc / (float)gsz;
     }
     __syncthreads();
@@ -51,7 +55,7 @@ __global__ __launch_bounds__(256) void mtl_head_kernel(HeadArgs a) {
       float se = 0.f;
       for (int k = 0; k < K; ++k) se += __expf(s_logit[k] - mx);
       const float lse = mx + __logf(se);
-      const int lab = (int)a.labels[(int64_t)b * a.lab_stride + a.lab_off + t];
+      const int lab = s_lab;
       for (int k = 0; k < K; ++k) {
         float lp = s_logit[k] - lse;
         a.logp[((int64_t)t * a.B + b) * 16 + k] = lp;
@@ -79,13 +83,12 @@ __global__ __launch_bounds__(256) void mtl_head_kernel(HeadArgs a) {
         d[i] = s_prob[ch / gsz] * scale;
       }
     }
-    __syncthreads();
   }
 }
 
 int launch_mtl_head(const HeadArgs& a, hipStream_t st) {
   if (a.C > 256 || 256 % a.C) return -2;
-  hipLaunchKernelGGL(mtl_head_kernel, dim3(a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(mtl_head_kernel, dim3(a.B, a.T), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -100,35 +103,74 @@ DEV uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 
-__global__ __launch_bounds__(256) void cls_head_kernel(ClsArgs a) {
-  extern __shared__ float sm[];
-  float* s_feat = sm;            // [C]
-  float* s_mask = sm + a.C;      // [C]
-  __shared__ float s_logit[64];
-  const int b = blockIdx.x;
+// One block of 1024 threads per sample; thread t owns channels t and t + 1024.  It loads its GAP inputs,
+// draws its dropout mask and loads its fc weight column W[:, c] ONCE: the column feeds the per-class
+// partial dot products (wave DPP sums, then 16 wave partials in LDS) and, after the softmax, the input
+// gradient -- no second pass over W, no global round trip for d(logits).  (The previous 256-thread form
+// walked W twice with long serial per-thread loops: 134 us per step on Model C.)
+constexpr int CLS_T = 1024, CLS_CPT = 2, CLS_NC = 32;  // threads, channels per thread, cached classes
+__global__ __launch_bounds__(CLS_T) void cls_head_kernel(ClsArgs a) {
+  __shared__ float s_red[CLS_T / 64][64];
+  __shared__ float s_logit[64], s_dl[64];
+  __shared__ int s_lab;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) s_lab = (int)a.labels[b];
   const uint32_t seed = a.seed ? (uint32_t)(*a.seed) : 0u;
   const float keep_scale = a.p_drop > 0.f ? 1.f / (1.f - a.p_drop) : 1.f;
-  for (int c = threadIdx.x; c < a.C; c += 256) {
-    float s = 0.f;
-    for (int p = 0; p < a.HW; ++p) s += bf2f(a.x[((int64_t)b * a.HW + p) * a.ldx + c]);
-    s /= (float)a.HW;
-    float m = 1.f;
-    if (a.p_drop > 0.f) {
-      float u = (hash3(seed, (uint32_t)b, (uint32_t)c) >> 8) * (1.f / 16777216.f);
-      m = u >= a.p_drop ? keep_scale : 0.f;
+  float f[CLS_CPT], msk[CLS_CPT], w[CLS_NC][CLS_CPT];
+#pragma unroll
+  for (int i = 0; i < CLS_CPT; ++i) {
+    const int c = tid + i * CLS_T;
+    f[i] = 0.f; msk[i] = 0.f;
+    if (c < a.C) {
+      float s = 0.f;
+      for (int p = 0; p < a.HW; ++p) s += bf2f(a.x[((int64_t)b * a.HW + p) * a.ldx + c]);
+      s /= (float)a.HW;
+      float m = 1.f;
+      if (a.p_drop > 0.f) {
+        float u = (hash3(seed, (uint32_t)b, (uint32_t)c) >> 8) * (1.f / 16777216.f);
+        m = u >= a.p_drop ? keep_scale : 0.f;
+      }
+      msk[i] = m;
+      f[i] = s * m;
+      a.feat[(int64_t)b * a.C + c] = s * m;
     }
-    s_mask[c] = m;
-    s_feat[c] = s * m;
-    a.feat[(int64_t)b * a.C + c] = s * m;
+  }
+  const bool cached = a.N <= CLS_NC;
+  if (cached) {  // fully unrolled: w[][] stays in registers (compile-time indices)
+#pragma unroll
+    for (int n = 0; n < CLS_NC; ++n) {
+      if (n < a.N) {
+        float p = 0.f;
+#pragma unroll
+        for (int i = 0; i < CLS_CPT; ++i) {
+          const int c = tid + i * CLS_T;
+          w[n][i] = c < a.C ? a.W[(int64_t)n * a.C + c] : 0.f;
+          p += w[n][i] * f[i];
+        }
+        p = wave_sum(p);
+        if (lane == 0) s_red[wid][n] = p;
+      }
+    }
+  } else {
+    for (int n = 0; n < a.N; ++n) {
+      float p = 0.f;
+#pragma unroll
+      for (int i = 0; i < CLS_CPT; ++i) {
+        const int c = tid + i * CLS_T;
+        p += (c < a.C ? a.W[(int64_t)n * a.C + c] : 0.f) * f[i];
+      }
+      p = wave_sum(p);
+      if (lane == 0) s_red[wid][n] = p;
+    }
   }
   __syncthreads();
-  // logits: one wave per output class group
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int n = wid; n < a.N; n += 4) {
+  if (tid < a.N) {
     float acc = 0.f;
-    for (int c = lane; c < a.C; c += 64) acc += a.W[(int64_t)n * a.C + c] * s_feat[c];
-    acc = wave_sum(acc);
-    if (lane == 0) s_logit[n] = acc + a.bias[n];
+#pragma unroll
+    for (int q = 0; q < CLS_T / 64; ++q) acc += s_red[q][tid];
+    s_logit[tid] = acc + a.bias[tid];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -138,7 +180,7 @@ __global__ __launch_bounds__(256) void cls_head_kernel(ClsArgs a) {
     float se = 0.f;
     for (int n = 0; n < a.N; ++n) se += __expf(s_logit[n] - mx);
     const float lse = mx + __logf(se);
-    const int lab = (int)a.labels[b];
+    const int lab = s_lab;
     for (int n = 0; n < a.N; ++n) a.logits[(int64_t)b * a.N + n] = s_logit[n];
     const float loss = lse - s_logit[lab];
     const int pd = am % 16, pe = am / 16, ld_ = lab % 16, le = lab / 16;
@@ -156,17 +198,29 @@ __global__ __launch_bounds__(256) void cls_head_kernel(ClsArgs a) {
     atomicAdd(a.confusion + 256 + le * 16 + pe, 1);
     }
     if (a.dlogits) {
-      for (int n = 0; n < a.N; ++n)
-        a.dlogits[(int64_t)b * a.N + n] = (__expf(s_logit[n] - lse) - (n == lab ? 1.f : 0.f)) / (float)a.B;
+      for (int n = 0; n < a.N; ++n) {
+        const float dl = (__expf(s_logit[n] - lse) - (n == lab ? 1.f : 0.f)) / (float)a.B;
+        s_dl[n] = dl;
+        a.dlogits[(int64_t)b * a.N + n] = dl;
+      }
     }
   }
   if (!a.dx) return;
   __syncthreads();
   // dx[b][p][c] = (sum_n dlogits[n] W[n][c]) * mask[c] / HW
-  for (int c = threadIdx.x; c < a.C; c += 256) {
+#pragma unroll
+  for (int i = 0; i < CLS_CPT; ++i) {
+    const int c = tid + i * CLS_T;
+    if (c >= a.C) continue;
     float acc = 0.f;
-    for (int n = 0; n < a.N; ++n) acc += a.dlogits[(int64_t)b * a.N + n] * a.W[(int64_t)n * a.C + c];
-    acc *= s_mask[c] / (float)a.HW;
+    if (cached) {
+#pragma unroll
+      for (int n = 0; n < CLS_NC; ++n)
+        if (n < a.N) acc += s_dl[n] * w[n][i];
+    } else {
+      for (int n = 0; n < a.N; ++n) acc += s_dl[n] * a.W[(int64_t)n * a.C + c];
+    }
+    acc *= msk[i] / (float)a.HW;
     for (int p = 0; p < a.HW; ++p) a.dx[((int64_t)b * a.HW + p) * a.C + c] = acc;
   }
 }
@@ -189,8 +243,8 @@ __global__ __launch_bounds__(256) void cls_wgrad_kernel(ClsArgs a, int64_t* seed
 }
 
 int launch_cls_head(const ClsArgs& a, int64_t* seed_mut, hipStream_t st) {
-  if (a.N > 64) return -2;
-  hipLaunchKernelGGL(cls_head_kernel, dim3(a.B), dim3(256), (size_t)2 * a.C * sizeof(float), st, a);
+  if (a.N > 64 || a.C > CLS_T * CLS_CPT) return -2;
+  hipLaunchKernelGGL(cls_head_kernel, dim3(a.B), dim3(CLS_T), 0, st, a);
   int rc = (int)hipGetLastError();
   if (rc || !a.dx) return rc;
   const int64_t n = (int64_t)a.N * a.C;

@@ -22,6 +22,15 @@ struct ConvArgs {
   int N, Npad, Cs;
   int KH, KW, sh, sw, ph, pw;
   int Kpad;
+  // DGRAD only, optional (bpart null = off): fused BN-backward statistics.  When this dgrad's output is
+  // the ONLY gradient source of a BN tail with an elementwise activation (ACT_NONE / ACT_RELU /
+  // ACT_SIGMOID), the epilogue recomputes that tail's dz from the stored pre-BN y and accumulates
+  // sum(dz), sum(dz * xhat) per channel into the tail's fp64 replica rows ([G][NREP][3][N], rows 0/1) --
+  // the tail backward then runs its apply pass only (bn.hip launch_tail_bwd, fused == 2).
+  const bf16_t* by; int64_t bygs; int ldby;
+  BNArgs bbn;
+  double* bpart;
+  int bkind;
 };
 
 // ------------------------------------------------------------------------------------------------

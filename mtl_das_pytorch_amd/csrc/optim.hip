@@ -48,7 +48,11 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, int64_t n) {
 // Writes the packed bf16 MFMA images of every conv weight, one thread per 8 packed elements (16-B
 // stores, coalesced); padding is (re)written as zeros.  Segment `kind` selects the image:
 // 1 = forward [Co][(kh,kw,ci)] (rows Npad, cols Kpad_f), 2 = data-gradient [Ci][(kh,kw,co)].
-__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, const OptSeg* __restrict__ segs, int ns) {
+// `step` (non-null after an Adam update): the step counter is advanced here -- the pack runs after the
+// Adam kernel that read it, so the separate one-thread launch is not needed.
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, const OptSeg* __restrict__ segs, int ns,
+                                                   float* step) {
+  if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1.f;
   int lo = 0, hi = ns - 1;
   while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (segs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
   const OptSeg& S = segs[lo];
@@ -94,10 +98,11 @@ int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nb
     int rc = (int)hipGetLastError();
     if (rc) return rc;
   }
-  if (nblocks > 0) hipLaunchKernelGGL(pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, (const float*)a.p, d_segs, ns);
+  float* step = a.update ? const_cast<float*>(a.step) : nullptr;
+  if (nblocks > 0) hipLaunchKernelGGL(pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, (const float*)a.p, d_segs, ns, step);
   int rc = (int)hipGetLastError();
-  if (rc || !a.update) return rc;
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, const_cast<float*>(a.step));
+  if (rc || !a.update || nblocks > 0) return rc;
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
   return (int)hipGetLastError();
 }
 

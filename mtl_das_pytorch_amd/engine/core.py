@@ -271,6 +271,8 @@ class BNLayer:
         # backward: fp64 replica sums of the 2-D tiled BN backward (csrc/bn.hip bnb_*), zeroed per step
         self.nchunk, self.chunk_px = bnb_plan(count, self.C, self.G)
         self.part = arena.zeroed((self.G, NREP, 3, self.C), torch.float64)
+        # batch constants (scale, shift, mean, invstd) published by the forward tail for the backward
+        self.consts = arena.empty((self.G, 4, self.C), torch.float32)
         self.arena = arena
         self.dzbuf = None
 
@@ -280,7 +282,8 @@ class BNLayer:
         return {"stats": P(self.stats), "gamma": P(f.params, f.off(m0.weight)), "beta": P(f.params, f.off(m0.bias)),
                 "run_mean": P(f.bn_mean, f.bn_offsets[id(m0)]), "run_var": P(f.bn_var, f.bn_offsets[id(m0)]),
                 "nbt": P(f.bn_nbt, f.bn_index[id(m0)]), "pstride": self.pstride, "C": self.C, "count": self.count,
-                "eps": self.eps, "momentum": self.momentum, "training": 1 if training else 0}
+                "eps": self.eps, "momentum": self.momentum, "training": 1 if training else 0,
+                "consts": P(self.consts)}
 
     def grad_ptrs(self) -> dict:
         f = self.flat

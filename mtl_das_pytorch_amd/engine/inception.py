@@ -275,6 +275,7 @@ class InceptionProgram(LoweredProgram):
         self.fwd_train = self._emit_forward(True)
         self.fwd_eval = self._emit_forward(False)
         self.bwd = self._emit_backward()
+        self.fuse_dgrad_bn_stats()
         self.opt = self._emit_optimizer()
 
     def _emit_streamed(self, ph: Phase, order, run) -> List[str]:

@@ -77,6 +77,42 @@ class LoweredProgram:
             mode, cfg, G, d = c.dgrad_args(dy, dx)
             ph.add("conv_dgrad", k_conv, mode, cfg, G, d, owner=c)
 
+    def fuse_dgrad_bn_stats(self) -> int:
+        """Move the BN-backward reduction of single-source elementwise tails into the producing dgrad.
+
+        A BN tail whose activation is elementwise (none / ReLU / sigmoid) and whose output gradient has
+        exactly ONE source -- the data gradient of the next conv, written once as fp32 on the tail's own
+        pixel grid -- gets its per-channel sum(dz), sum(dz * xhat) from that dgrad's epilogue
+        (csrc/conv.hip, ConvArgs::bpart), and its backward runs the apply pass only (``fused = 2``): one
+        launch and one full pass over the gradient less per such layer (Model A: the 8 residual-block
+        inner BNs and the 4 attention-generator BNs; Model C: every BasicConv2d feeding exactly one
+        other).  MDA_DGRAD_BNSTATS=0 disables it.  Returns the number of fused layers."""
+        import os
+        self.n_dgrad_bnstats = 0
+        if os.environ.get("MDA_DGRAD_BNSTATS", "1") != "1":
+            return 0
+        producers = {}
+        for l in self.bwd.launches:
+            if l.name == "conv_dgrad":
+                producers[l.args[3]["out"]] = l
+            elif l.name.startswith("tailbwd"):
+                kind, G, nchunk, d = l.args
+                if kind not in (ACT_NONE, ACT_RELU, ACT_SIGMOID) or len(d["g"]) != 1 or d.get("dzbuf"):
+                    continue
+                gp, ggs, gld = d["g"][0]
+                prod = producers.get(gp)
+                if prod is None:
+                    continue
+                mode, cfg, PG, pd = prod.args
+                if (PG != G or pd["ogs"] != ggs or pd["ldo"] != gld or pd["N"] != d["C"] or pd["B"] != d["B"]
+                        or (pd["Ho"], pd["Wo"]) != (d["H"], d["W"]) or d["bn"]["C"] != d["C"]):
+                    continue
+                pd["bnb"] = {"y": d["y"], "ygs": d["ygs"], "ldy": d["ldy"], "bn": d["bn"], "part": d["part"],
+                             "kind": kind}
+                d["fused"] = 2
+                self.n_dgrad_bnstats += 1
+        return self.n_dgrad_bnstats
+
     def set_source(self, X: torch.Tensor, labels: torch.Tensor, idx: torch.Tensor):
         """Bind the dataset tensors the gather launch reads (X [N,C,H,W] fp32, labels [N,2], idx [B])."""
         self.src = (X, labels, idx)

@@ -120,7 +120,10 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return prepare_conv2d(x, w, bias, stride, padding, stats, x2, cfg).run()
 
 
-def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg=None) -> ConvCall:
+def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg=None, bn_stats=None) -> ConvCall:
+    """``bn_stats`` (optional): ``(y, bn, part, kind)`` -- the dgrad output is the gradient of
+    ``act(BN(y))`` and the epilogue accumulates that BN's backward sums sum(dz), sum(dz*xhat) into rows 0/1
+    of ``part`` ([NREP, 3, C] fp64, zero-initialised); see :func:`bn_tail_backward` ``stats_done``."""
     _check(dy, torch.bfloat16)
     B, Ho, Wo, Co = dy.shape
     _, Ci, KH, KW = w.shape
@@ -133,13 +136,21 @@ def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg
     d = {"src": {"p0": ptr(dy), "ld0": Co, "C0": Co, "C1": 0}, "w": ptr(wd), "out": ptr(dx), "ldo": Cs,
          "B": B, "Hs": Ho, "Ws": Wo, "Ho": H, "Wo": W, "N": Cs, "Npad": wd.shape[0], "Cs": Co, "KH": KH, "KW": KW,
          "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": wd.shape[1]}
-    return ConvCall(1, _fwd_cfg(Cs, B * H * W) if cfg is None else cfg, d, dx, (dy, wd))
+    keep = (dy, wd)
+    if bn_stats is not None:
+        y, bn, part, kind = bn_stats
+        _check(y, torch.bfloat16)
+        if part.dtype != torch.float64 or tuple(y.shape) != (B, H, W, Cs):
+            raise ValueError("bn_stats: y must be the [B, H, W, C] bf16 BN input and part fp64 [NREP, 3, C]")
+        d["bnb"] = {"y": ptr(y), "ldy": Cs, "bn": bn, "part": ptr(part), "kind": kind}
+        keep = keep + (y, part)
+    return ConvCall(1, _fwd_cfg(Cs, B * H * W) if cfg is None else cfg, d, dx, keep)
 
 
 def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw: Tuple[int, int], stride=1, padding=0,
-                 cin_stored: Optional[int] = None, cfg: Optional[int] = None):
+                 cin_stored: Optional[int] = None, cfg: Optional[int] = None, bn_stats=None):
     """Gradient w.r.t. the NHWC input: fp32 ``[B, H, W, Cin_stored]``."""
-    return prepare_conv2d_dgrad(dy, w, in_hw, stride, padding, cin_stored, cfg).run()
+    return prepare_conv2d_dgrad(dy, w, in_hw, stride, padding, cin_stored, cfg, bn_stats).run()
 
 
 WGRAD_TILES = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 64), 4: (16, 64, 128),
@@ -246,17 +257,22 @@ def bnb_plan(M: int, C: int, G: int = 1, target_blocks: int = 1024):
 
 def bn_tail_backward(kind: int, y: torch.Tensor, bn: dict, grads: Sequence[torch.Tensor], dgamma, dbeta,
                      r: Optional[torch.Tensor] = None, bn2: Optional[dict] = None, dgamma2=None, dbeta2=None,
-                     fused: bool = False, store_dz: bool = False):
+                     fused: bool = False, store_dz: bool = False, part: Optional[torch.Tensor] = None):
     """Returns ``(dy bf16, side fp32 | None, dy2 bf16 | None)``; writes dgamma/dbeta (and 2) in place.
     ``fused``: single-launch variant (block per 8 channels over all pixels) instead of reduce + apply;
-    ``store_dz``: the reduce stores dz and the apply reads it instead of recomputing it."""
+    ``store_dz``: the reduce stores dz and the apply reads it instead of recomputing it;
+    ``part``: the statistics were already accumulated (by a dgrad with ``bn_stats``): apply pass only."""
     B, H, W, C = y.shape
     nchunk, chunk_px = bnb_plan(B * H * W, C)
-    part = torch.zeros(NREP, 3, C, device=y.device, dtype=torch.float64)
+    mode = int(fused)
+    if part is not None:
+        mode = 2
+    else:
+        part = torch.zeros(NREP, 3, C, device=y.device, dtype=torch.float64)
     dy = torch.empty_like(y)
     d = {"y": ptr(y), "ldy": C, "bn": bn, "B": B, "H": H, "W": W, "C": C,
          "g": [(ptr(g), 0, g.shape[-1]) for g in grads], "part": ptr(part), "chunk_px": chunk_px,
-         "dy": ptr(dy), "ldd": C, "dgamma": ptr(dgamma), "dbeta": ptr(dbeta), "fused": int(fused)}
+         "dy": ptr(dy), "ldd": C, "dgamma": ptr(dgamma), "dbeta": ptr(dbeta), "fused": mode}
     dzbuf = None
     if store_dz:
         dzbuf = torch.empty(B, H, W, C, device=y.device)

@@ -109,6 +109,25 @@ def test_wgrad_fanout_structure(monkeypatch):
     _check_event_order(p.bwd)
 
 
+def test_dgrad_fused_bn_stats_wiring():
+    """Single-source elementwise BN tails take their backward sums from the producing dgrad's epilogue
+    (Model A: 8 residual-block inner BNs + 4 grouped attention-generator BNs)."""
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.models import Multi_Classifier
+    p = MTLProgram(MTL_Net(), 8, "cpu")
+    assert p.n_dgrad_bnstats == 12
+    fused = [l for l in p.bwd.launches if l.name.startswith("tailbwd") and l.args[3].get("fused") == 2]
+    bnb = [l for l in p.bwd.launches if l.name == "conv_dgrad" and "bnb" in l.args[3]]
+    assert len(fused) == len(bnb) == 12
+    for l in fused:
+        kind, G, nchunk, d = l.args
+        prod = [x for x in bnb if x.args[3]["out"] == d["g"][0][0]]
+        assert len(prod) == 1 and prod[0].args[3]["bnb"]["part"] == d["part"] and prod[0].args[2] == G
+        assert p.bwd.launches.index(prod[0]) < p.bwd.launches.index(l)
+    c = InceptionProgram(Multi_Classifier(), 4, "cpu")
+    assert c.n_dgrad_bnstats >= 40
+
+
 def _check_event_order(ph):
     seen = set()
     for l in ph.launches:

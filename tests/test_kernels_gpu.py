@@ -193,6 +193,45 @@ def test_bn_tail_forward_backward(fn, kind, C, fused):
         assert rel(nchw(side), rr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("kind", [0, 1, 2])
+@pytest.mark.parametrize("case", [(4, 17, 42, 32, 16, 3, 1, 1), (4, 9, 21, 64, 128, 3, 2, 1),
+                                  (2, 33, 83, 16, 16, 3, 1, 1), (4, 5, 11, 128, 64, 1, 1, 0)])
+def test_dgrad_fused_bn_backward_stats(fn, kind, case):
+    """conv(act(BN(y))): the dgrad epilogue accumulates the BN-backward sums, the tail runs its apply pass
+    only; dy / dgamma / dbeta against autograd, and against the two-pass (reduce + apply) backward."""
+    B, H, W, C, Co, k, s, p = case
+    g = torch.Generator().manual_seed(30 + kind)
+    y = (torch.randn(B, C, H, W, generator=g) * 2 + 0.3).bfloat16().float().cuda()
+    bn, gamma, beta, rm, rv, nbt = _bn_setup(fn, y, C, seed=kind)
+    w = (torch.randn(Co, C, k, k, generator=g) / math.sqrt(C * k * k)).bfloat16().float().cuda()
+    yr = y.clone().requires_grad_(True)
+    gam = gamma.clone().requires_grad_(True)
+    bet = beta.clone().requires_grad_(True)
+    z = _torch_bn(yr, gam, bet)
+    act = z if kind == 0 else (F.relu(z) if kind == 1 else torch.sigmoid(z))
+    out = F.conv2d(act, w, stride=s, padding=p)
+    go = torch.randn(out.shape, generator=g).bfloat16().float().cuda()
+    out.backward(go)
+    yb = nhwc(y).bfloat16()
+    part = torch.zeros(NREP, 3, C, device="cuda", dtype=torch.float64)
+    dx = fn.conv2d_dgrad(nhwc(go).bfloat16(), w, (H, W), stride=s, padding=p, bn_stats=(yb, bn, part, kind))
+    dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    dy, _, _ = fn.bn_tail_backward(kind, yb, bn, [dx], dg, db, part=part)
+    assert rel(nchw(dy), yr.grad) < 1e-2
+    # the BN sums are cancelling sums (|sum| << sum |terms|): check them in fp64 on the ENGINE's own dx
+    yd, gx = y.double(), nchw(dx).double()
+    mu = yd.mean((0, 2, 3), keepdim=True)
+    inv = torch.rsqrt(yd.var((0, 2, 3), unbiased=False, keepdim=True) + 1e-5)
+    xh = (yd - mu) * inv
+    zz = gamma.double().view(1, -1, 1, 1) * xh + beta.double().view(1, -1, 1, 1)
+    dz = gx if kind == 0 else (gx * (zz > 0) if kind == 1 else gx * torch.sigmoid(zz) * (1 - torch.sigmoid(zz)))
+    assert rel(dg, (dz * xh).sum((0, 2, 3))) < 1e-4
+    assert rel(db, dz.sum((0, 2, 3))) < 1e-4
+    dg2, db2 = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    dy2, _, _ = fn.bn_tail_backward(kind, yb, bn, [dx], dg2, db2)
+    assert rel(dy, dy2) < 1e-4 and rel(dg, dg2) < 1e-5 and rel(db, db2) < 1e-5
+
+
 @pytest.mark.parametrize("fused", [False, True])
 def test_bn_residual_projection(fn, fused):
     g = torch.Generator().manual_seed(20)
