@@ -223,10 +223,10 @@ void cls_head(int64_t stream, py::dict d) {
 }
 
 void gather_batch(int64_t X, int64_t idx, int64_t lab, int lab_w, int64_t out, int64_t lab_out, int B, int Cin, int H,
-                  int W, int64_t stream) {
+                  int W, int64_t stream, int taps, int off) {
   check(launch_gather_batch(reinterpret_cast<const float*>(X), reinterpret_cast<const int64_t*>(idx),
                             reinterpret_cast<const int64_t*>(lab), lab_w, reinterpret_cast<bf16_t*>(out),
-                            reinterpret_cast<int64_t*>(lab_out), B, Cin, H, W, S(stream)), "gather_batch");
+                            reinterpret_cast<int64_t*>(lab_out), B, Cin, H, W, taps, off, S(stream)), "gather_batch");
 }
 
 void pool3(int is_max, int backward, int64_t stream, py::dict d) {
@@ -275,7 +275,9 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("tail_bwd", &tail_bwd);
   m.def("mtl_head", &mtl_head);
   m.def("cls_head", &cls_head);
-  m.def("gather_batch", &gather_batch);
+  m.def("gather_batch", &gather_batch, py::arg("X"), py::arg("idx"), py::arg("lab"), py::arg("lab_w"), py::arg("out"),
+        py::arg("lab_out"), py::arg("B"), py::arg("Cin"), py::arg("H"), py::arg("W"), py::arg("stream"),
+        py::arg("taps") = 0, py::arg("off") = 0);
   m.def("pool3", &pool3);
   m.def("wgrad_table", &wgrad_table);
   m.def("wgrad_batched", &wgrad_batched);

@@ -155,7 +155,7 @@ int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, int fused, h
 int launch_mtl_head(const HeadArgs& a, hipStream_t st);
 int launch_cls_head(const ClsArgs& a, int64_t* seed_mut, hipStream_t st);
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
-                        int64_t* lab_out, int B, int Cin, int H, int W, hipStream_t st);
+                        int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, hipStream_t st);
 int launch_pool3(int is_max, int backward, const PoolArgs& a, hipStream_t st);
 int launch_grad_sum(const GradSrcs& g, float* out, int ldo, int64_t M, int C, hipStream_t st);
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st);

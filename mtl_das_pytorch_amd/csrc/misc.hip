@@ -12,18 +12,31 @@
 
 namespace mda {
 
+// taps > 0 (single-channel input): vertical tap packing for the stem conv -- channel j of pixel (h, w)
+// holds x[h - off + j][w] (zero outside the image, j < taps), so a KHxKW stem over 1 channel runs as a
+// 1xKW conv over KH real channels (engine/core.py stem_pack_geom) instead of wasting 7/8 of its K on
+// zero padding channels.
 __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restrict__ X, const int64_t* __restrict__ idx,
                                                            const int64_t* __restrict__ lab, int lab_w,
                                                            bf16_t* __restrict__ out, int64_t* __restrict__ lab_out,
-                                                           int B, int Cin, int H, int W) {
+                                                           int B, int Cin, int H, int W, int taps, int off) {
   const int64_t M = (int64_t)B * H * W;
   for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < M; p += (int64_t)gridDim.x * 256) {
     const int b = (int)(p / (H * W));
     const int r = (int)(p - (int64_t)b * H * W);
     const int64_t src = idx[b];
     float v[8];
+    if (taps > 0) {
+      const int h = r / W;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) v[c] = c < Cin ? X[(src * Cin + c) * (int64_t)H * W + r] : 0.f;
+      for (int j = 0; j < 8; ++j) {
+        const int hh = h - off + j;
+        v[j] = (j < taps && hh >= 0 && hh < H) ? X[src * (int64_t)H * W + r + (hh - h) * W] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = c < Cin ? X[(src * Cin + c) * (int64_t)H * W + r] : 0.f;
+    }
     store8(out + p * 8, v);
   }
   if (blockIdx.x == 0)
@@ -34,11 +47,12 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restri
 }
 
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
-                        int64_t* lab_out, int B, int Cin, int H, int W, hipStream_t st) {
-  if (Cin > 8) return -2;
+                        int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, hipStream_t st) {
+  if (Cin > 8 || taps > 8 || (taps > 0 && Cin != 1)) return -2;
   const int64_t M = (int64_t)B * H * W;
   int blocks = (int)std::min<int64_t>((M + 255) / 256, 2048);
-  hipLaunchKernelGGL(gather_batch_kernel, dim3(blocks), dim3(256), 0, st, X, idx, lab, lab_w, out, lab_out, B, Cin, H, W);
+  hipLaunchKernelGGL(gather_batch_kernel, dim3(blocks), dim3(256), 0, st, X, idx, lab, lab_w, out, lab_out, B, Cin, H, W,
+                     taps, off);
   return (int)hipGetLastError();
 }
 

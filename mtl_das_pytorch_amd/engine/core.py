@@ -291,13 +291,37 @@ class BNLayer:
         return {"dgamma": P(f.grads, f.off(m0.weight)), "dbeta": P(f.grads, f.off(m0.bias)), "pgs": self.pstride}
 
 
+def stem_pack_geom(m: nn.Conv2d, Hi: int, Wi: int) -> Optional[dict]:
+    """Vertical tap packing of a single-channel stem conv (MI355X-specific lowering; csrc/misc.hip gather).
+
+    The engine stores the 1-channel input as 8 bf16 channels so that every conv runs on the 8-channel
+    k-groups of the MFMA implicit GEMM; for the stem that makes 7/8 of the reduction dimension zeros
+    (Model A: K = 7*7*8 = 392 for 49 real taps).  Instead the gather writes x[h - ph + j][w] into channel j
+    (j < KH), and the stem becomes a 1 x KW conv over KH stored channels with vertical padding folded into
+    the packing: K = KW * 8 (Model A 416 -> 64 padded, Model C 96 -> 32).  The virtual weight
+    [Co][Ci=KH][1][KW] has exactly the memory layout of the real [Co][1][KH][KW], so the packed images,
+    the weight-gradient finalize and the checkpoint format are unchanged.  Returns the virtual geometry,
+    or None when the conv does not qualify (more than one input channel, KH > 8, groups/dilation)."""
+    KH, KW = m.kernel_size
+    if m.in_channels != 1 or KH > 8 or m.groups != 1 or m.dilation != (1, 1):
+        return None
+    sh, sw = m.stride
+    ph, pw = m.padding
+    Ho = (Hi + 2 * ph - KH) // sh + 1
+    Wo = (Wi + 2 * pw - KW) // sw + 1
+    if (Ho - 1) * sh >= Hi:  # the packed rows read are h' = oh * sh, all inside the stored image
+        return None
+    return {"Ci": KH, "KH": 1, "KW": KW, "sh": sh, "sw": sw, "ph": 0, "pw": pw, "Ho": Ho, "Wo": Wo,
+            "taps": KH, "off": ph}
+
+
 class ConvLayer:
     """One convolution (or a group of identically shaped per-task convolutions) lowered to the MFMA
     implicit-GEMM kernels.  Holds the packed bf16 weight images, the wgrad slab and the finalize /
-    Adam-pack descriptors."""
+    Adam-pack descriptors.  ``geom`` overrides the module's geometry with a virtual one (stem_pack_geom)."""
 
     def __init__(self, mods: Sequence[nn.Conv2d], flat: FlatState, arena: Arena, B: int, Hi: int, Wi: int,
-                 cin_stored: Optional[int] = None):
+                 cin_stored: Optional[int] = None, geom: Optional[dict] = None):
         self.mods = list(mods)
         self.G = len(mods)
         m = mods[0]
@@ -308,12 +332,17 @@ class ConvLayer:
         self.ph, self.pw = m.padding
         if m.groups != 1 or m.dilation != (1, 1):
             raise ValueError("grouped / dilated convolutions are not supported")
+        if geom is not None:
+            self.Ci, self.KH, self.KW = geom["Ci"], geom["KH"], geom["KW"]
+            self.sh, self.sw, self.ph, self.pw = geom["sh"], geom["sw"], geom["ph"], geom["pw"]
         self.Cs = cin_stored if cin_stored is not None else self.Ci
         if self.Cs % 8 or self.Co % 8:
             raise ValueError(f"channels must be multiples of 8 (Cin stored {self.Cs}, Cout {self.Co})")
         self.B, self.Hi, self.Wi = B, Hi, Wi
         self.Ho = (Hi + 2 * self.ph - self.KH) // self.sh + 1
         self.Wo = (Wi + 2 * self.pw - self.KW) // self.sw + 1
+        if geom is not None:
+            self.Ho, self.Wo = geom["Ho"], geom["Wo"]
         self.M_out = B * self.Ho * self.Wo
         self.M_in = B * Hi * Wi
         self.has_bias = m.bias is not None

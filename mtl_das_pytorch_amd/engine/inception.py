@@ -24,7 +24,7 @@ import torch
 
 from ..models.multi_classifier import (BasicConv2d, InceptionA, InceptionB, InceptionC, InceptionD, InceptionE,
                                        Multi_Classifier)
-from .core import Act, Arena, BNLayer, ConvLayer, FlatState, P, grads_of, new_act, src_dict
+from .core import Act, Arena, BNLayer, ConvLayer, FlatState, P, grads_of, new_act, src_dict, stem_pack_geom
 from .lowering import ACT_RELU, LoweredProgram
 from .program import Phase, k_cls_head, k_pool, k_wgfin
 
@@ -52,11 +52,11 @@ class Val:
 class CBR:
     """conv -> BN -> ReLU (one BasicConv2d)."""
 
-    def __init__(self, prog: "InceptionProgram", bc: BasicConv2d, src: Val, out: Val):
+    def __init__(self, prog: "InceptionProgram", bc: BasicConv2d, src: Val, out: Val, geom: Optional[dict] = None):
         A, B, f = prog.arena, prog.B, prog.flat
         self.src, self.out = src, out
         s = src.act
-        self.conv = c = ConvLayer([bc.conv], f, A, B, s.H, s.W, cin_stored=s.C)
+        self.conv = c = ConvLayer([bc.conv], f, A, B, s.H, s.W, cin_stored=s.C, geom=geom)
         if (c.Ho, c.Wo, c.Co) != (out.act.H, out.act.W, out.act.C):
             raise ValueError(f"shape mismatch lowering {bc}: conv gives {(c.Ho, c.Wo, c.Co)}, "
                              f"destination {(out.act.H, out.act.W, out.act.C)}")
@@ -142,7 +142,7 @@ class InceptionProgram(LoweredProgram):
         self.ops.append(op)
         self.op_meta.append(self._cur)
 
-    def _cbr(self, bc: BasicConv2d, src: Val, out: Optional[Val] = None) -> Val:
+    def _cbr(self, bc: BasicConv2d, src: Val, out: Optional[Val] = None, geom: Optional[dict] = None) -> Val:
         if out is None:
             kh, kw = bc.conv.kernel_size
             sh, sw = bc.conv.stride
@@ -150,7 +150,7 @@ class InceptionProgram(LoweredProgram):
             H = (src.act.H + 2 * ph - kh) // sh + 1
             W = (src.act.W + 2 * pw - kw) // sw + 1
             out = self._val(H, W, bc.conv.out_channels)
-        self._push(CBR(self, bc, src, out))
+        self._push(CBR(self, bc, src, out, geom))
         return out
 
     def _pool(self, is_max: bool, src: Val, out: Optional[Val] = None) -> Val:
@@ -231,7 +231,10 @@ class InceptionProgram(LoweredProgram):
         self.op_meta = []   # per op: None (stem, stream 0) or (block index, branch index)
         self._bi, self._cur = 0, None
         v = Val(Act(self.x, 0, 8, 8, 0, B, self.H0, self.W0), needs_grad=False)
-        v = self._cbr(m.Conv2d_1a_3x3, v)
+        geom = stem_pack_geom(m.Conv2d_1a_3x3.conv, self.H0, self.W0)  # 1-channel input: taps as channels
+        if geom is not None:
+            self.stem_pack = (geom["taps"], geom["off"])
+        v = self._cbr(m.Conv2d_1a_3x3, v, geom=geom)
         v = self._cbr(m.Conv2d_2a_3x3, v)
         v = self._cbr(m.Conv2d_2b_3x3, v)
         v = self._pool(True, v)

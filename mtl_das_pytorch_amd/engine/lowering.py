@@ -117,9 +117,14 @@ class LoweredProgram:
         """Bind the dataset tensors the gather launch reads (X [N,C,H,W] fp32, labels [N,2], idx [B])."""
         self.src = (X, labels, idx)
 
+    stem_pack = (0, 0)  # (taps, offset) of the gather's vertical tap packing (core.stem_pack_geom)
+
     def gather_phase(self, X, labels, idx) -> Phase:
         ph = Phase("gather")
-        ph.add("gather", k_gather, X, idx, labels, self.label_width, self.x, self.labels, self.B, X.shape[1], self.H0, self.W0)
+        if self.stem_pack[0] and X.shape[1] != 1:
+            raise ValueError("stem tap packing needs a single-channel input")
+        ph.add("gather", k_gather, X, idx, labels, self.label_width, self.x, self.labels, self.B, X.shape[1], self.H0,
+               self.W0, *self.stem_pack)
         return ph
 
     def _wgfin_args(self):

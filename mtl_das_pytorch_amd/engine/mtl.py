@@ -27,7 +27,7 @@ import torch
 
 from ..models.mtl import MTLNet
 from ..ops.hip import lib
-from .core import NREP, Act, Arena, BNLayer, ConvLayer, FlatState, P, new_act, src_dict
+from .core import NREP, Act, Arena, BNLayer, ConvLayer, FlatState, P, new_act, src_dict, stem_pack_geom
 from .lowering import ACT_NONE, ACT_RELU, ACT_SIGMOID, ADD_RELU, POOL_RELU, SIGMUL, LoweredProgram
 from .program import Phase, k_head, k_wgfin
 
@@ -81,7 +81,10 @@ class MTLProgram(LoweredProgram):
         self.labels = torch.zeros((B, 2), dtype=torch.int64, device=self.device)
         self.xin = Act(self.x, 0, 8, 8, 0, B, self.H0, self.W0)
         # stem
-        c1 = ConvLayer([m.conv1[0]], f, A, B, self.H0, self.W0, cin_stored=8)
+        geom = stem_pack_geom(m.conv1[0], self.H0, self.W0)  # 1-channel input: taps packed as channels
+        if geom is not None:
+            self.stem_pack = (geom["taps"], geom["off"])
+        c1 = ConvLayer([m.conv1[0]], f, A, B, self.H0, self.W0, cin_stored=8, geom=geom)
         self.conv1 = c1
         H, W = c1.Ho, c1.Wo
         self.bn1 = BNLayer([m.conv1[1]], f, A, B * H * W)

@@ -151,6 +151,6 @@ def k_adam(d, st):
     lib().adam_pack(st, d)
 
 
-def k_gather(X, idx, lab, lab_w, out, lab_out, B, Cin, H, W, st):
+def k_gather(X, idx, lab, lab_w, out, lab_out, B, Cin, H, W, taps, off, st):
     lib().gather_batch(X.data_ptr(), idx.data_ptr(), lab.data_ptr(), lab_w, out.data_ptr(), lab_out.data_ptr(),
-                       B, Cin, H, W, st)
+                       B, Cin, H, W, st, taps, off)

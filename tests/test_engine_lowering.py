@@ -128,6 +128,27 @@ def test_dgrad_fused_bn_stats_wiring():
     assert c.n_dgrad_bnstats >= 40
 
 
+def test_stem_tap_packing_geometry():
+    """Single-channel stems run as 1 x KW convs over KH packed taps (the gather writes x[h - ph + j] into
+    channel j): Model A's reduction shrinks from 416 to 64, Model C's from 96 to 32; output shapes and the
+    weight layout seen by pack / finalize are the real ones."""
+    from mtl_das_pytorch_amd.engine.core import stem_pack_geom
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.models import Multi_Classifier
+    p = MTLProgram(MTL_Net(), 4, "cpu")
+    c1 = p.conv1
+    assert p.stem_pack == (7, 2)
+    assert (c1.Ci, c1.KH, c1.KW, c1.Cs, c1.ph, c1.pw, c1.Ho, c1.Wo, c1.Kpad) == (7, 1, 7, 8, 0, 2, 33, 83, 64)
+    d = c1.finalize_desc()
+    assert d["elems"] == 16 * 7 * 8 and (d["Ci"], d["KH"], d["KW"]) == (7, 1, 7)
+    c = InceptionProgram(Multi_Classifier(), 4, "cpu")
+    s = c.ops[0].conv
+    assert c.stem_pack == (3, 0) and (s.Ho, s.Wo, s.Kpad) == (49, 124, 32)
+    assert stem_pack_geom(MTL_Net(in_channels=2).conv1[0], 100, 250) is None
+    p2 = MTLProgram(MTL_Net(in_channels=2), 4, "cpu")
+    assert p2.stem_pack == (0, 0) and p2.conv1.Kpad == 416  # 7*7*8 padded to 32
+
+
 def _check_event_order(ph):
     seen = set()
     for l in ph.launches:
