@@ -282,6 +282,9 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("wgrad_table", &wgrad_table);
   m.def("wgrad_batched", &wgrad_batched);
   m.def("grad_sum", &grad_sum);
+  m.def("tick", [](int64_t buf, int i, int64_t stream) {
+    check(launch_tick(reinterpret_cast<uint64_t*>(static_cast<intptr_t>(buf)), i, S(stream)), "tick");
+  });
   m.def("adam_pack", &adam_pack);
   m.def("hip_device_sync", []() { return (int)hipDeviceSynchronize(); });
 }

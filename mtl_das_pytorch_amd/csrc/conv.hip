@@ -449,35 +449,56 @@ __global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob*
 
 // Sums the split-M partial slabs of many convolutions into the flat fp32 gradient buffer (deterministic,
 // one launch per backward), reference weight layout [Cout][Cin][KH][KW].
+// Each weight is reduced by D.lanes threads (a power of two <= 16, chosen per conv from its split count):
+// lane q sums splits q, q + lanes, ... and the lane partials are added in lane order through LDS --
+// deterministic, and a conv with many splits no longer sets the launch's length with one long serial
+// chain of loads.  The lane is the slow thread index of a block (block = 256/lanes weights x lanes), so
+// neighbouring threads still read neighbouring slab columns.  Descriptors own whole blocks, so `lanes`
+// is uniform within a block.
 __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale) {
+  __shared__ float s_part[256];
   int lo = 0, hi = nd - 1;  // last descriptor with block0 <= blockIdx.x
   while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (descs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
   const WgFinDesc& D = descs[lo];
+  const int L = D.lanes, EPB = 256 / L;
   // threads walk the slab in its own (k-fastest) order so the split reads are coalesced; the single
   // write per weight is scattered into the NCHW layout.
   const int Kt = D.KH * D.KW * D.Cs;
-  const int64_t e = ((int64_t)blockIdx.x - D.block0) * 256 + threadIdx.x;
-  if (e >= D.elems) return;
+  const int q = threadIdx.x / EPB, ie = threadIdx.x - q * EPB;
+  const int64_t e = ((int64_t)blockIdx.x - D.block0) * EPB + ie;
   const int64_t per = (int64_t)D.Co * Kt;
   const int g = (int)(e / per);
   int64_t r = e - g * per;
   const int co = (int)(r / Kt);
   const int k = (int)(r - (int64_t)co * Kt);
   const int ci = k % D.Cs, tap = k / D.Cs;
-  if (ci >= D.Ci) return;
+  const bool ok = e < D.elems && ci < D.Ci;
   const int kh = tap / D.KW, kw = tap - kh * D.KW;
   const float* s = D.slab + (((int64_t)g * D.splits) * D.Npad + co) * D.Kpad + k;
   const int64_t sstride = (int64_t)D.Npad * D.Kpad;
-  // 8 independent partial sums keep 8 loads in flight (the split count reaches ~150 on the big-M layers)
+  // 8 independent partial sums keep 8 loads in flight per thread
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int sp = 0;
-  for (; sp + 8 <= D.splits; sp += 8) {
+  if (ok) {
+    int sp = q;
+    for (; sp + 7 * L < D.splits; sp += 8 * L) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += s[(sp + j) * sstride];
+      for (int j = 0; j < 8; ++j) acc[j] += s[(int64_t)(sp + j * L) * sstride];
+    }
+    for (; sp < D.splits; sp += L) acc[0] += s[(int64_t)sp * sstride];
   }
-  for (; sp < D.splits; ++sp) acc[0] += s[sp * sstride];
-  const float t = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  D.grad[g * D.ggs + (((int64_t)co * D.Ci + ci) * D.KH + kh) * D.KW + kw] = t * scale;
+  const float v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  float* dst = D.grad + g * D.ggs + (((int64_t)co * D.Ci + ci) * D.KH + kh) * D.KW + kw;
+  if (L == 1) {
+    if (ok) *dst = v * scale;
+    return;
+  }
+  s_part[threadIdx.x] = v;
+  __syncthreads();
+  if (ok && q == 0) {
+    float sum = 0.f;
+    for (int j = 0; j < L; ++j) sum += s_part[j * EPB + ie];
+    *dst = sum * scale;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -522,24 +543,27 @@ int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
   return mode == MODE_FWD ? launch_conv_cfg<MODE_FWD>(a, G, cfg, st) : launch_conv_cfg<MODE_DGRAD>(a, G, cfg, st);
 }
 
+// Weight-gradient tile configurations (TN = output channels, TK = reduction columns, MCH = pixels per
+// LDS chunk); keep in sync with wgrad_tile_shape and ops/functional.py WGRAD_TILES.  Configs 8-11 cover
+// the whole reduction of a small-Cout layer in one tile: dy is read once per pixel and the im2col taps
+// of neighbouring pixels re-hit L1, instead of every 32-wide K tile re-reading dy and its im2col slice
+// from L2 (Model A's 16-channel 33x83 layers moved ~50 MB of L2 traffic each with TK = 32).
+#define WGRAD_CFG_CASES(X)                                                                          \
+  case 0: X(16, 32, 128) case 1: X(32, 32, 128) case 2: X(32, 64, 64) case 3: X(64, 64, 64)         \
+  case 4: X(16, 64, 128) case 5: X(16, 32, 256) case 6: X(32, 32, 256) case 7: X(64, 32, 64)        \
+  case 8: X(16, 192, 64) case 9: X(16, 128, 64) case 10: X(32, 192, 64) case 11: X(32, 320, 32)
+
 int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st) {
-  const int ntn = (a.Npad + 15) / 16;
 #define LAUNCH_WG(TN, TK, MCH)                                                                      \
   {                                                                                                 \
     dim3 grid(((a.Npad + TN - 1) / TN) * (a.Kpad / TK), a.splits, G);                               \
     hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, a);                \
     break;                                                                                          \
   }
-  (void)ntn;
+  int TN_, TK_;
+  if (wgrad_tile_shape(cfg, TN_, TK_) || a.Kpad % TK_) return -2;  // the K tiles must cover Kpad exactly
   switch (cfg) {
-    case 0: LAUNCH_WG(16, 32, 128)
-    case 1: LAUNCH_WG(32, 32, 128)
-    case 2: LAUNCH_WG(32, 64, 64)
-    case 3: LAUNCH_WG(64, 64, 64)
-    case 4: LAUNCH_WG(16, 64, 128)
-    case 5: LAUNCH_WG(16, 32, 256)
-    case 6: LAUNCH_WG(32, 32, 256)
-    case 7: LAUNCH_WG(64, 32, 64)
+    WGRAD_CFG_CASES(LAUNCH_WG)
     default: return -1;
   }
 #undef LAUNCH_WG
@@ -547,8 +571,9 @@ int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st) {
 }
 
 int wgrad_tile_shape(int cfg, int& TN, int& TK) {
-  static const int tn[8] = {16, 32, 32, 64, 16, 16, 32, 64}, tk[8] = {32, 32, 64, 64, 64, 32, 32, 32};
-  if (cfg < 0 || cfg > 7) return -1;
+  static const int tn[] = {16, 32, 32, 64, 16, 16, 32, 64, 16, 16, 32, 32};
+  static const int tk[] = {32, 32, 64, 64, 64, 32, 32, 32, 192, 128, 192, 320};
+  if (cfg < 0 || cfg >= (int)(sizeof(tn) / sizeof(tn[0]))) return -1;
   TN = tn[cfg]; TK = tk[cfg];
   return 0;
 }
@@ -560,14 +585,7 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
   hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, d_jobs, nj); \
   break;
   switch (cfg) {
-    case 0: LAUNCH_WGB(16, 32, 128)
-    case 1: LAUNCH_WGB(32, 32, 128)
-    case 2: LAUNCH_WGB(32, 64, 64)
-    case 3: LAUNCH_WGB(64, 64, 64)
-    case 4: LAUNCH_WGB(16, 64, 128)
-    case 5: LAUNCH_WGB(16, 32, 256)
-    case 6: LAUNCH_WGB(32, 32, 256)
-    case 7: LAUNCH_WGB(64, 32, 64)
+    WGRAD_CFG_CASES(LAUNCH_WGB)
     default: return -1;
   }
 #undef LAUNCH_WGB

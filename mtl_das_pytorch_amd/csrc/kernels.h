@@ -64,6 +64,7 @@ struct WgFinDesc {
   float* grad;        // NCHW weight grad of group 0
   int64_t ggs;        // element stride between groups in the flat grad buffer
   int G, splits, Npad, Kpad, Co, Ci, Cs, KH, KW;
+  int lanes;          // threads per weight (power of two <= 16): the splits are summed in lanes x parallel
   int64_t elems;      // G * Co * Ci * KH * KW
   int64_t block0;     // first block index of this descriptor
 };
@@ -157,6 +158,7 @@ int launch_cls_head(const ClsArgs& a, int64_t* seed_mut, hipStream_t st);
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
                         int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, hipStream_t st);
 int launch_pool3(int is_max, int backward, const PoolArgs& a, hipStream_t st);
+int launch_tick(uint64_t* buf, int i, hipStream_t st);
 int launch_grad_sum(const GradSrcs& g, float* out, int ldo, int64_t M, int C, hipStream_t st);
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st);
 

@@ -155,6 +155,15 @@ int launch_pool3(int is_max, int backward, const PoolArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// In-graph timeline stamp (tools/timeline.py): one thread stores the 100 MHz wall clock after the work
+// enqueued before it on its stream -- a profiler-free view of multi-stream graph replays.
+__global__ void tick_kernel(uint64_t* buf, int i) { buf[i] = wall_clock64(); }
+
+int launch_tick(uint64_t* buf, int i, hipStream_t st) {
+  hipLaunchKernelGGL(tick_kernel, dim3(1), dim3(1), 0, st, buf, i);
+  return (int)hipGetLastError();
+}
+
 // sum of up to 6 fp32 gradient sources into one buffer (used where a consumer is not a fused tail)
 __global__ __launch_bounds__(256) void grad_sum_kernel(GradSrcs g, float* out, int ldo, int64_t M, int C) {
   const int CG = C >> 3;

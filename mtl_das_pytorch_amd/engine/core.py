@@ -359,7 +359,7 @@ class ConvLayer:
         # largest split count any config can ask for)
         self.Kpad_w = pad_to(taps * self.Cs, 64)
         self._wgrad_args = None
-        max_splits = max(self.wgrad_plan(c)[0] for c in WGRAD_TILES)
+        max_splits = max(self.wgrad_plan(c)[0] for c in WGRAD_TILES if self.wgrad_valid(c))
         self.slab = arena.empty((self.G, max_splits, self.Npad, self.Kpad_w), torch.float32)
         self.set_wgrad_cfg(wgrad_cfg(self.Co, self.Kpad_w))
 
@@ -369,11 +369,18 @@ class ConvLayer:
     # finalize (Model C: ~0.9 GB/step of slab traffic with grid-filling splits)
     MIN_SPLIT_PX = 1024
 
+    def wgrad_valid(self, cfg: int) -> bool:
+        """The K tiles of ``cfg`` cover this conv's padded reduction exactly."""
+        return self.Kpad_w % WGRAD_TILES[cfg][1] == 0
+
     def wgrad_plan(self, cfg: int):
         TN, TK, MCH = WGRAD_TILES[cfg]
         tiles = math.ceil(self.Npad / TN) * (self.Kpad_w // TK) * self.G
+        # whole-reduction tiles (TK >= 128) have one tile per channel block: shorter per-block pixel
+        # ranges keep enough blocks in flight (the finalize sums the extra splits with several lanes)
+        min_px = self.MIN_SPLIT_PX // 2 if TK >= 128 else self.MIN_SPLIT_PX
         splits = max(1, min(math.ceil(self.M_out / MCH), math.ceil(512 / tiles),
-                            math.ceil(self.M_out / self.MIN_SPLIT_PX)))
+                            math.ceil(self.M_out / min_px)))
         mps = pad_to(math.ceil(self.M_out / splits), MCH)
         return math.ceil(self.M_out / mps), mps
 
@@ -442,19 +449,32 @@ class ConvLayer:
 
 # ------------------------------------------------------------------------------------------------
 # descriptor tables (uploaded once; read by wgrad_finalize / adam_pack)
+def finalize_lanes(splits: int) -> int:
+    """Threads per weight in wgrad_finalize: about 8 splits per thread, a power of two <= 16
+    (MDA_FIN_LANES caps it; 1 = one thread per weight)."""
+    import os
+    cap = int(os.environ.get("MDA_FIN_LANES", "16"))
+    lanes = 1
+    while lanes < cap and splits > 8 * lanes:
+        lanes *= 2
+    return lanes
+
+
 def build_wgfin_table(descs: List[dict], device) -> tuple:
     """Pack WgFinDesc structs (layout must match csrc/kernels.h)."""
     dt = np.dtype([("slab", "<u8"), ("grad", "<u8"), ("ggs", "<i8"), ("G", "<i4"), ("splits", "<i4"),
                    ("Npad", "<i4"), ("Kpad", "<i4"), ("Co", "<i4"), ("Ci", "<i4"), ("Cs", "<i4"), ("KH", "<i4"),
-                   ("KW", "<i4"), ("_pad", "<i4"), ("elems", "<i8"), ("block0", "<i8")])
+                   ("KW", "<i4"), ("lanes", "<i4"), ("elems", "<i8"), ("block0", "<i8")])
     assert dt.itemsize == lib().SIZEOF_WGFIN, (dt.itemsize, lib().SIZEOF_WGFIN)
     arr = np.zeros(len(descs), dtype=dt)
     b0 = 0
     for i, d in enumerate(descs):
         for k, v in d.items():
             arr[i][k] = v
+        lanes = finalize_lanes(d["splits"])
+        arr[i]["lanes"] = lanes
         arr[i]["block0"] = b0
-        b0 += math.ceil(d["elems"] / 256)
+        b0 += math.ceil(d["elems"] * lanes / 256)
     t = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
     return t, len(descs), b0
 

@@ -149,10 +149,13 @@ class LoweredProgram:
             return
         fin = next(i for i, l in enumerate(ls) if l.name == "wgrad_finalize")
         keep = []
+        anchor_of = {}  # stream-0 wgrad -> the last kept stream-0 launch before it (its dy producer)
         for l in ls[:fin]:
             if l.name != "conv_wgrad":
                 keep.append(l)
                 continue
+            if l.stream == 0:
+                anchor_of[id(l)] = next((k for k in reversed(keep) if k.stream == 0), None)
             if l.record is not None and l.record != "wgrads":
                 # an event recorded on a removed launch now stands for the stream's previous kept launch
                 prev = next((k for k in reversed(keep) if k.stream == l.stream), None)
@@ -162,6 +165,7 @@ class LoweredProgram:
                     prev.record = l.record
                 else:
                     self.bwd.alias[l.record] = prev.record
+        staged = self._stage_wgrads(wg, ls, anchor_of)
         self.wgrad_tables = []
         inserts, tags = [], []
         for st in sorted({l.stream for l in wg}):
@@ -176,6 +180,9 @@ class LoweredProgram:
                 costs.append(sum(l.args[2]["splits"] * l.args[2]["m_per_split"] * l.args[1] * TN * TK *
                                  math.ceil(l.args[2]["Npad"] / TN) * (l.args[2]["Kpad"] // TK) for l in group))
             pos = max((i for i, k in enumerate(keep) if k.stream == st), default=len(keep) - 1) + 1
+            if staged is not None and st == staged[0]:
+                pos = keep.index(staged[1]) + 1
+                batched[0].waits = ("wgstage",)
             if st == 0 and len(batched) > 1 and pos > 0 and self._fan_out_wgrads():
                 # the main stream's batches form the step's tail (nothing else is left to overlap them):
                 # fan them out over the side streams from one fork point so the tile configs run side by
@@ -195,6 +202,31 @@ class LoweredProgram:
         fin_l.waits = tuple(tags)
         self.bwd.launches = keep + ls[fin:]
         self.wgrads_batched = True
+
+    STAGE_STREAM = 2
+
+    def _stage_wgrads(self, wg: List[Launch], ls: List[Launch], anchor_of: dict):
+        """MDA_WGRAD_STAGE=f (0 < f < 1): the first fraction f (program order) of the main stream's weight
+        gradients -- the deep layers, whose backward kernels leave most CUs idle -- are batched on side
+        stream 2 right after their last dy is produced (one fork event), overlapping the rest of the
+        backbone's backward instead of queueing at the step's tail.  Only when stream 2 is otherwise
+        unused (Model A/B).  Returns (stream, anchor launch) or None."""
+        import os
+        frac = float(os.environ.get("MDA_WGRAD_STAGE", "0"))
+        wg0 = [l for l in wg if l.stream == 0]
+        n1 = int(len(wg0) * frac)
+        if not 0 < n1 < len(wg0) or any(l.stream == self.STAGE_STREAM for l in ls):
+            return None
+        anchor = anchor_of[id(wg0[n1 - 1])]
+        if anchor is None:
+            return None
+        if anchor.record is None:
+            anchor.record = "wgstage"
+        else:
+            self.bwd.alias["wgstage"] = anchor.record
+        for l in wg0[:n1]:
+            l.stream = self.STAGE_STREAM
+        return self.STAGE_STREAM, anchor
 
     @staticmethod
     def _fan_out_wgrads() -> bool:

@@ -15,6 +15,7 @@ from typing import Dict, Iterable, Optional
 
 import torch
 
+from ..ops.functional import WGRAD_TILES
 from ..ops.hip import lib
 
 CONV_CFGS = list(range(14))
@@ -23,7 +24,7 @@ CONV_CFGS = list(range(14))
 def fused_max_m(kind: int) -> int:
     """csrc/bn.hip tail_bwd_fused_kernel: 1024 threads x <= 4 register-cached pixels (2 for ADD_RELU)."""
     return 1024 * (2 if kind == 4 else 4)
-WGRAD_CFGS = list(range(8))
+WGRAD_CFGS = sorted(WGRAD_TILES)
 _CACHE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_cfgs.json")
 
 
@@ -102,6 +103,8 @@ def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, ve
             if sig not in cache:
                 best, best_t = cfg, float("inf")
                 for c in WGRAD_CFGS:
+                    if not conv.wgrad_valid(c):
+                        continue
                     conv.set_wgrad_cfg(c)
                     t = _time(lambda: L.wgrad(c, G, torch.cuda.current_stream().cuda_stream, d))
                     if t < best_t:

@@ -154,7 +154,9 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw: Tuple[int, int], stri
 
 
 WGRAD_TILES = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 64), 4: (16, 64, 128),
-               5: (16, 32, 256), 6: (32, 32, 256), 7: (64, 32, 64)}  # (TN, TK, MCH), csrc/conv.hip
+               5: (16, 32, 256), 6: (32, 32, 256), 7: (64, 32, 64),
+               # whole-reduction tiles for small-Cout layers (csrc/conv.hip WGRAD_CFG_CASES)
+               8: (16, 192, 64), 9: (16, 128, 64), 10: (32, 192, 64), 11: (32, 320, 32)}  # (TN, TK, MCH)
 
 
 def wgrad_cfg(Co: int, Kpad: int) -> int:
@@ -176,6 +178,8 @@ def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=No
     if cfg is None:
         cfg = wgrad_cfg(Co, Kpad)
     TN, TK, MCH = WGRAD_TILES[cfg]
+    if Kpad % TK:
+        raise ValueError(f"wgrad config {cfg} (TK={TK}) does not tile the padded reduction {Kpad}")
     M = B * Ho * Wo
     tiles = math.ceil(Npad / TN) * (Kpad // TK)
     if splits is None:

@@ -95,6 +95,20 @@ def test_conv_wgrad(fn, case):
     assert rel(dw, w.grad) < 5e-3
 
 
+@pytest.mark.parametrize("case,cfg", [((2, 33, 83, 16, 16, 3, 1, 1), 8), ((2, 33, 83, 16, 16, 3, 1, 1), 10),
+                                      ((2, 33, 83, 8, 16, 3, 1, 1), 9), ((2, 17, 42, 32, 32, 3, 1, 1), 11),
+                                      ((2, 33, 83, 16, 32, 3, 2, 1), 10), ((4, 9, 21, 32, 32, 3, 1, 1), 11)])
+def test_conv_wgrad_whole_k_tiles(fn, case, cfg):
+    """Whole-reduction weight-gradient tiles (configs 8-11) and the multi-lane finalize of many splits."""
+    x, w, b, s, p = _mk(case, seed=3)
+    w.requires_grad_(True)
+    ref = F.conv2d(x, w, None, stride=s, padding=p)
+    dy = torch.randn_like(ref).bfloat16().float()
+    ref.backward(dy)
+    dw = fn.conv2d_wgrad(nhwc(x).bfloat16(), nhwc(dy).bfloat16(), w.shape, stride=s, padding=p, cfg=cfg)
+    assert rel(dw, w.grad) < 5e-3
+
+
 def test_conv_two_segment_input(fn):
     g = torch.Generator().manual_seed(3)
     a = torch.randn(2, 32, 17, 42, generator=g).bfloat16().float().cuda()
