@@ -6,7 +6,7 @@
 
 namespace mda {
 
-enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD_BNS = 2 };  // 2: dgrad + fused BN-backward statistics
 
 struct ConvArgs {
   Src2 src;
