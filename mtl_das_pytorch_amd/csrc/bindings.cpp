@@ -110,6 +110,15 @@ void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
         a.ldby % 4 || a.bkind < ACT_NONE || a.bkind > ACT_SIGMOID)
       throw std::runtime_error("conv: bad fused BN-backward statistics arguments");
   }
+  if (d.contains("nol") && !d["nol"].is_none()) {  // normalise-on-load of the input (forward)
+    py::dict n = d["nol"].cast<py::dict>();
+    a.nbn = parse_bn(n["bn"].cast<py::dict>());
+    a.nol = 1;
+    a.nol_kind = (int)I(n, "kind");
+    if (mode != MODE_FWD || a.src.C1 != 0 || a.nbn.C != a.Cs || (a.nol_kind != ACT_NONE && a.nol_kind != ACT_RELU) ||
+        (a.nbn.training && !a.nbn.stats))
+      throw std::runtime_error("conv: bad normalise-on-load arguments");
+  }
   check(launch_conv(mode, a, G, cfg, S(stream)), "conv");
 }
 
@@ -156,6 +165,14 @@ WgradArgs parse_wgrad(const py::dict& d) {
   a.KH = (int)I(d, "KH"); a.KW = (int)I(d, "KW"); a.sh = (int)I(d, "sh"); a.sw = (int)I(d, "sw");
   a.ph = (int)I(d, "ph"); a.pw = (int)I(d, "pw"); a.Kpad = (int)I(d, "Kpad");
   if (a.Cs % 8 || a.Co % 8 || a.Kpad % 64) throw std::runtime_error("wgrad: bad geometry");
+  if (d.contains("nol") && !d["nol"].is_none()) {
+    py::dict n = d["nol"].cast<py::dict>();
+    a.nol_consts = P<const float>(n, "consts");
+    a.nol = 1;
+    a.nol_kind = (int)I(n, "kind");
+    if (!a.nol_consts || a.src.C1 != 0 || (a.nol_kind != ACT_NONE && a.nol_kind != ACT_RELU))
+      throw std::runtime_error("wgrad: bad normalise-on-load arguments");
+  }
   return a;
 }
 

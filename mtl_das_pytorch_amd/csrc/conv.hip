@@ -38,11 +38,38 @@ DEV int encode_kg(int i, int Ktot, int Cs8, int KW, int C0) {
   return c | (kw << 14) | (kh << 21) | (seg << 28) | (1 << 29);
 }
 
+template <int MODE>
+constexpr bool is_fwd() { return MODE == MODE_FWD || MODE == MODE_FWD_NOL; }
+
+// Normalise-on-load: the 8 channels [c, c+8) of an im2col fragment are pre-BN conv outputs y; the operand
+// is act(y * scale + shift) (act = ReLU or identity), rounded to bf16 exactly as the BN tail that used to
+// materialise it.  Fragments of zero padding (bit f of okm clear) stay zero.
+template <int FM>
+DEV void nol_apply(bf16x8* bfr, uint32_t okm, int c, const float* s_nol, int Cs, bool relu) {
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = s_nol[c + j]; sh[j] = s_nol[Cs + c + j]; }
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    if (!((okm >> f) & 1)) continue;
+    bf16x8 v = bfr[f];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = __uint_as_float(((uint32_t)(uint16_t)v[j]) << 16) * sc[j] + sh[j];
+      if (relu) x = fmaxf(x, 0.f);
+      v[j] = (short)f2bf(x);
+    }
+    bfr[f] = v;
+  }
+}
+
 // One wave's fragment loads for k-step `ks`: FM im2col fragments (B operand) + FN weight fragments (A).
+// okm / cch: which im2col fragments hold real (not padding) data and their first channel (for NOL).
 template <int MODE, int FN, int FM>
 DEV void conv_load_stage(const ConvArgs& a, const int* s_tab, int ks, int kgl, int l16, int n_base,
                          const int* pb, const int* py, const int* px, const bool* pv, const bf16_t* base0,
-                         const bf16_t* base1, int ld0, int ld1, const bf16_t* wz, bf16x8* afr, bf16x8* bfr) {
+                         const bf16_t* base1, int ld0, int ld1, const bf16_t* wz, bf16x8* afr, bf16x8* bfr,
+                         uint32_t& okm, int& cch) {
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   const int e = s_tab[ks * 4 + kgl];
   const bool valid = (e >> 29) & 1;
@@ -50,11 +77,13 @@ DEV void conv_load_stage(const ConvArgs& a, const int* s_tab, int ks, int kgl, i
   const int kh = (e >> 21) & 127, kw = (e >> 14) & 127, c = e & 16383;
   const bf16_t* sb = seg ? base1 : base0;
   const int sld = seg ? ld1 : ld0;
+  okm = 0;
+  cch = c;
 #pragma unroll
   for (int f = 0; f < FM; ++f) {
     int ih, iw;
     bool ok;
-    if (MODE == MODE_FWD) {
+    if (is_fwd<MODE>()) {
       ih = py[f] + kh; iw = px[f] + kw;
       ok = valid && pv[f] && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
     } else {
@@ -65,6 +94,7 @@ DEV void conv_load_stage(const ConvArgs& a, const int* s_tab, int ks, int kgl, i
       ok = ok && ih < a.Hs && iw < a.Ws;
     }
     bfr[f] = ok ? *reinterpret_cast<const bf16x8*>(sb + ((int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw) * sld + c) : zero8;
+    okm |= (uint32_t)ok << f;
   }
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
@@ -89,6 +119,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const int nkg = a.Kpad >> 3;
   float* s_red = reinterpret_cast<float*>(s_dyn + ((nkg + 3) & ~3));  // KSPLIT partials, then stats
   float* s_bn = s_red + (RED > ST2 ? RED : ST2);  // [4][BN_T] fused BN-backward: scale, shift, mean, invstd
+  float* s_nol = s_bn;                             // [2][Cs] normalise-on-load scale, shift (forward only)
   const int z = blockIdx.z;
   const int Ktot = a.KH * a.KW * a.Cs;
   for (int i = threadIdx.x; i < nkg; i += 256) s_tab[i] = encode_kg(i, Ktot, a.Cs >> 3, a.KW, a.src.C0);
@@ -103,6 +134,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       s_bn[i] = sc; s_bn[BN_T + i] = sh; s_bn[2 * BN_T + i] = mu; s_bn[3 * BN_T + i] = inv;
     }
   }
+  // MODE_FWD_NOL: the input is the previous conv's pre-BN y; its BN constants for all Cs channels go to
+  // LDS, and block (0, 0) of each group performs that BN's running-statistics update and publishes its
+  // batch constants for the backward (the work of the forward tail this mode replaces)
+  constexpr bool NOL = MODE == MODE_FWD_NOL;
+  if (NOL) bn_prepare(a.nbn, z, s_nol, s_nol + a.Cs, nullptr, nullptr, blockIdx.x == 0 && blockIdx.y == 0);
+  const bool nol_relu = a.nol_kind == ACT_RELU;
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -123,7 +160,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     int b = mm / HWo, r = mm - b * HWo;
     int oh = r / a.Wo, ow = r - oh * a.Wo;
     pb[f] = b;
-    if (MODE == MODE_FWD) { py[f] = oh * a.sh - a.ph; px[f] = ow * a.sw - a.pw; }
+    if (is_fwd<MODE>()) { py[f] = oh * a.sh - a.ph; px[f] = ow * a.sw - a.pw; }
     else { py[f] = oh + a.ph; px[f] = ow + a.pw; }
   }
   const bf16_t* base0 = a.src.p[0] + a.src.gs[0] * z;
@@ -158,18 +195,22 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   };
   if (PREFETCH_Y) load_y();
   bf16x8 a0[FN], b0[FM], a1[FN], b1[FM];
-#define LOAD_STAGE(KS, AF, BF) \
-  conv_load_stage<MODE, FN, FM>(a, s_tab, KS, kgl, l16, n_base, pb, py, px, pv, base0, base1, ld0, ld1, wz, AF, BF)
-#define MMA_STAGE(AF, BF)                                                                                 \
+  uint32_t ok0 = 0, ok1 = 0;
+  int c0 = 0, c1 = 0;
+#define LOAD_STAGE(KS, AF, BF, OK, CC) \
+  conv_load_stage<MODE, FN, FM>(a, s_tab, KS, kgl, l16, n_base, pb, py, px, pv, base0, base1, ld0, ld1, wz, AF, BF, OK, CC)
+  // NOL: the operand transform runs when the stage is consumed, so the loads stay in flight meanwhile
+#define MMA_STAGE(AF, BF, OK, CC)                                                                         \
+  if (NOL) nol_apply<FM>(BF, OK, CC, s_nol, a.Cs, nol_relu);                                              \
   _Pragma("unroll") for (int i = 0; i < FN; ++i)                                                          \
   _Pragma("unroll") for (int f = 0; f < FM; ++f)                                                          \
     acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AF[i], BF[f], acc[i][f], 0, 0, 0);
-  if (kbeg < kend) LOAD_STAGE(kbeg, a0, b0);
+  if (kbeg < kend) LOAD_STAGE(kbeg, a0, b0, ok0, c0);
   for (int ks = kbeg; ks < kend; ks += 2) {
-    if (ks + 1 < kend) LOAD_STAGE(ks + 1, a1, b1);
-    MMA_STAGE(a0, b0)
-    if (ks + 2 < kend) LOAD_STAGE(ks + 2, a0, b0);
-    if (ks + 1 < kend) { MMA_STAGE(a1, b1) }
+    if (ks + 1 < kend) LOAD_STAGE(ks + 1, a1, b1, ok1, c1);
+    MMA_STAGE(a0, b0, ok0, c0)
+    if (ks + 2 < kend) LOAD_STAGE(ks + 2, a0, b0, ok0, c0);
+    if (ks + 1 < kend) { MMA_STAGE(a1, b1, ok1, c1) }
   }
 #undef LOAD_STAGE
 #undef MMA_STAGE
@@ -205,7 +246,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // BN partial sums are reduced across the block's pixel-waves in LDS and published with ONE atomic per
   // (channel, statistic) per block into replica blockIdx.x % NREP.
   float* s_st = s_red;  // [WAVES_M][BN_T][2]
-  const bool want_stats = MODE == MODE_FWD && a.stats != nullptr;
+  const bool want_stats = is_fwd<MODE>() && a.stats != nullptr;
   const bool want_red = want_stats || want_bnb;
   if (want_bnb && !PREFETCH_Y) load_y();
   if (wk == 0) {
@@ -214,7 +255,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       const int n0 = n_base + i * 16 + 4 * kgl;
       const bool nok = n0 < a.N;
       float bias[4] = {0.f, 0.f, 0.f, 0.f};
-      if (MODE == MODE_FWD && a.bias && nok) {
+      if (is_fwd<MODE>() && a.bias && nok) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) bias[r] = a.bias[a.bgs * z + n0 + r];
       }
@@ -226,7 +267,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] + bias[r];
         if (nok && pv[f]) {
-          if (MODE == MODE_FWD) {
+          if (is_fwd<MODE>()) {
             bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
             uint2 w;
             w.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
@@ -321,6 +362,7 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
   __shared__ __attribute__((aligned(16))) bf16_t s_dy[MCH * LDY];
   __shared__ __attribute__((aligned(16))) bf16_t s_x[MCH * LDX];
   __shared__ int s_tab[TK / 8];
+  __shared__ float s_nsc[TK], s_nsh[TK];  // normalise-on-load constants of this tile's input channels
   constexpr int FN = TN / 16, FK = TK / 16, NFR = FN * FK;
   constexpr int FPW = (NFR + 3) / 4;  // fragments per wave
   constexpr int VY = MCH * (TN / 8), VX = MCH * (TK / 8);
@@ -331,6 +373,15 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
   const int n0 = tn * TN, k0 = tk * TK;
   const int Ktot = a.KH * a.KW * a.Cs;
   if (threadIdx.x < TK / 8) s_tab[threadIdx.x] = encode_kg(k0 / 8 + threadIdx.x, Ktot, a.Cs >> 3, a.KW, a.src.C0);
+  if (a.nol) {  // the forward conv read act(BN(y)) on load: rebuild the operand the same way
+    for (int t = threadIdx.x; t < TK; t += 256) {
+      const int e = encode_kg(k0 / 8 + t / 8, Ktot, a.Cs >> 3, a.KW, a.src.C0);
+      const int c = (e & 16383) + (t & 7);
+      const float* kz = a.nol_consts + (int64_t)z * 4 * a.Cs;
+      s_nsc[t] = ((e >> 29) & 1) ? kz[c] : 0.f;
+      s_nsh[t] = ((e >> 29) & 1) ? kz[a.Cs + c] : 0.f;
+    }
+  }
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int HWo = a.Ho * a.Wo;
@@ -347,7 +398,9 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
   __syncthreads();
 
   uint4 ry[NY], rx[NX];
+  uint32_t rok = 0;  // which rx hold real input (not zero padding)
   auto load_chunk = [&](int mc) {
+    rok = 0;
 #pragma unroll
     for (int i = 0; i < NY; ++i) {
       const int v = threadIdx.x + 256 * i;
@@ -375,6 +428,7 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
             const int seg = (e >> 28) & 1;
             const bf16_t* sb = seg ? base1 : base0;
             rx[i] = *reinterpret_cast<const uint4*>(sb + ((int64_t)(b * a.Hi + ih) * a.Wi + iw) * a.src.ld[seg] + (e & 16383));
+            rok |= 1u << i;
           }
         }
       }
@@ -394,7 +448,19 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
       const int v = threadIdx.x + 256 * i;
       if (v < VX) {
         const int p = v / (TK / 8), g = v - p * (TK / 8);
-        *reinterpret_cast<uint4*>(&s_x[p * LDX + g * 8]) = rx[i];
+        uint4 u = rx[i];
+        if (a.nol && ((rok >> i) & 1)) {
+          uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            float lo = __uint_as_float(w4[h] << 16) * s_nsc[g * 8 + 2 * h] + s_nsh[g * 8 + 2 * h];
+            float hi = __uint_as_float(w4[h] & 0xffff0000u) * s_nsc[g * 8 + 2 * h + 1] + s_nsh[g * 8 + 2 * h + 1];
+            if (a.nol_kind == ACT_RELU) { lo = fmaxf(lo, 0.f); hi = fmaxf(hi, 0.f); }
+            w4[h] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+          }
+          u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+        *reinterpret_cast<uint4*>(&s_x[p * LDX + g * 8]) = u;
       }
     }
   };
@@ -522,7 +588,8 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
     constexpr int TILE = (WN / 16) * (WM / 16) * 4 * 64;                                                \
     size_t red = (size_t)(KS - 1) * WAN * WAM * TILE;                                                   \
     size_t st2 = (size_t)WAM * WN * WAN * 2;                                                            \
-    size_t lds = (size_t)nkg4 * 4 + (red > st2 ? red : st2) * 4 + (a.bpart ? 4 * WN * WAN * 4 : 0);     \
+    size_t lds = (size_t)nkg4 * 4 + (red > st2 ? red : st2) * 4 +                                        \
+                 std::max<size_t>(a.bpart ? 4 * WN * WAN * 4 : 0, a.nol ? 2 * a.Cs * 4 : 0);              \
     dim3 grid((M + WM * WAM - 1) / (WM * WAM), (a.N + WN * WAN - 1) / (WN * WAN), G);                    \
     hipLaunchKernelGGL((conv_igemm_kernel<MODE, WN, WM, WAN, WAM, KS>), grid, dim3(256), lds, st, a);   \
     break;                                                                                              \
@@ -549,7 +616,7 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
 }
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
-  if (mode == MODE_FWD) return launch_conv_cfg<MODE_FWD>(a, G, cfg, st);
+  if (mode == MODE_FWD) return a.nol ? launch_conv_cfg<MODE_FWD_NOL>(a, G, cfg, st) : launch_conv_cfg<MODE_FWD>(a, G, cfg, st);
   return a.bpart ? launch_conv_cfg<MODE_DGRAD_BNS>(a, G, cfg, st) : launch_conv_cfg<MODE_DGRAD>(a, G, cfg, st);
 }
 

@@ -6,7 +6,8 @@
 
 namespace mda {
 
-enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD_BNS = 2 };  // 2: dgrad + fused BN-backward statistics
+// 2: dgrad + fused BN-backward statistics; 3: forward with normalise-on-load of its input
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD_BNS = 2, MODE_FWD_NOL = 3 };
 
 struct ConvArgs {
   Src2 src;
@@ -31,6 +32,12 @@ struct ConvArgs {
   BNArgs bbn;
   double* bpart;
   int bkind;
+  // FWD only, optional (nol = 0 off): normalise-on-load.  The (single-segment) input is the previous
+  // conv's pre-BN output y and the im2col operand is act(BN(y)) computed on load (act = nol_kind: ACT_NONE
+  // or ACT_RELU), so the forward BN tail that materialised act(BN(y)) is not launched.  Block (0, 0) of each
+  // group updates that BN's running statistics and publishes its constants (BNArgs::consts).
+  BNArgs nbn;
+  int nol, nol_kind;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -47,6 +54,10 @@ struct WgradArgs {
   int Co, Npad, Cs;
   int KH, KW, sh, sw, ph, pw;
   int Kpad;
+  // optional (nol = 0 off): the forward conv normalised its input on load (ConvArgs::nol); the x operand is
+  // rebuilt the same way from the BN constants the forward published ([G][4][Cs]: scale, shift, ...)
+  const float* nol_consts;
+  int nol, nol_kind;
 };
 
 // One conv of a horizontally batched weight-gradient launch (device table, built by wgrad_table).

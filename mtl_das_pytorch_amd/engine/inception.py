@@ -64,14 +64,24 @@ class CBR:
         self.y = new_act(A, 1, B, c.Ho, c.Wo, c.Co)
         self.dy = new_act(A, 1, B, c.Ho, c.Wo, c.Co)
         self.dx = new_act(A, 1, B, s.H, s.W, s.C, torch.float32) if src.needs_grad else None
+        self.nol_from: Optional["CBR"] = None  # producer whose BN+ReLU this conv applies on load
+        self.skip_tail = False                 # the (single) consumer normalises self.y on load
+
+    def _src(self):
+        if self.nol_from is not None:
+            return src_dict(self.nol_from.y), (self.nol_from.bn, ACT_RELU)
+        return src_dict(self.src.act), None
 
     def forward(self, prog, ph: Phase, training: bool):
-        prog._conv_fwd(ph, self.conv, src_dict(self.src.act), self.y, self.bn, training)
-        prog._tail(ph, ACT_RELU, 1, self.y, self.bn, self.out.act, training)
+        src, nol = self._src()
+        prog._conv_fwd(ph, self.conv, src, self.y, self.bn, training, nol=nol)
+        if not self.skip_tail:
+            prog._tail(ph, ACT_RELU, 1, self.y, self.bn, self.out.act, training)
 
     def backward(self, prog, ph: Phase):
         prog._tail_bwd(ph, ACT_RELU, 1, self.y, self.bn, grads_of(self.out.grad_sources()), self.dy)
-        prog._conv_bwd(ph, self.conv, src_dict(self.src.act), self.dy, self.dx)
+        src, nol = self._src()
+        prog._conv_bwd(ph, self.conv, src, self.dy, self.dx, nol=nol)
         if self.dx is not None:
             self.src.grads.append(self.dx)
 
@@ -261,6 +271,27 @@ class InceptionProgram(LoweredProgram):
         self.confusion = torch.zeros((2, 16, 16), device=self.device, dtype=torch.int32)
         self.nvalid = torch.full((1,), B, device=self.device, dtype=torch.int64)
         self.convs: List[ConvLayer] = [op.conv for op in self.ops if isinstance(op, CBR)]
+        self._plan_nol()
+
+    def _plan_nol(self):
+        """Normalise-on-load: a BasicConv2d output consumed by exactly one other BasicConv2d (and not a
+        slice of a block's concat buffer) is never materialised -- the consumer reads the producer's
+        pre-BN y and applies BN + ReLU to its operand (engine/lowering.py nol_enabled)."""
+        self.n_nol = 0
+        if not self.nol_enabled():
+            return
+        consumers = {}
+        for op in self.ops:
+            consumers[id(op.src)] = consumers.get(id(op.src), 0) + 1
+        consumers[id(self.feat)] = consumers.get(id(self.feat), 0) + 1
+        producer = {id(op.out): op for op in self.ops if isinstance(op, CBR)}
+        for op in self.ops:
+            p = producer.get(id(op.src))
+            if (isinstance(op, CBR) and p is not None and op.src.parent is None
+                    and consumers[id(op.src)] == 1 and op.conv.Cs == p.conv.Co):
+                op.nol_from = p
+                p.skip_tail = True
+                self.n_nol += 1
 
     # -------------------------------------------------------------------------------------------
     def _head_args(self, training: bool) -> dict:

@@ -63,14 +63,26 @@ class LoweredProgram:
             raise ValueError("BN backward chunking assumes the BN count equals the tail's pixel count")
         ph.add(f"tailbwd{kind}", k_tail_bwd, kind, G, bn.nchunk, d)
 
-    def _conv_fwd(self, ph: Phase, c: ConvLayer, src: dict, out: Act, bn: BNLayer, training: bool):
+    @staticmethod
+    def nol_enabled() -> bool:
+        """Normalise-on-load (MDA_NOL, default on): a conv whose input is the single-consumer output of a
+        BN + ReLU tail reads the pre-BN y and applies the BN affine + ReLU to its im2col operand (and so
+        does its weight gradient), so that tail is never launched (csrc/conv.hip MODE_FWD_NOL)."""
+        import os
+        return os.environ.get("MDA_NOL", "1") == "1"
+
+    def _conv_fwd(self, ph: Phase, c: ConvLayer, src: dict, out: Act, bn: BNLayer, training: bool, nol=None):
         mode, cfg, G, d = c.fwd_args(src, out, bn, training)
+        if nol is not None:  # (BNLayer of the input, activation kind)
+            d["nol"] = {"bn": nol[0].args(training), "kind": nol[1]}
         ph.add("conv_fwd", k_conv, mode, cfg, G, d, owner=c)
 
-    def _conv_bwd(self, ph: Phase, c: ConvLayer, src: dict, dy: Act, dx: Optional[Act]):
+    def _conv_bwd(self, ph: Phase, c: ConvLayer, src: dict, dy: Act, dx: Optional[Act], nol=None):
         # per-conv weight gradient on the producer's stream (production programs replace these by the
         # batched launches at the end of the backward pass: batch_wgrads)
         cfg, G, d = c.wgrad_args(src, dy)
+        if nol is not None:  # the forward normalised its input on load: rebuild the operand the same way
+            d["nol"] = {"consts": P(nol[0].consts), "kind": nol[1]}
         ph.add("conv_wgrad", k_wgrad, cfg, G, d, owner=c)
         self._last_wgrad = len(ph.launches) - 1
         if dx is not None:

@@ -163,6 +163,7 @@ class MTLProgram(LoweredProgram):
                                       [L[k] for L in self.levels for k in ("c0", "c3", "co") if k in L]
 
     def _emit(self):
+        self.nol = self.nol_enabled()
         self.fwd_train = self._emit_forward(True)
         self.fwd_eval = self._emit_forward(False)
         self.bwd = self._emit_backward()
@@ -178,8 +179,11 @@ class MTLProgram(LoweredProgram):
         for ri, L in enumerate(self.rbs):
             s = src_dict(L["in"])
             self._conv_fwd(ph, L["ca"], s, L["ya"], L["bna"], training)
-            self._tail(ph, ACT_RELU, 1, L["ya"], L["bna"], L["ha"], training)
-            self._conv_fwd(ph, L["cb"], src_dict(L["ha"]), L["yb"], L["bnb"], training)
+            if self.nol:  # conv b normalises ya on load: no BN+ReLU tail, ha never materialised
+                self._conv_fwd(ph, L["cb"], src_dict(L["ya"]), L["yb"], L["bnb"], training, nol=(L["bna"], ACT_RELU))
+            else:
+                self._tail(ph, ACT_RELU, 1, L["ya"], L["bna"], L["ha"], training)
+                self._conv_fwd(ph, L["cb"], src_dict(L["ha"]), L["yb"], L["bnb"], training)
             if L["proj"]:
                 self._conv_fwd(ph, L["cs"], s, L["ys"], L["bns"], training)
                 self._tail(ph, ADD_RELU, 1, L["yb"], L["bnb"], L["out"], training, r=L["ys"], bn2=L["bns"])
@@ -192,8 +196,11 @@ class MTLProgram(LoweredProgram):
             ph.pending_waits.append(f"F{2 * lvl + 2}")
             s = src_dict(L["Fa"], L["prevB"]) if L["prevB"] is not None else src_dict(L["Fa"])
             self._conv_fwd(ph, L["c0"], s, L["ym1"], L["bn0"], training)
-            self._tail(ph, ACT_RELU, T, L["ym1"], L["bn0"], L["hm"], training)
-            self._conv_fwd(ph, L["c3"], src_dict(L["hm"]), L["ym2"], L["bn3"], training)
+            if self.nol:
+                self._conv_fwd(ph, L["c3"], src_dict(L["ym1"]), L["ym2"], L["bn3"], training, nol=(L["bn0"], ACT_RELU))
+            else:
+                self._tail(ph, ACT_RELU, T, L["ym1"], L["bn0"], L["hm"], training)
+                self._conv_fwd(ph, L["c3"], src_dict(L["hm"]), L["ym2"], L["bn3"], training)
             self._tail(ph, SIGMUL, T, L["ym2"], L["bn3"], L["Aout"], training, r=L["Fb"])
             if "co" in L:
                 self._conv_fwd(ph, L["co"], src_dict(L["Aout"]), L["yo"], L["bno"], training)
@@ -227,7 +234,10 @@ class MTLProgram(LoweredProgram):
                 self._conv_bwd(ph, L["co"], src_dict(L["Aout"]), L["dyo"], L["dA"])
             self._tail_bwd(ph, SIGMUL, T, L["ym2"], L["bn3"], [(L["dA"].p, L["dA"].gs, L["dA"].ld)], L["dym2"],
                            r=L["Fb"], side=L["dF"])
-            self._conv_bwd(ph, L["c3"], src_dict(L["hm"]), L["dym2"], L["dhm"])
+            if self.nol:
+                self._conv_bwd(ph, L["c3"], src_dict(L["ym1"]), L["dym2"], L["dhm"], nol=(L["bn0"], ACT_RELU))
+            else:
+                self._conv_bwd(ph, L["c3"], src_dict(L["hm"]), L["dym2"], L["dhm"])
             self._tail_bwd(ph, ACT_RELU, T, L["ym1"], L["bn0"], [(L["dhm"].p, L["dhm"].gs, L["dhm"].ld)], L["dym1"])
             s = src_dict(L["Fa"], L["prevB"]) if L["prevB"] is not None else src_dict(L["Fa"])
             self._conv_bwd(ph, L["c0"], s, L["dym1"], L["dcat"])
@@ -260,7 +270,10 @@ class MTLProgram(LoweredProgram):
                 self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["ys"], bn2=R["bns"], dy2=R["dys"])
             else:
                 self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["in"], side=R["side"])
-            self._conv_bwd(ph, R["cb"], src_dict(R["ha"]), R["dyb"], R["dha"])
+            if self.nol:
+                self._conv_bwd(ph, R["cb"], src_dict(R["ya"]), R["dyb"], R["dha"], nol=(R["bna"], ACT_RELU))
+            else:
+                self._conv_bwd(ph, R["cb"], src_dict(R["ha"]), R["dyb"], R["dha"])
             self._tail_bwd(ph, ACT_RELU, 1, R["ya"], R["bna"], [(R["dha"].p, 0, R["dha"].ld)], R["dya"])
             self._conv_bwd(ph, R["ca"], src_dict(R["in"]), R["dya"], R["dxa"])
             if R["proj"]:

@@ -91,7 +91,7 @@ class WgradCall:
         return self.post(self.slab)
 
 
-def prepare_conv2d(x, w, bias=None, stride=1, padding=0, stats=None, x2=None, cfg=None) -> ConvCall:
+def prepare_conv2d(x, w, bias=None, stride=1, padding=0, stats=None, x2=None, cfg=None, nol=None) -> ConvCall:
     if stats is not None and stats.dtype != torch.float64:
         raise TypeError("BN statistic replicas are fp64 ([NREP, 2, Co])")
     _check(x, torch.bfloat16)
@@ -109,15 +109,19 @@ def prepare_conv2d(x, w, bias=None, stride=1, padding=0, stats=None, x2=None, cf
     d = {"src": src, "w": ptr(wf), "bias": ptr(bias) if bias is not None else 0, "out": ptr(y), "ldo": Co,
          "stats": ptr(stats) if stats is not None else 0, "B": B, "Hs": H, "Ws": W, "Ho": Ho, "Wo": Wo, "N": Co,
          "Npad": wf.shape[0], "Cs": Cs, "KH": KH, "KW": KW, "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": wf.shape[1]}
+    if nol is not None:  # (bn dict of x's BN, kind): x is a pre-BN y, the operand is act(BN(x)) on load
+        d["nol"] = {"bn": nol[0], "kind": nol[1]}
     return ConvCall(0, _fwd_cfg(Co, B * Ho * Wo) if cfg is None else cfg, d, y, (x, x2, wf, bias, stats))
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0,
-           stats: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
+           stats: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None, cfg: Optional[int] = None,
+           nol=None):
     """NHWC bf16 convolution.  ``x2`` (optional) is a second input whose channels are concatenated after
     ``x``'s (the kernel reads both without materialising the concat).  ``stats`` ([NREP, 2, Co] fp64,
-    zero-initialised by the caller) receives per-channel sums of the output and its square."""
-    return prepare_conv2d(x, w, bias, stride, padding, stats, x2, cfg).run()
+    zero-initialised by the caller) receives per-channel sums of the output and its square.  ``nol``
+    ((bn dict, kind)): normalise-on-load -- ``x`` is a pre-BN tensor and the conv input is act(BN(x))."""
+    return prepare_conv2d(x, w, bias, stride, padding, stats, x2, cfg, nol).run()
 
 
 def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg=None, bn_stats=None) -> ConvCall:
@@ -163,7 +167,7 @@ def wgrad_cfg(Co: int, Kpad: int) -> int:
     return 0 if Co <= 16 else ((1 if Kpad <= 64 else 2) if Co <= 32 else 3)
 
 
-def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=None, cfg=None) -> WgradCall:
+def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=None, cfg=None, nol=None) -> WgradCall:
     _check(x, torch.bfloat16)
     _check(dy, torch.bfloat16)
     Co, Ci, KH, KW = w_shape
@@ -194,16 +198,20 @@ def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=No
          "B": B, "Hi": H, "Wi": W, "Ho": Ho, "Wo": Wo, "Co": Co, "Npad": Npad, "Cs": Cs, "KH": KH, "KW": KW,
          "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": Kpad}
 
+    if nol is not None:  # (consts [1, 4, Cs] fp32: scale, shift, mean, invstd; kind)
+        d["nol"] = {"consts": ptr(nol[0]), "kind": nol[1]}
+
     def post(sl):
         dWp = sl.sum(dim=1)[0, :Co, :KH * KW * Cs].view(Co, KH, KW, Cs)[..., :Ci]
         return dWp.permute(0, 3, 1, 2).contiguous()
-    return WgradCall(cfg, d, slab, post, (x, x2, dy))
+    return WgradCall(cfg, d, slab, post, (x, x2, dy, nol))
 
 
 def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, w_shape, stride=1, padding=0, x2: Optional[torch.Tensor] = None,
-                 splits: Optional[int] = None, cfg: Optional[int] = None):
-    """Weight gradient in the reference layout ``[Co, Ci, KH, KW]`` (fp32)."""
-    return prepare_conv2d_wgrad(x, dy, w_shape, stride, padding, x2, splits, cfg).run()
+                 splits: Optional[int] = None, cfg: Optional[int] = None, nol=None):
+    """Weight gradient in the reference layout ``[Co, Ci, KH, KW]`` (fp32).  ``nol`` ((consts, kind)): ``x``
+    is pre-BN and the operand is act(x * consts[0,0] + consts[0,1]), as in a normalise-on-load forward."""
+    return prepare_conv2d_wgrad(x, dy, w_shape, stride, padding, x2, splits, cfg, nol).run()
 
 
 # ---------------------------------------------------------------------------------------------------

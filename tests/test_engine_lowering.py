@@ -15,7 +15,8 @@ def test_mtl_program_structure():
         assert torch.equal(v, sd_before[k]), k
     assert p.flat.numel >= sum(x.numel() for x in m.parameters())
     n = p.num_launches()
-    assert n["forward_train"] == 60 and n["backward"] == 90
+    # forward: 12 BN+ReLU tails are folded into their consumer conv (normalise-on-load)
+    assert n["forward_train"] == 48 and n["backward"] == 90
     # both task branches of a level are ONE grouped launch with an even parameter stride
     L = p.levels[1]
     assert L["c0"].G == 2 and L["c0"].wstride > 0
@@ -57,7 +58,7 @@ def test_inception_program_structure():
     assert len(pools) == 13
     assert (p.feat.act.H, p.feat.act.W, p.feat.act.C) == (1, 6, 2048)
     kernels = lambda ph: sum(1 for l in ph.launches if l.fn is not None)  # not the fork points
-    assert kernels(p.fwd_train) == 94 * 2 + 13 + 1
+    assert kernels(p.fwd_train) == 94 * 2 + 13 + 1 - p.n_nol  # tails folded into their consumer conv
     assert kernels(p.bwd) == 94 * 2 + 93 + 13 + 1   # the stem conv has no data gradient
     # Mixed_5b's 1x1 branch writes channels [0, 64) of the 256-wide block buffer in place
     blk = [o for o in cbr if o.conv.mods[0] is m.Mixed_5b.branch1x1.conv][0]

@@ -159,7 +159,14 @@ def test_inception_backward_layer_local():
     worst = {}
     for op in prog.ops:
         g = sum(_nchw(a) for a in op.out.grad_sources())
-        x = _nchw(op.src.act).contiguous()  # (torch's channels-last max-pool breaks ties differently)
+        if getattr(op, "nol_from", None) is not None:
+            # normalise-on-load: the input is never materialised; rebuild relu(BN(y)) of the producer from
+            # its stored y and the BN constants its consumer published, rounded to bf16 as the operand
+            pk = op.nol_from.bn.consts[0]
+            x = torch.relu(_nchw(op.nol_from.y) * pk[0].view(1, -1, 1, 1) + pk[1].view(1, -1, 1, 1))
+            x = x.bfloat16().float().contiguous()
+        else:
+            x = _nchw(op.src.act).contiguous()  # (torch's channels-last max-pool breaks ties differently)
         if isinstance(op, CBR):
             conv, bn = op.conv.mods[0], op.bn.mods[0]
             x = x[:, :conv.in_channels].clone().requires_grad_(op.dx is not None)

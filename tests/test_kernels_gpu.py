@@ -109,6 +109,35 @@ def test_conv_wgrad_whole_k_tiles(fn, case, cfg):
     assert rel(dw, w.grad) < 5e-3
 
 
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("case", [(4, 17, 42, 32, 32, 3, 1, 1), (2, 33, 83, 16, 16, 3, 1, 1), (4, 9, 21, 64, 128, 3, 2, 1),
+                                  (4, 5, 11, 64, 128, 3, 1, 1)])
+def test_conv_normalise_on_load(fn, kind, case):
+    """Forward conv reading a pre-BN y and applying act(BN(y)) to its operand (training statistics from the
+    replicas; running statistics updated and batch constants published by block 0), and the matching
+    weight gradient that rebuilds the operand from the published constants."""
+    B, H, W, C, Co, k, s, p = case
+    g = torch.Generator().manual_seed(40 + kind)
+    y = (torch.randn(B, C, H, W, generator=g) * 2 + 0.3).bfloat16().float().cuda()
+    bn, gamma, beta, rm, rv, nbt = _bn_setup(fn, y, C, seed=kind)
+    consts = torch.zeros(1, 4, C, device="cuda")
+    bn["consts"] = consts.data_ptr()
+    w = (torch.randn(Co, C, k, k, generator=g) / math.sqrt(C * k * k)).bfloat16().float().cuda()
+    z = _torch_bn(y, gamma, beta)
+    act = (z if kind == 0 else F.relu(z)).bfloat16().float()  # the engine's operand is bf16
+    ref = F.conv2d(act, w, stride=s, padding=p)
+    out = fn.conv2d(nhwc(y).bfloat16(), w, stride=s, padding=p, nol=(bn, kind))
+    assert rel(nchw(out), ref) < 6e-3
+    assert torch.allclose(rm, 0.1 * y.mean((0, 2, 3)), atol=1e-4, rtol=1e-3) and int(nbt.item()) == 1
+    inv = torch.rsqrt(y.var((0, 2, 3), unbiased=False) + 1e-5)
+    assert torch.allclose(consts[0, 0], gamma * inv, rtol=1e-4, atol=1e-5)
+    dy = torch.randn(ref.shape, generator=g).bfloat16().float().cuda()
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(act, wr, stride=s, padding=p).backward(dy)
+    dw = fn.conv2d_wgrad(nhwc(y).bfloat16(), nhwc(dy).bfloat16(), w.shape, stride=s, padding=p, nol=(consts, kind))
+    assert rel(dw, wr.grad) < 5e-3
+
+
 def test_conv_two_segment_input(fn):
     g = torch.Generator().manual_seed(3)
     a = torch.randn(2, 32, 17, 42, generator=g).bfloat16().float().cuda()
