@@ -193,7 +193,9 @@ class MTLProgram(LoweredProgram):
         # task branches (both tasks per launch) on side stream 1, overlapping the backbone
         ph.cur_stream = 1
         for lvl, L in enumerate(self.levels):
-            ph.pending_waits.append(f"F{2 * lvl + 2}")
+            # the mask generator needs only F_{2l+1} (and the previous level, same stream); F_{2l+2} is
+            # waited for right before the mask multiply, so the generator overlaps the next residual block
+            ph.pending_waits.append(f"F{2 * lvl + 1}")
             s = src_dict(L["Fa"], L["prevB"]) if L["prevB"] is not None else src_dict(L["Fa"])
             self._conv_fwd(ph, L["c0"], s, L["ym1"], L["bn0"], training)
             if self.nol:
@@ -201,6 +203,7 @@ class MTLProgram(LoweredProgram):
             else:
                 self._tail(ph, ACT_RELU, T, L["ym1"], L["bn0"], L["hm"], training)
                 self._conv_fwd(ph, L["c3"], src_dict(L["hm"]), L["ym2"], L["bn3"], training)
+            ph.pending_waits.append(f"F{2 * lvl + 2}")
             self._tail(ph, SIGMUL, T, L["ym2"], L["bn3"], L["Aout"], training, r=L["Fb"])
             if "co" in L:
                 self._conv_fwd(ph, L["co"], src_dict(L["Aout"]), L["yo"], L["bno"], training)
@@ -234,6 +237,7 @@ class MTLProgram(LoweredProgram):
                 self._conv_bwd(ph, L["co"], src_dict(L["Aout"]), L["dyo"], L["dA"])
             self._tail_bwd(ph, SIGMUL, T, L["ym2"], L["bn3"], [(L["dA"].p, L["dA"].gs, L["dA"].ld)], L["dym2"],
                            r=L["Fb"], side=L["dF"])
+            ph.mark(f"dF{li}")  # F_{2l+2}'s gradient from this level is complete here
             if self.nol:
                 self._conv_bwd(ph, L["c3"], src_dict(L["ym1"]), L["dym2"], L["dhm"], nol=(L["bn0"], ACT_RELU))
             else:
@@ -265,7 +269,9 @@ class MTLProgram(LoweredProgram):
         for i in range(7, -1, -1):
             R = self.rbs[i]
             g = sources(i + 1)
-            ph.pending_waits.append(f"lvl{i // 2}")  # F_{i+1}'s task-branch gradients
+            # F_{i+1}'s task-branch gradients: for F_{2l+2} (i odd) the mask-target gradient dF, ready right
+            # after the level's sigmoid-mask backward; for F_{2l+1} the concat gradient of the whole level
+            ph.pending_waits.append(f"dF{i // 2}" if i % 2 == 1 else f"lvl{i // 2}")
             if R["proj"]:
                 self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["ys"], bn2=R["bns"], dy2=R["dys"])
             else:
