@@ -84,6 +84,25 @@ BNArgs parse_bn(const py::dict& d) {
   return b;
 }
 
+// Apply-on-load of a BN-tail backward (ConvArgs::ao / WgradArgs::ao); C = the dy channel count.
+AolArgs parse_aol(const py::dict& o, int C, bool dgrad) {
+  AolArgs r{};
+  r.g = P<const float>(o, "g"); r.ggs = I(o, "ggs"); r.ldg = (int)I(o, "ldg");
+  r.y = P<const bf16_t>(o, "y"); r.ygs = I(o, "ygs"); r.ldy = (int)I(o, "ldy");
+  r.coef = P<float>(o, "coef");
+  r.kind = (int)I(o, "kind");
+  if (dgrad) {
+    r.bn = parse_bn(o["bn"].cast<py::dict>());
+    r.part = P<const double>(o, "part");
+    r.dgamma = P<float>(o, "dgamma"); r.dbeta = P<float>(o, "dbeta"); r.pgs = I(o, "pgs");
+    if (!r.part || !r.bn.gamma || r.bn.C != C || !r.bn.training) throw std::runtime_error("bad apply-on-load BN arguments");
+  }
+  if (!r.g || !r.y || !r.coef || r.ldg % 8 || r.ldy % 8 || r.ggs % 8 || r.ygs % 8 ||
+      (r.kind != ACT_NONE && r.kind != ACT_RELU))
+    throw std::runtime_error("bad apply-on-load arguments");
+  return r;
+}
+
 void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
   ConvArgs a{};
   a.src = parse_src(d["src"].cast<py::dict>());
@@ -119,6 +138,11 @@ void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
         (a.nbn.training && !a.nbn.stats))
       throw std::runtime_error("conv: bad normalise-on-load arguments");
   }
+  if (d.contains("aol") && !d["aol"].is_none()) {  // dgrad: dy operand = BN-tail backward applied on load
+    if (mode != MODE_DGRAD || a.src.C1 != 0) throw std::runtime_error("conv: apply-on-load needs a one-segment dgrad");
+    a.ao = parse_aol(d["aol"].cast<py::dict>(), a.Cs, true);
+    a.aol = 1;
+  }
   check(launch_conv(mode, a, G, cfg, S(stream)), "conv");
 }
 
@@ -130,6 +154,8 @@ void wgrad(int cfg, int G, int64_t stream, py::dict d) {
 
 // Packs the WgradJob table of a batched weight-gradient launch; returns (bytes, total blocks).
 py::tuple wgrad_table(int cfg, py::list dicts, py::list groups) {
+  const bool aol = cfg >= WGRAD_AOL_CFG;  // the AOL instantiation: every job must apply on load
+  if (aol) cfg -= WGRAD_AOL_CFG;
   int TN, TK;
   if (wgrad_tile_shape(cfg, TN, TK)) throw std::runtime_error("wgrad_table: bad cfg");
   std::vector<WgradJob> jobs(dicts.size());
@@ -138,6 +164,7 @@ py::tuple wgrad_table(int cfg, py::list dicts, py::list groups) {
     WgradJob& j = jobs[i];
     j = WgradJob{};
     j.a = parse_wgrad(dicts[i].cast<py::dict>());
+    if ((j.a.aol != 0) != aol) throw std::runtime_error("wgrad_table: apply-on-load jobs need the AOL cfg and vice versa");
     j.G = groups[i].cast<int>();
     j.ntiles = ((j.a.Npad + TN - 1) / TN) * (j.a.Kpad / TK);
     if (j.a.Kpad % TK) throw std::runtime_error("wgrad_table: Kpad not a multiple of the tile");
@@ -172,6 +199,10 @@ WgradArgs parse_wgrad(const py::dict& d) {
     a.nol_kind = (int)I(n, "kind");
     if (!a.nol_consts || a.src.C1 != 0 || (a.nol_kind != ACT_NONE && a.nol_kind != ACT_RELU))
       throw std::runtime_error("wgrad: bad normalise-on-load arguments");
+  }
+  if (d.contains("aol") && !d["aol"].is_none()) {
+    a.ao = parse_aol(d["aol"].cast<py::dict>(), a.Co, false);
+    a.aol = 1;
   }
   return a;
 }

@@ -6,8 +6,23 @@
 
 namespace mda {
 
-// 2: dgrad + fused BN-backward statistics; 3: forward with normalise-on-load of its input
-enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD_BNS = 2, MODE_FWD_NOL = 3 };
+// 2: dgrad + fused BN-backward statistics; 3: forward with normalise-on-load of its input;
+// 5: dgrad with apply-on-load of its dy operand; 6: both 2 and 5
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD_BNS = 2, MODE_FWD_NOL = 3, MODE_DGRAD_AOL = 5, MODE_DGRAD_AOL_BNS = 6 };
+
+// Apply-on-load of a BN-tail backward (ACT_NONE / ACT_RELU): the conv operand dy = A*dz + B*y + C with
+// dz = g * act'(y * scale + shift) is computed from the tail's fp32 upstream gradient g and its pre-BN y
+// when loaded, so the tail's apply pass never runs.
+struct AolArgs {
+  const float* g; int64_t ggs; int ldg;     // upstream fp32 gradient of the tail output
+  const bf16_t* y; int64_t ygs; int ldy;    // the tail's pre-BN input
+  BNArgs bn;                                // its BN (constants from bn.consts)
+  const double* part;                       // [G][NREP][3][C] rows 0/1: sum dz, sum dz*xhat (fused stats)
+  float* coef;                              // [G][5][C] A, B, C, scale, shift: written by the dgrad's block
+                                            // (0, 0), read by the weight gradient
+  float* dgamma; float* dbeta; int64_t pgs; // written by the dgrad's block (0, 0)
+  int kind;
+};
 
 struct ConvArgs {
   Src2 src;
@@ -38,6 +53,9 @@ struct ConvArgs {
   // group updates that BN's running statistics and publishes its constants (BNArgs::consts).
   BNArgs nbn;
   int nol, nol_kind;
+  // DGRAD only, optional (aol = 0 off): the dy operand is applied on load (AolArgs)
+  AolArgs ao;
+  int aol;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -58,6 +76,10 @@ struct WgradArgs {
   // rebuilt the same way from the BN constants the forward published ([G][4][Cs]: scale, shift, ...)
   const float* nol_consts;
   int nol, nol_kind;
+  // optional (aol = 0 off): the dy operand is applied on load from ao.g / ao.y with the coefficient table
+  // ao.coef written by the matching dgrad
+  AolArgs ao;
+  int aol;
 };
 
 // One conv of a horizontally batched weight-gradient launch (device table, built by wgrad_table).
@@ -160,6 +182,7 @@ struct AdamArgs {
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st);
 int wgrad_tile_shape(int cfg, int& TN, int& TK);
+constexpr int WGRAD_AOL_CFG = 100;  // batched-wgrad cfg offset selecting the apply-on-load kernels
 int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st);
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);

@@ -15,6 +15,18 @@ from .program import Launch, Phase, k_adam, k_conv, k_gather, k_tail_bwd, k_tail
 ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
 
 
+WGRAD_AOL_CFG = 100  # batched-wgrad cfg offset of the apply-on-load kernels (csrc/kernels.h)
+
+
+def _refers_to(args, ptr: int) -> bool:
+    """Whether a launch's argument tree names the device address ``ptr``."""
+    if isinstance(args, dict):
+        return any(_refers_to(v, ptr) for v in args.values())
+    if isinstance(args, (list, tuple)):
+        return any(_refers_to(v, ptr) for v in args)
+    return isinstance(args, int) and not isinstance(args, bool) and args == ptr
+
+
 def _blocks(M: int, C: int, cap: int = 1024, per_thread: int = 4) -> int:
     cg = max(1, C // 8)
     pl = max(1, 256 // cg)
@@ -78,16 +90,18 @@ class LoweredProgram:
         ph.add("conv_fwd", k_conv, mode, cfg, G, d, owner=c)
 
     def _conv_bwd(self, ph: Phase, c: ConvLayer, src: dict, dy: Act, dx: Optional[Act], nol=None):
-        # per-conv weight gradient on the producer's stream (production programs replace these by the
-        # batched launches at the end of the backward pass: batch_wgrads)
+        # data gradient first (it is on the critical chain, and under apply-on-load it writes the
+        # coefficient table the weight gradient reads), then the per-conv weight gradient on the same
+        # stream (production programs replace these by the batched launches at the end of the backward
+        # pass: batch_wgrads)
+        if dx is not None:
+            mode, cfg, G, d = c.dgrad_args(dy, dx)
+            ph.add("conv_dgrad", k_conv, mode, cfg, G, d, owner=c)
         cfg, G, d = c.wgrad_args(src, dy)
         if nol is not None:  # the forward normalised its input on load: rebuild the operand the same way
             d["nol"] = {"consts": P(nol[0].consts), "kind": nol[1]}
         ph.add("conv_wgrad", k_wgrad, cfg, G, d, owner=c)
         self._last_wgrad = len(ph.launches) - 1
-        if dx is not None:
-            mode, cfg, G, d = c.dgrad_args(dy, dx)
-            ph.add("conv_dgrad", k_conv, mode, cfg, G, d, owner=c)
 
     def fuse_dgrad_bn_stats(self) -> int:
         """Move the BN-backward reduction of single-source elementwise tails into the producing dgrad.
@@ -124,6 +138,77 @@ class LoweredProgram:
                 d["fused"] = 2
                 self.n_dgrad_bnstats += 1
         return self.n_dgrad_bnstats
+
+    def apply_on_load(self) -> int:
+        """Fold apply-only BN tails (``fused = 2``, after fuse_dgrad_bn_stats) into their consumers.
+
+        Such a tail reads the fp32 gradient g and the pre-BN y and writes the bf16 dy of its conv, whose
+        only readers are that conv's dgrad and wgrad.  Both now rebuild dy from g and y while loading
+        their operand (csrc/conv.hip MODE_DGRAD_AOL, wgrad_block<AOL>): the dgrad derives the per-channel
+        coefficients from the fused statistics, writes d(gamma), d(beta) and the coefficient table, and
+        the wgrad (after it on the same stream) reads that table.  The tail launch and one bf16 write +
+        two reads of dy disappear from the backward chain.  ReLU / identity tails only.
+
+        Opt-in (MDA_AOL=1: every eligible conv, MDA_AOL=pw: 1x1 convs only).  Measured on MI355X it
+        loses: an im2col operand is loaded KH*KW times, so a 3x3 dgrad re-reads fp32 g + bf16 y and
+        redoes the transform 9x per element, and every dgrad block reduces the NREP statistic replicas
+        again (Model A backward 767 -> 900 us, Model C -4.5%; 1x1-only: A -2%, C -2.5%).  Returns the number of folded tails."""
+        import os
+        self.n_aol = 0
+        mode = os.environ.get("MDA_AOL", "0")
+        if mode not in ("1", "pw"):
+            return 0
+        ls = self.bwd.launches
+        removed = set()
+        for i, l in enumerate(ls):
+            if not l.name.startswith("tailbwd"):
+                continue
+            kind, G, nchunk, d = l.args
+            if d.get("fused") != 2 or kind not in (ACT_NONE, ACT_RELU) or d.get("dy2") or len(d["g"]) != 1:
+                continue
+            if l.record is not None and l.waits:
+                continue
+            dy = d["dy"]
+            users = [(j, k) for j, k in enumerate(ls) if j != i and _refers_to(k.args, dy)]
+            dg = [(j, k) for j, k in users if k.name == "conv_dgrad" and k.args[3]["src"]["p0"] == dy]
+            wg = [(j, k) for j, k in users if k.name == "conv_wgrad" and k.args[2]["dy"] == dy]
+            if len(users) != 2 or len(dg) != 1 or len(wg) != 1:
+                continue
+            (jd, ld), (jw, lw) = dg[0], wg[0]
+            _, cfg, DG, dd = ld.args
+            if mode == "pw" and dd["KH"] * dd["KW"] != 1:
+                continue
+            wcfg, WG, wd = lw.args
+            if (not (i < jd < jw) or ld.stream != lw.stream or ld.stream != l.stream or DG != G or WG != G
+                    or dd["src"].get("C1", 0) != 0 or dd["src"]["gs0"] != d["dgs"] or dd["src"]["ld0"] != d["ldd"]
+                    or wd["dgs"] != d["dgs"] or wd["ldd"] != d["ldd"] or dd["Cs"] != d["C"] or wd["Co"] != d["C"]):
+                continue
+            gp, ggs, gld = d["g"][0]
+            ao = {"g": gp, "ggs": ggs, "ldg": gld, "y": d["y"], "ygs": d["ygs"], "ldy": d["ldy"],
+                  "coef": P(self._aol_coef(G, d["C"])), "kind": kind}
+            dd["aol"] = dict(ao, bn=d["bn"], part=d["part"], dgamma=d.get("dgamma", 0), dbeta=d.get("dbeta", 0),
+                             pgs=d.get("pgs", 0))
+            wd["aol"] = ao
+            nxt = next((k for k in ls[i + 1:] if k.stream == l.stream), None)
+            if l.waits:
+                nxt.waits = tuple(nxt.waits) + tuple(l.waits)
+            if l.record is not None:
+                prev = next((k for k in reversed(ls[:i]) if k.stream == l.stream and id(k) not in removed), None)
+                if prev is None:
+                    continue
+                if prev.record is None:
+                    prev.record = l.record
+                else:
+                    self.bwd.alias[l.record] = prev.record
+            removed.add(id(l))
+            self.n_aol += 1
+        self.bwd.launches = [k for k in ls if id(k) not in removed]
+        return self.n_aol
+
+    def _aol_coef(self, G: int, C: int) -> torch.Tensor:
+        t = torch.empty(G * 5 * C, dtype=torch.float32, device=self.device)
+        self.aol_coefs = getattr(self, "aol_coefs", []) + [t]
+        return t
 
     def set_source(self, X: torch.Tensor, labels: torch.Tensor, idx: torch.Tensor):
         """Bind the dataset tensors the gather launch reads (X [N,C,H,W] fp32, labels [N,2], idx [B])."""
@@ -182,13 +267,15 @@ class LoweredProgram:
         inserts, tags = [], []
         for st in sorted({l.stream for l in wg}):
             batched, costs = [], []
-            for cfg in sorted({l.args[0] for l in wg if l.stream == st}):
-                group = [l for l in wg if l.stream == st and l.args[0] == cfg]
-                raw, nblocks = lib().wgrad_table(cfg, [l.args[2] for l in group], [l.args[1] for l in group])
+            # key: tile config, + WGRAD_AOL_CFG for the apply-on-load instantiation
+            key_of = lambda l: l.args[0] + (WGRAD_AOL_CFG if l.args[2].get("aol") else 0)  # noqa: E731
+            for key in sorted({key_of(l) for l in wg if l.stream == st}):
+                group = [l for l in wg if l.stream == st and key_of(l) == key]
+                raw, nblocks = lib().wgrad_table(key, [l.args[2] for l in group], [l.args[1] for l in group])
                 table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
                 self.wgrad_tables.append(table)
-                batched.append(Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, stream=st))
-                TN, TK, MCH = WGRAD_TILES[cfg]
+                batched.append(Launch("wgrad_batched", k_wgrad_batched, key, table, len(group), nblocks, stream=st))
+                TN, TK, MCH = WGRAD_TILES[key % WGRAD_AOL_CFG]
                 costs.append(sum(l.args[2]["splits"] * l.args[2]["m_per_split"] * l.args[1] * TN * TK *
                                  math.ceil(l.args[2]["Npad"] / TN) * (l.args[2]["Kpad"] // TK) for l in group))
             pos = max((i for i, k in enumerate(keep) if k.stream == st), default=len(keep) - 1) + 1

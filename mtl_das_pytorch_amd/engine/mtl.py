@@ -168,6 +168,7 @@ class MTLProgram(LoweredProgram):
         self.fwd_eval = self._emit_forward(False)
         self.bwd = self._emit_backward()
         self.fuse_dgrad_bn_stats()
+        self.apply_on_load()
         self.opt = self._emit_optimizer()
 
     def _emit_forward(self, training: bool) -> Phase:

@@ -110,11 +110,12 @@ def test_wgrad_fanout_structure(monkeypatch):
     _check_event_order(p.bwd)
 
 
-def test_dgrad_fused_bn_stats_wiring():
+def test_dgrad_fused_bn_stats_wiring(monkeypatch):
     """Single-source elementwise BN tails take their backward sums from the producing dgrad's epilogue
     (Model A: 8 residual-block inner BNs + 4 grouped attention-generator BNs)."""
     from mtl_das_pytorch_amd.engine.inception import InceptionProgram
     from mtl_das_pytorch_amd.models import Multi_Classifier
+    monkeypatch.setenv("MDA_AOL", "0")  # keep the apply-only tails in the program
     p = MTLProgram(MTL_Net(), 8, "cpu")
     assert p.n_dgrad_bnstats == 12
     fused = [l for l in p.bwd.launches if l.name.startswith("tailbwd") and l.args[3].get("fused") == 2]
@@ -127,6 +128,36 @@ def test_dgrad_fused_bn_stats_wiring():
         assert p.bwd.launches.index(prod[0]) < p.bwd.launches.index(l)
     c = InceptionProgram(Multi_Classifier(), 4, "cpu")
     assert c.n_dgrad_bnstats >= 40
+
+
+def test_apply_on_load_wiring(monkeypatch):
+    """Apply-only BN tails disappear: their conv's dgrad and wgrad read the tail's g / y (same pointers,
+    strides and groups), the dgrad before the wgrad on one stream, sharing one coefficient table; the
+    dgrad also takes over d(gamma) / d(beta).  Event tags the program uses stay recorded."""
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.models import Multi_Classifier
+    monkeypatch.setenv("MDA_AOL", "1")  # opt-in
+    for p in (MTLProgram(MTL_Net(), 8, "cpu"), InceptionProgram(Multi_Classifier(), 4, "cpu")):
+        ls = p.bwd.launches
+        assert p.n_aol > 0 and p.n_aol <= p.n_dgrad_bnstats
+        dg = [l for l in ls if l.name == "conv_dgrad" and "aol" in l.args[3]]
+        wg = [l for l in ls if l.name == "conv_wgrad" and "aol" in l.args[2]]
+        assert len(dg) == len(wg) == p.n_aol
+        for d in dg:
+            a = d.args[3]["aol"]
+            w = [x for x in wg if x.args[2]["aol"]["coef"] == a["coef"]]
+            assert len(w) == 1 and w[0].stream == d.stream and ls.index(w[0]) > ls.index(d)
+            assert w[0].args[2]["aol"]["g"] == a["g"] and w[0].args[2]["aol"]["y"] == a["y"]
+            assert a["dgamma"] and a["dbeta"] and a["part"]
+        _check_event_order(p.bwd)
+    p = MTLProgram(MTL_Net(), 8, "cpu")
+    assert p.n_aol == 12 and not any(l.name.startswith("tailbwd") and l.args[3].get("fused") == 2
+                                     for l in p.bwd.launches)
+    assert p.num_launches()["backward"] == 90 - 12
+    monkeypatch.setenv("MDA_AOL", "pw")
+    c = InceptionProgram(Multi_Classifier(), 4, "cpu")
+    assert 0 < c.n_aol < 43 and all(l.args[3]["KH"] * l.args[3]["KW"] == 1 for l in c.bwd.launches
+                                    if l.name == "conv_dgrad" and "aol" in l.args[3])
 
 
 def test_stem_tap_packing_geometry():

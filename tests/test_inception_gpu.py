@@ -145,18 +145,27 @@ def _nchw(a):
     return t[idx].float().view(a.B, a.H, a.W, a.C).permute(0, 3, 1, 2)
 
 
-def test_inception_backward_layer_local():
+@pytest.mark.parametrize("aol", ["0", "1"])
+def test_inception_backward_layer_local(monkeypatch, aol):
     """Every op's backward against autograd of that single op, fed with the ENGINE's own input activation
     and incoming gradient (the sum of its gradient sources).  This checks the whole backward wiring (the
     concat-slice gradient routing, multi-consumer source lists, pool backward) and every kernel at
     bf16-rounding precision, independent of the network's error amplification."""
     from mtl_das_pytorch_amd.engine.inception import CBR
+    monkeypatch.setenv("MDA_AOL", aol)  # apply-on-load (opt-in) folds the apply-only tails into the convs
     model, ref, prog, X, labels = _setup(p_drop=0.5)
+    assert (prog.n_aol > 0) == (aol == "1")
     idx = torch.arange(prog.B, device="cuda")
     _engine_step(prog, X, labels, idx)
     prog.flat.sync_module_grads()
     q = lambda t: t.bfloat16().float()
     worst = {}
+    # apply-on-load: dy of these convs is never materialised -- rebuild it from the engine's own
+    # coefficient table exactly as the dgrad / wgrad operand loaders do
+    from mtl_das_pytorch_amd.engine.core import P
+    coefs = {c.data_ptr(): c for c in getattr(prog, "aol_coefs", [])}
+    aol = {l.args[3]["aol"]["y"]: l.args[3]["aol"] for l in prog.bwd.launches
+           if l.name == "conv_dgrad" and "aol" in l.args[3]}
     for op in prog.ops:
         g = sum(_nchw(a) for a in op.out.grad_sources())
         if getattr(op, "nol_from", None) is not None:
@@ -183,8 +192,15 @@ def test_inception_backward_layer_local():
             dgam, dbet = (dz * xh).sum((0, 2, 3)), dz.sum((0, 2, 3))
             dyq = gam.view(1, -1, 1, 1) * inv * (dz - dz.mean((0, 2, 3), keepdim=True)
                                                  - xh * (dz * xh).mean((0, 2, 3), keepdim=True))
-            y.backward(_nchw(op.dy))  # the conv backward kernels are checked on the engine's own dy
-            checks = {"dy": (_nchw(op.dy), dyq), "dW": (conv.weight.grad, w.grad),
+            dye = _nchw(op.dy)
+            a = aol.get(P(op.y.t, op.y.off))
+            if a is not None:
+                k = coefs[a["coef"]].view(5, -1, 1, 1)
+                yv = _nchw(op.y)
+                dze = g * ((yv * k[3] + k[4]) > 0)
+                dye = q(k[0] * dze + k[1] * yv + k[2])
+            y.backward(dye)  # the conv backward kernels are checked on the engine's own dy
+            checks = {"dy": (dye, dyq), "dW": (conv.weight.grad, w.grad),
                       "dgamma": (bn.weight.grad, dgam), "dbeta": (bn.bias.grad, dbet)}
             if op.dx is not None:
                 dxe = _nchw(op.dx)[:, :conv.in_channels]
