@@ -171,6 +171,11 @@ struct OptSeg {
   int64_t block0;
 };
 
+// Data-gradient image pack tiles (optim.hip pack_dgrad_tile): 64 co x cit ci, cit*taps <= PACK_ROWS LDS rows;
+// keep in sync with engine/core.py build_optseg_table.
+constexpr int PACK_ROWS = 72;
+__host__ __device__ inline int pack_dgrad_cit(int taps) { return std::min(32, PACK_ROWS / taps); }
+
 struct AdamArgs {
   float* p; const float* g; float* m; float* v;
   int64_t n;  // flat buffer length (multiple of 4)

@@ -45,19 +45,55 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, int64_t n) {
   }
 }
 
-// Writes the packed bf16 MFMA images of every conv weight, one thread per 8 packed elements (16-B
-// stores, coalesced); padding is (re)written as zeros.  Segment `kind` selects the image:
-// 1 = forward [Co][(kh,kw,ci)] (rows Npad, cols Kpad_f), 2 = data-gradient [Ci][(kh,kw,co)].
+// Data-gradient image [Ci][(kh,kw,co)] of one (64 co) x (cit ci) tile of a [Co][Ci][taps] weight, through
+// LDS: the reads walk each co's contiguous (ci, tap) run, the writes 16-byte chunks of 8 co -- both
+// coalesced.  (The per-element mapping read the masters with a stride of Ci*taps floats: every 4-byte
+// value pulled its own cache line, on each of the 8 XCD L2s.)  Padding rows / columns are never written:
+// the images are zero-initialised and nothing else writes them.
+DEV void pack_dgrad_tile(const float* __restrict__ W, const OptSeg& S, int tile, float (*s_t)[65]) {
+  const int taps = S.KH * S.KW;
+  const int cit = pack_dgrad_cit(taps);
+  const int nci = (S.Ci + cit - 1) / cit;
+  const int co0 = (tile / nci) * 64, ci0 = (tile % nci) * cit;
+  const int run = min(cit, S.Ci - ci0) * taps;  // contiguous floats per co
+  const int nco = min(64, S.Co - co0);
+  for (int e = threadIdx.x; e < nco * run; e += 256) {
+    const int col = e / run, r = e - col * run;
+    s_t[r][col] = W[((int64_t)(co0 + col) * S.Ci + ci0) * taps + r];
+  }
+  __syncthreads();
+  for (int item = threadIdx.x; item < run * 8; item += 256) {
+    const int r = item >> 3, ch = item & 7;
+    if (ch * 8 >= nco) continue;
+    const int ci = ci0 + r / taps, tap = r % taps;
+    uint32_t w4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w4[j] = (uint32_t)f2bf(s_t[r][ch * 8 + 2 * j]) | ((uint32_t)f2bf(s_t[r][ch * 8 + 2 * j + 1]) << 16);
+    *reinterpret_cast<uint4*>(S.wd + (int64_t)ci * S.Kpad_d + tap * S.Co + co0 + ch * 8) =
+        make_uint4(w4[0], w4[1], w4[2], w4[3]);
+  }
+}
+
+// Writes the packed bf16 MFMA images of every conv weight.  Segment `kind` selects the image:
+// 1 = forward [Co][(kh,kw,ci)] (rows Npad, cols Kpad_f): one thread per 8 packed elements (16-B stores,
+// coalesced), padding (re)written as zeros; 2 = data-gradient [Ci][(kh,kw,co)]: one block per LDS-
+// transposed tile (pack_dgrad_tile).
 // `step` (non-null after an Adam update): the step counter is advanced here -- the pack runs after the
 // Adam kernel that read it, so the separate one-thread launch is not needed.
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, const OptSeg* __restrict__ segs, int ns,
                                                    float* step) {
+  __shared__ float s_t[PACK_ROWS][65];
   if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1.f;
   int lo = 0, hi = ns - 1;
   while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (segs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
   const OptSeg& S = segs[lo];
+  if (S.kind == 2) {
+    pack_dgrad_tile(P + S.off, S, (int)((int64_t)blockIdx.x - S.block0), s_t);
+    return;
+  }
   const int64_t e8 = ((int64_t)blockIdx.x - S.block0) * 256 + threadIdx.x;  // index of an 8-element chunk
-  const int K = S.kind == 1 ? S.Kpad_f : S.Kpad_d;
+  const int K = S.Kpad_f;
   const int64_t total8 = S.n / 8;  // S.n = rows * K (multiple of 8)
   if (e8 >= total8) return;
   const int64_t e = e8 * 8;
@@ -72,19 +108,14 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, 
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = k0 + j + h;
-      float x = 0.f;
-      if (S.kind == 1) {  // row = co, k = tap*Cs + ci
-        const int ci = k % S.Cs, tap = k / S.Cs;
-        if (row < S.Co && tap < taps && ci < S.Ci) x = W[((int64_t)row * S.Ci + ci) * taps + tap];
-      } else {            // row = ci, k = tap*Co + co
-        const int co = k % S.Co, tap = k / S.Co;
-        if (row < S.Ci && tap < taps) x = W[((int64_t)co * S.Ci + row) * taps + tap];
-      }
+      float x = 0.f;  // row = co, k = tap*Cs + ci
+      const int ci = k % S.Cs, tap = k / S.Cs;
+      if (row < S.Co && tap < taps && ci < S.Ci) x = W[((int64_t)row * S.Ci + ci) * taps + tap];
       v[h] = x;
     }
     w4[j / 2] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
   }
-  bf16_t* dst = (S.kind == 1 ? S.wf : S.wd) + e;
+  bf16_t* dst = S.wf + e;
   *reinterpret_cast<uint4*>(dst) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
 }
 

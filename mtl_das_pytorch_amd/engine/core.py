@@ -479,6 +479,9 @@ def build_wgfin_table(descs: List[dict], device) -> tuple:
     return t, len(descs), b0
 
 
+PACK_ROWS = 72  # csrc/kernels.h
+
+
 def build_optseg_table(segs: List[dict], device) -> tuple:
     dt = np.dtype([("off", "<i8"), ("n", "<i8"), ("kind", "<i4"), ("_pad0", "<i4"), ("wf", "<u8"), ("wd", "<u8"),
                    ("Co", "<i4"), ("Ci", "<i4"), ("KH", "<i4"), ("KW", "<i4"), ("Cs", "<i4"), ("Kpad_f", "<i4"),
@@ -490,6 +493,13 @@ def build_optseg_table(segs: List[dict], device) -> tuple:
         for k, v in s.items():
             arr[i][k] = v
         arr[i]["block0"] = b0
-        b0 += math.ceil(s["n"] / 2048)  # 256 threads x 8 packed elements
+        if s["kind"] == 2:  # LDS-transposed tiles of 64 co x cit ci (csrc/optim.hip pack_dgrad_tile)
+            taps = s["KH"] * s["KW"]
+            if taps > PACK_ROWS:
+                raise ValueError(f"pack: {taps} taps exceed the {PACK_ROWS} LDS rows of a tile")
+            cit = min(32, PACK_ROWS // taps)
+            b0 += math.ceil(s["Co"] / 64) * math.ceil(s["Ci"] / cit)
+        else:
+            b0 += math.ceil(s["n"] / 2048)  # 256 threads x 8 packed elements
     t = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
     return t, len(segs), b0

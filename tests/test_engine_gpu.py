@@ -198,3 +198,37 @@ def test_batched_wgrad_bitwise_equal(model_name):
         _engine_step(prog, X, lab, torch.arange(8, device="cuda"))
         grads.append(prog.flat.grads.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
+def test_pack_images_match_layouts(model_name):
+    """The optimizer's pack (forward image per 8 elements, data-gradient image through LDS-transposed
+    tiles) writes exactly the bf16 layouts of ops.functional.pack_weight_fwd / pack_weight_dgrad, with
+    zero padding, for every conv of the program (after perturbing the masters so no stale image passes)."""
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.engine.mtl import MTLProgram
+    from mtl_das_pytorch_amd.models import MTL_Net, Multi_Classifier
+    from mtl_das_pytorch_amd.ops.functional import pack_weight_dgrad, pack_weight_fwd
+    torch.manual_seed(3)
+    prog = MTLProgram(MTL_Net(), 4, "cuda") if model_name == "MTL" else InceptionProgram(Multi_Classifier(), 4, "cuda")
+    with torch.no_grad():
+        prog.flat.params.add_(torch.randn_like(prog.flat.params) * 1e-2)
+    prog.opt["pack"].run()
+    torch.cuda.synchronize()
+    n = 0
+    for c in prog.convs:
+        for g, m in enumerate(c.mods):
+            w = m.weight.detach().float()
+            if c.KH * c.KW == w.shape[2] * w.shape[3]:  # the packed-tap stem has its own (virtual) layout
+                ef = pack_weight_fwd(w, c.Cs)
+                got = c.wf[g]
+                assert torch.equal(got[:ef.shape[0], :ef.shape[1]], ef)
+                assert not got[ef.shape[0]:].any() and not got[:, ef.shape[1]:].any()
+            ed = pack_weight_dgrad(w, c.Cs)
+            gd = c.wd[g]
+            if c.KH * c.KW != w.shape[2] * w.shape[3]:
+                continue
+            assert torch.equal(gd[:ed.shape[0], :ed.shape[1]], ed), (c.Co, c.Ci, c.KH, c.KW)
+            assert not gd[ed.shape[0]:].any() and not gd[:, ed.shape[1]:].any()
+            n += 1
+    assert n > 10
