@@ -156,8 +156,6 @@ void wgrad(int cfg, int G, int64_t stream, py::dict d) {
 py::tuple wgrad_table(int cfg, py::list dicts, py::list groups) {
   const bool aol = cfg >= WGRAD_AOL_CFG;  // the AOL instantiation: every job must apply on load
   if (aol) cfg -= WGRAD_AOL_CFG;
-  int TN, TK;
-  if (wgrad_tile_shape(cfg, TN, TK)) throw std::runtime_error("wgrad_table: bad cfg");
   std::vector<WgradJob> jobs(dicts.size());
   int64_t b0 = 0;
   for (size_t i = 0; i < jobs.size(); ++i) {
@@ -166,8 +164,8 @@ py::tuple wgrad_table(int cfg, py::list dicts, py::list groups) {
     j.a = parse_wgrad(dicts[i].cast<py::dict>());
     if ((j.a.aol != 0) != aol) throw std::runtime_error("wgrad_table: apply-on-load jobs need the AOL cfg and vice versa");
     j.G = groups[i].cast<int>();
-    j.ntiles = ((j.a.Npad + TN - 1) / TN) * (j.a.Kpad / TK);
-    if (j.a.Kpad % TK) throw std::runtime_error("wgrad_table: Kpad not a multiple of the tile");
+    j.ntiles = wgrad_ntiles(cfg, j.a);
+    if (j.ntiles < 0) throw std::runtime_error("wgrad_table: cfg " + std::to_string(cfg) + " invalid for job " + std::to_string(i));
     j.block0 = b0;
     b0 += (int64_t)j.ntiles * j.a.splits * j.G;
   }

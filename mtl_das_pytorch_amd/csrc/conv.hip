@@ -641,6 +641,171 @@ __global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob*
   wgrad_block<TN, TK, MCH, AOL>(J.a, r % J.ntiles, r / J.ntiles, z);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Patch weight gradient for 3x3 / stride 1 / pad 1 convolutions (tile configs 12-15).  The im2col operand
+// of a 3x3 conv re-reads every input pixel 9 times; here a block stages a strip of PR output rows' INPUT
+// rows (PR + 2 rows with halo, CB channels) once in LDS and forms all 9 taps' MFMA operands from it with
+// shifted transposed reads -- the input is read once per (strip, channel slice) instead of once per
+// (tap, K tile).  Output rows are padded to a multiple of 8 pixels (Wo8) so that each 8-pixel MFMA row
+// group stays inside one image row; the pad pixels carry dy = 0.  Work unit = (image, strip); split s of
+// a job covers units [s * m_per_split, ...).  Tile = (TN output channels) x (all 9 taps x CB input
+// channels), written to the same [split][Npad][Kpad] slab layout as the im2col kernel (k = tap*Cs + ci).
+constexpr int PATCH_R = 4;  // output rows per strip
+template <int TN, int CB, int W8>
+DEV void wgrad_patch_block(const WgradArgs& a, const int tile, const int split, const int z) {
+  constexpr int R = PATCH_R, TAPS = 9;
+  constexpr int CBP = CB + 8, LDY = TN + 8, WP = W8 + 2;
+  constexpr int FN = TN / 16, FC = CB / 16, NFR = FN * TAPS * FC, FPW = (NFR + 3) / 4;
+  constexpr int NPI = (R + 2) * WP * (CB / 8), NDI = R * W8 * (TN / 8);
+  constexpr int NPL = (NPI + 255) / 256, NDL = (NDI + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t s_p[(R + 2) * WP * CBP];
+  __shared__ __attribute__((aligned(16))) bf16_t s_y[R * W8 * LDY];
+  __shared__ float s_nsc[CB], s_nsh[CB];
+
+  const int ncs = a.Cs / CB;
+  const int tn = tile / ncs, tcs = tile - tn * ncs;
+  const int n0 = tn * TN, c0 = tcs * CB;
+  const int Wo8 = (a.Wo + 7) & ~7;
+  const int wpr = Wo8 + 2;  // staged input columns: iw = -1 .. Wo8
+  const int nstrip = (a.Ho + R - 1) / R;
+  const int U = a.B * nstrip;
+  const int ubeg = split * a.m_per_split, uend = min(U, ubeg + a.m_per_split);
+  const int seg = (a.src.C1 > 0 && c0 >= a.src.C0) ? 1 : 0;
+  const bf16_t* xz = a.src.p[seg] + a.src.gs[seg] * z + (c0 - seg * a.src.C0);
+  const int ldx = a.src.ld[seg];
+  const bf16_t* dyz = a.dy + a.dgs * z;
+  if (a.nol) {
+    const float* kz = a.nol_consts + (int64_t)z * 4 * a.Cs;
+    for (int t = threadIdx.x; t < CB; t += 256) { s_nsc[t] = kz[c0 + t]; s_nsh[t] = kz[a.Cs + c0 + t]; }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  f32x4 acc[FPW];
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 rp[NPL], ry[NDL];
+  uint32_t pok = 0;
+  const int npi = (R + 2) * wpr * (CB / 8), ndi = R * Wo8 * (TN / 8);
+  auto load_unit = [&](int u) {
+    const int b = u / nstrip, oh0 = (u - b * nstrip) * R;
+    pok = 0;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int v = threadIdx.x + 256 * i;
+      rp[i] = make_uint4(0, 0, 0, 0);
+      if (v < npi) {
+        const int cg = v % (CB / 8), q = v / (CB / 8);
+        const int j = q / wpr, c = q - j * wpr;
+        const int ih = oh0 - 1 + j, iw = c - 1;
+        if (ih >= 0 && ih < a.Hi && iw >= 0 && iw < a.Wi) {
+          rp[i] = *reinterpret_cast<const uint4*>(xz + ((int64_t)(b * a.Hi + ih) * a.Wi + iw) * ldx + cg * 8);
+          pok |= 1u << i;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NDL; ++i) {
+      const int v = threadIdx.x + 256 * i;
+      ry[i] = make_uint4(0, 0, 0, 0);
+      if (v < ndi) {
+        const int cg = v % (TN / 8), p = v / (TN / 8);
+        const int r = p / Wo8, ow = p - r * Wo8;
+        const int oh = oh0 + r, n = n0 + cg * 8;
+        if (oh < a.Ho && ow < a.Wo && n < a.Co)
+          ry[i] = *reinterpret_cast<const uint4*>(dyz + ((int64_t)(b * a.Ho + oh) * a.Wo + ow) * a.ldd + n);
+      }
+    }
+  };
+  auto store_unit = [&]() {
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int v = threadIdx.x + 256 * i;
+      if (v < npi) {
+        const int cg = v % (CB / 8), q = v / (CB / 8);
+        const int j = q / wpr, c = q - j * wpr;
+        uint4 u = rp[i];
+        if (a.nol && ((pok >> i) & 1)) {
+          uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const int cc = cg * 8 + 2 * h;
+            float lo = __uint_as_float(w4[h] << 16) * s_nsc[cc] + s_nsh[cc];
+            float hi = __uint_as_float(w4[h] & 0xffff0000u) * s_nsc[cc + 1] + s_nsh[cc + 1];
+            if (a.nol_kind == ACT_RELU) { lo = fmaxf(lo, 0.f); hi = fmaxf(hi, 0.f); }
+            w4[h] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+          }
+          u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+        *reinterpret_cast<uint4*>(&s_p[(j * WP + c) * CBP + cg * 8]) = u;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NDL; ++i) {
+      const int v = threadIdx.x + 256 * i;
+      if (v < ndi) {
+        const int cg = v % (TN / 8), p = v / (TN / 8);
+        *reinterpret_cast<uint4*>(&s_y[p * LDY + cg * 8]) = ry[i];
+      }
+    }
+  };
+
+  __syncthreads();  // NOL constants
+  const int ksteps = R * Wo8 / 32;
+  if (ubeg < uend) load_unit(ubeg);
+  for (int u = ubeg; u < uend; ++u) {
+    store_unit();
+    __syncthreads();
+    if (u + 1 < uend) load_unit(u + 1);  // in flight during this strip's MFMAs
+    for (int ks = 0; ks < ksteps; ++ks) {
+      const int prow = ks * 32 + 8 * (lane >> 4);  // this lane group's 8 pixels: one image row
+      const int r = prow / Wo8, ow = prow - r * Wo8;
+#pragma unroll
+      for (int j = 0; j < FPW; ++j) {
+        const int fr = wid + 4 * j;
+        if (fr < NFR) {
+          const int cs = fr % FC, t2 = fr / FC;
+          const int tap = t2 % TAPS, fi = t2 / TAPS;
+          const int kh = tap / 3, kw = tap - kh * 3;
+          bf16x8 av = tr_read8(&s_y[prow * LDY], LDY, fi * 16, lane);
+          bf16x8 bv = tr_read8(&s_p[((r + kh) * WP + ow + kw) * CBP], CBP, cs * 16, lane);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* slab = a.slab + (((int64_t)z * a.splits + split) * a.Npad) * a.Kpad;
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) {
+    const int fr = wid + 4 * j;
+    if (fr < NFR) {
+      const int cs = fr % FC, t2 = fr / FC;
+      const int tap = t2 % TAPS, fi = t2 / TAPS;
+      const int row = n0 + fi * 16 + 4 * (lane >> 4);
+      const int col = tap * a.Cs + c0 + cs * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (row + q < a.Npad) slab[(int64_t)(row + q) * a.Kpad + col] = acc[j][q];
+    }
+  }
+}
+
+template <int TN, int CB, int W8>
+__global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(WgradArgs a) {
+  wgrad_patch_block<TN, CB, W8>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+template <int TN, int CB, int W8>
+__global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const WgradJob* __restrict__ jobs, int nj) {
+  int lo = 0, hi = nj - 1;
+  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
+  const WgradJob& J = jobs[lo];
+  const int local = (int)((int64_t)blockIdx.x - J.block0);
+  const int per_z = J.ntiles * J.a.splits;
+  const int z = local / per_z, r = local - z * per_z;
+  wgrad_patch_block<TN, CB, W8>(J.a, r % J.ntiles, r / J.ntiles, z);
+}
+
 // Sums the split-M partial slabs of many convolutions into the flat fp32 gradient buffer (deterministic,
 // one launch per backward), reference weight layout [Cout][Cin][KH][KW].
 // Each weight is reduced by D.lanes threads (a power of two <= 16, chosen per conv from its split count):
@@ -751,7 +916,44 @@ int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
   case 4: X(16, 64, 128) case 5: X(16, 32, 256) case 6: X(32, 32, 256) case 7: X(64, 32, 64)        \
   case 8: X(16, 192, 64) case 9: X(16, 128, 64) case 10: X(32, 192, 64) case 11: X(32, 320, 32)
 
+// Patch configs 12-15 (TN, CB, max padded output width); keep in sync with ops/functional.py WGRAD_PATCH.
+#define WGRAD_PATCH_CASES(X) case 12: X(16, 16, 88) case 13: X(32, 16, 88) case 14: X(32, 32, 48) case 15: X(64, 32, 24)
+
+int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8) {
+  static const int tn[] = {16, 32, 32, 64}, cb[] = {16, 16, 32, 32}, w8[] = {88, 88, 48, 24};
+  if (cfg < WGRAD_PATCH_CFG0 || cfg >= WGRAD_PATCH_CFG0 + 4) return -1;
+  TN = tn[cfg - WGRAD_PATCH_CFG0]; CB = cb[cfg - WGRAD_PATCH_CFG0]; W8 = w8[cfg - WGRAD_PATCH_CFG0];
+  return 0;
+}
+
+int wgrad_ntiles(int cfg, const WgradArgs& a) {
+  int TN, TK, CB, W8;
+  if (!wgrad_patch_shape(cfg, TN, CB, W8)) {
+    const int Wo8 = (a.Wo + 7) & ~7;
+    const bool seg_ok = a.src.C1 == 0 || a.src.C0 % CB == 0;
+    if (a.KH != 3 || a.KW != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1 || a.Hi != a.Ho ||
+        a.Wi != a.Wo || a.Cs % CB || Wo8 > W8 || a.aol || !seg_ok || a.Kpad < 9 * a.Cs)
+      return -2;
+    return ((a.Npad + TN - 1) / TN) * (a.Cs / CB);
+  }
+  if (wgrad_tile_shape(cfg, TN, TK) || a.Kpad % TK) return -2;  // the K tiles must cover Kpad exactly
+  return ((a.Npad + TN - 1) / TN) * (a.Kpad / TK);
+}
+
 int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st) {
+  if (cfg >= WGRAD_PATCH_CFG0) {
+    const int nt = wgrad_ntiles(cfg, a);
+    if (nt < 0) return nt;
+#define LAUNCH_WGP(TN, CB, W8)                                                                      \
+  hipLaunchKernelGGL((conv_wgrad_patch_kernel<TN, CB, W8>), dim3(nt, a.splits, G), dim3(256), 0, st, a); \
+  break;
+    switch (cfg) {
+      WGRAD_PATCH_CASES(LAUNCH_WGP)
+      default: return -1;
+    }
+#undef LAUNCH_WGP
+    return (int)hipGetLastError();
+  }
 #define LAUNCH_WG(TN, TK, MCH)                                                                      \
   {                                                                                                 \
     dim3 grid(((a.Npad + TN - 1) / TN) * (a.Kpad / TK), a.splits, G);                               \
@@ -784,6 +986,18 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
   dim3 grid((unsigned)nblocks);
   const bool aol = cfg >= WGRAD_AOL_CFG;
   if (aol) cfg -= WGRAD_AOL_CFG;
+  if (cfg >= WGRAD_PATCH_CFG0) {
+    if (aol) return -2;
+#define LAUNCH_WGPB(TN, CB, W8)                                                                                 \
+  hipLaunchKernelGGL((conv_wgrad_patch_batched_kernel<TN, CB, W8>), grid, dim3(256), 0, st, d_jobs, nj); \
+  break;
+    switch (cfg) {
+      WGRAD_PATCH_CASES(LAUNCH_WGPB)
+      default: return -1;
+    }
+#undef LAUNCH_WGPB
+    return (int)hipGetLastError();
+  }
 #define LAUNCH_WGB(TN, TK, MCH)                                                                              \
   if (aol) hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH, true>), grid, dim3(256), 0, st, d_jobs, nj); \
   else hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH, false>), grid, dim3(256), 0, st, d_jobs, nj); \

@@ -187,6 +187,9 @@ struct AdamArgs {
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st);
 int wgrad_tile_shape(int cfg, int& TN, int& TK);
+constexpr int WGRAD_PATCH_CFG0 = 12;  // wgrad cfgs 12-15: 3x3/s1 patch kernels (conv.hip wgrad_patch_block)
+int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8);
+int wgrad_ntiles(int cfg, const WgradArgs& a);  // tiles per group of a wgrad launch, < 0: cfg invalid for a
 constexpr int WGRAD_AOL_CFG = 100;  // batched-wgrad cfg offset selecting the apply-on-load kernels
 int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st);
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..ops.functional import WGRAD_TILES, bnb_plan, wgrad_cfg
+from ..ops.functional import WGRAD_PATCH, WGRAD_TILES, bnb_plan, patch_plan, patch_valid, wgrad_cfg
 from ..ops.hip import lib, ptr
 
 NREP = 32  # must match csrc/common.h
@@ -332,6 +332,8 @@ class ConvLayer:
         self.ph, self.pw = m.padding
         if m.groups != 1 or m.dilation != (1, 1):
             raise ValueError("grouped / dilated convolutions are not supported")
+        self.stem_geom = geom
+        self.src_C0, self.src_C1 = None, 0  # input segments, known once the backward is emitted (wgrad_args)
         if geom is not None:
             self.Ci, self.KH, self.KW = geom["Ci"], geom["KH"], geom["KW"]
             self.sh, self.sw, self.ph, self.pw = geom["sh"], geom["sw"], geom["ph"], geom["pw"]
@@ -359,7 +361,7 @@ class ConvLayer:
         # largest split count any config can ask for)
         self.Kpad_w = pad_to(taps * self.Cs, 64)
         self._wgrad_args = None
-        max_splits = max(self.wgrad_plan(c)[0] for c in WGRAD_TILES if self.wgrad_valid(c))
+        max_splits = max(self.wgrad_plan(c)[0] for c in list(WGRAD_TILES) + list(WGRAD_PATCH) if self.wgrad_valid(c))
         self.slab = arena.empty((self.G, max_splits, self.Npad, self.Kpad_w), torch.float32)
         self.set_wgrad_cfg(wgrad_cfg(self.Co, self.Kpad_w))
 
@@ -370,10 +372,19 @@ class ConvLayer:
     MIN_SPLIT_PX = 1024
 
     def wgrad_valid(self, cfg: int) -> bool:
-        """The K tiles of ``cfg`` cover this conv's padded reduction exactly."""
+        """The K tiles of ``cfg`` cover this conv's padded reduction exactly (patch configs: a 3x3 / s1 /
+        p1 conv whose input channels split into whole CB slices and whose rows fit the tile width)."""
+        if cfg in WGRAD_PATCH:
+            return self.stem_geom is None and patch_valid(cfg, self.Cs, self.KH, self.KW, (self.sh, self.sw),
+                                                          (self.ph, self.pw), self.Hi, self.Wi, self.Ho, self.Wo,
+                                                          self.src_C0, self.src_C1)
         return self.Kpad_w % WGRAD_TILES[cfg][1] == 0
 
     def wgrad_plan(self, cfg: int):
+        if cfg in WGRAD_PATCH:
+            import os
+            return patch_plan(cfg, self.B, self.Ho, self.Npad, self.Cs, self.G,
+                              int(os.environ.get("MDA_PATCH_TARGET", "128")))
         TN, TK, MCH = WGRAD_TILES[cfg]
         tiles = math.ceil(self.Npad / TN) * (self.Kpad_w // TK) * self.G
         # whole-reduction tiles (TK >= 128) have one tile per channel block: shorter per-block pixel
@@ -440,6 +451,7 @@ class ConvLayer:
         return (1, self.fwd_cfg(self.Cs, self.M_in), self.G, d)
 
     def wgrad_args(self, src: dict, dy: Act) -> tuple:
+        self.src_C0, self.src_C1 = src.get("C0"), src.get("C1", 0)
         self._wgrad_args = d = {"src": src, "dy": dy.p, "dgs": dy.gs, "ldd": dy.ld, "slab": P(self.slab), "splits": self.splits,
              "m_per_split": self.m_per_split, "B": self.B, "Hi": self.Hi, "Wi": self.Wi, "Ho": self.Ho, "Wo": self.Wo,
              "Co": self.Co, "Npad": self.Npad, "Cs": self.Cs, "KH": self.KH, "KW": self.KW, "sh": self.sh,

@@ -7,15 +7,25 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ..ops.functional import WGRAD_TILES
+from ..ops.functional import PATCH_R, WGRAD_PATCH, WGRAD_TILES
 from ..ops.hip import lib
-from .core import Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table
+from .core import Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, pad_to
 from .program import Launch, Phase, k_adam, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad, k_wgrad_batched
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
 
 
 WGRAD_AOL_CFG = 100  # batched-wgrad cfg offset of the apply-on-load kernels (csrc/kernels.h)
+
+
+def _wgrad_cost(cfg: int, G: int, d: dict) -> int:
+    """MFMA work (MACs incl. tile padding) of one weight-gradient launch -- used to balance fan-out."""
+    if cfg in WGRAD_PATCH:
+        TN, CB, _ = WGRAD_PATCH[cfg]
+        px = d["splits"] * d["m_per_split"] * PATCH_R * pad_to(d["Wo"], 8)
+        return px * G * math.ceil(d["Npad"] / TN) * TN * 9 * d["Cs"]
+    TN, TK, MCH = WGRAD_TILES[cfg]
+    return d["splits"] * d["m_per_split"] * G * TN * TK * math.ceil(d["Npad"] / TN) * (d["Kpad"] // TK)
 
 
 def _refers_to(args, ptr: int) -> bool:
@@ -275,9 +285,7 @@ class LoweredProgram:
                 table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
                 self.wgrad_tables.append(table)
                 batched.append(Launch("wgrad_batched", k_wgrad_batched, key, table, len(group), nblocks, stream=st))
-                TN, TK, MCH = WGRAD_TILES[key % WGRAD_AOL_CFG]
-                costs.append(sum(l.args[2]["splits"] * l.args[2]["m_per_split"] * l.args[1] * TN * TK *
-                                 math.ceil(l.args[2]["Npad"] / TN) * (l.args[2]["Kpad"] // TK) for l in group))
+                costs.append(sum(_wgrad_cost(key % WGRAD_AOL_CFG, l.args[1], l.args[2]) for l in group))
             pos = max((i for i, k in enumerate(keep) if k.stream == st), default=len(keep) - 1) + 1
             if staged is not None and st == staged[0]:
                 pos = keep.index(staged[1]) + 1

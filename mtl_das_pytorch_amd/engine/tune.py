@@ -15,7 +15,7 @@ from typing import Dict, Iterable, Optional
 
 import torch
 
-from ..ops.functional import WGRAD_TILES
+from ..ops.functional import WGRAD_PATCH, WGRAD_TILES
 from ..ops.hip import lib
 
 CONV_CFGS = list(range(14))
@@ -24,7 +24,7 @@ CONV_CFGS = list(range(14))
 def fused_max_m(kind: int) -> int:
     """csrc/bn.hip tail_bwd_fused_kernel: 1024 threads x <= 4 register-cached pixels (2 for ADD_RELU)."""
     return 1024 * (2 if kind == 4 else 4)
-WGRAD_CFGS = sorted(WGRAD_TILES)
+WGRAD_CFGS = sorted(WGRAD_TILES) + sorted(WGRAD_PATCH)
 _CACHE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_cfgs.json")
 
 

@@ -177,6 +177,29 @@ WGRAD_TILES = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 
                8: (16, 192, 64), 9: (16, 128, 64), 10: (32, 192, 64), 11: (32, 320, 32)}  # (TN, TK, MCH)
 
 
+# 3x3 / stride-1 / pad-1 patch kernels (csrc/conv.hip wgrad_patch_block): (TN, CB, max padded width)
+WGRAD_PATCH = {12: (16, 16, 88), 13: (32, 16, 88), 14: (32, 32, 48), 15: (64, 32, 24)}
+PATCH_R = 4  # output rows per work unit
+
+
+def patch_valid(cfg, Cs, KH, KW, stride, padding, Hi, Wi, Ho, Wo, C0=None, C1=0) -> bool:
+    TN, CB, W8 = WGRAD_PATCH[cfg]
+    s = (stride, stride) if isinstance(stride, int) else tuple(stride)
+    p = (padding, padding) if isinstance(padding, int) else tuple(padding)
+    return ((KH, KW) == (3, 3) and s == (1, 1) and p == (1, 1) and (Hi, Wi) == (Ho, Wo) and Cs % CB == 0
+            and _pad(Wo, 8) <= W8 and (C1 == 0 or C0 % CB == 0))
+
+
+def patch_plan(cfg, B, Ho, Npad, Cs, G=1, target=512):
+    """(splits, units per split) of a patch wgrad: unit = (image, strip of PATCH_R output rows)."""
+    TN, CB, _ = WGRAD_PATCH[cfg]
+    U = B * math.ceil(Ho / PATCH_R)
+    tiles = math.ceil(Npad / TN) * (Cs // CB) * G
+    splits = max(1, min(U, math.ceil(target / tiles)))
+    ups = math.ceil(U / splits)
+    return math.ceil(U / ups), ups
+
+
 def wgrad_cfg(Co: int, Kpad: int) -> int:
     return 0 if Co <= 16 else ((1 if Kpad <= 64 else 2) if Co <= 32 else 3)
 
@@ -196,15 +219,20 @@ def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=No
     Npad = _pad(Co, 16)
     if cfg is None:
         cfg = wgrad_cfg(Co, Kpad)
-    TN, TK, MCH = WGRAD_TILES[cfg]
-    if Kpad % TK:
-        raise ValueError(f"wgrad config {cfg} (TK={TK}) does not tile the padded reduction {Kpad}")
-    M = B * Ho * Wo
-    tiles = math.ceil(Npad / TN) * (Kpad // TK)
-    if splits is None:
-        splits = max(1, min(math.ceil(M / MCH), math.ceil(512 / tiles)))
-    mps = _pad(math.ceil(M / splits), MCH)
-    splits = math.ceil(M / mps)
+    if cfg in WGRAD_PATCH:
+        if not patch_valid(cfg, Cs, KH, KW, (sh, sw), (ph, pw), H, W, Ho, Wo, x.shape[-1], C1):
+            raise ValueError(f"wgrad patch config {cfg} does not fit this convolution")
+        splits, mps = patch_plan(cfg, B, Ho, Npad, Cs)
+    else:
+        TN, TK, MCH = WGRAD_TILES[cfg]
+        if Kpad % TK:
+            raise ValueError(f"wgrad config {cfg} (TK={TK}) does not tile the padded reduction {Kpad}")
+        M = B * Ho * Wo
+        tiles = math.ceil(Npad / TN) * (Kpad // TK)
+        if splits is None:
+            splits = max(1, min(math.ceil(M / MCH), math.ceil(512 / tiles)))
+        mps = _pad(math.ceil(M / splits), MCH)
+        splits = math.ceil(M / mps)
     slab = torch.empty(1, splits, Npad, Kpad, device=x.device, dtype=torch.float32)
     src = {"p0": ptr(x), "ld0": x.shape[-1], "C0": x.shape[-1], "C1": C1}
     if x2 is not None:

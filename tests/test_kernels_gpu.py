@@ -109,6 +109,35 @@ def test_conv_wgrad_whole_k_tiles(fn, case, cfg):
     assert rel(dw, w.grad) < 5e-3
 
 
+@pytest.mark.parametrize("case,cfg", [((2, 33, 83, 16, 16, 3, 1, 1), 12), ((3, 33, 83, 16, 32, 3, 1, 1), 13),
+                                      ((2, 17, 42, 16, 32, 3, 1, 1), 12), ((4, 17, 42, 32, 32, 3, 1, 1), 14),
+                                      ((4, 17, 42, 32, 64, 3, 1, 1), 14), ((4, 9, 21, 64, 64, 3, 1, 1), 15),
+                                      ((4, 5, 11, 128, 128, 3, 1, 1), 15), ((2, 7, 13, 32, 48, 3, 1, 1), 14)])
+@pytest.mark.parametrize("nol", [False, True])
+def test_conv_wgrad_patch(fn, case, cfg, nol):
+    """3x3 / stride-1 patch weight gradients (configs 12-15: the input strip staged once in LDS, all 9 taps
+    read from it): widths that are not multiples of 8, heights that are not multiples of the 4-row strip,
+    Cout not a multiple of the tile, several channel slices, and normalise-on-load of the input."""
+    B, H, W, C, Co, k, s, p = case
+    x, w, _, _, _ = _mk(case, seed=cfg)
+    g = torch.Generator().manual_seed(cfg + 7)
+    dy = torch.randn(B, Co, H, W, generator=g).bfloat16().float().cuda()
+    if nol:
+        consts = torch.zeros(1, 4, C, device="cuda")
+        consts[0, 0] = torch.rand(C, generator=g).cuda() + 0.5
+        consts[0, 1] = torch.randn(C, generator=g).cuda() * 0.3
+        act = F.relu(x * consts[0, 0].view(1, -1, 1, 1) + consts[0, 1].view(1, -1, 1, 1)).bfloat16().float()
+    else:
+        act = x
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(act, wr, stride=s, padding=p).backward(dy)
+    kw = {"nol": (consts, 1)} if nol else {}
+    dw = fn.conv2d_wgrad(nhwc(x).bfloat16(), nhwc(dy).bfloat16(), w.shape, stride=s, padding=p, cfg=cfg, **kw)
+    assert rel(dw, wr.grad) < 5e-3
+    ref = fn.conv2d_wgrad(nhwc(x).bfloat16(), nhwc(dy).bfloat16(), w.shape, stride=s, padding=p, **kw)
+    assert rel(dw, ref) < 1e-5  # same bf16 operands, fp32 accumulation: only the summation order differs
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("case", [(4, 17, 42, 32, 32, 3, 1, 1), (2, 33, 83, 16, 16, 3, 1, 1), (4, 9, 21, 64, 128, 3, 2, 1),
                                   (4, 5, 11, 64, 128, 3, 1, 1)])
