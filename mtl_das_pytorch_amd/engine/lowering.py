@@ -244,6 +244,42 @@ class LoweredProgram:
             if l.name == "wgrad_finalize":
                 l.args = self._wgfin_args()
 
+    def merge_wgrad_cfgs(self, max_batches: Optional[int] = None) -> int:
+        """Cap the number of distinct weight-gradient tile configs per stream (= batched launches, which run
+        back to back at the end of the stream's backward): repeatedly move the cheapest config group whose
+        convs are all valid under another config of the stream into the most expensive such config.  The
+        autotuner picks each conv's config from its isolated time, but a batch that holds one small conv
+        still costs a full dependent launch on the step's tail (~20 us each on Model A's main stream).
+        MDA_WGRAD_MAXB (default 3) sets the cap.  Returns the number of convs moved."""
+        import os
+        if max_batches is None:
+            max_batches = int(os.environ.get("MDA_WGRAD_MAXB", "3"))
+        wg = [l for l in self.bwd.launches if l.name == "conv_wgrad" and l.owner is not None]
+        moved = 0
+        for st in sorted({l.stream for l in wg}):
+            mine = [l for l in wg if l.stream == st and not l.args[2].get("aol")]
+            while True:
+                groups = {}
+                for l in mine:
+                    groups.setdefault(l.args[0], []).append(l)
+                if len(groups) <= max_batches:
+                    break
+                cost = {c: sum(_wgrad_cost(c, l.args[1], l.args[2]) for l in ls) for c, ls in groups.items()}
+                move = None
+                for c in sorted(groups, key=lambda c: cost[c]):
+                    targets = [t for t in groups if t != c and all(l.owner.wgrad_valid(t) for l in groups[c])]
+                    if targets:
+                        move = (c, max(targets, key=lambda t: cost[t]))
+                        break
+                if move is None:
+                    break
+                for l in groups[move[0]]:
+                    l.owner.set_wgrad_cfg(move[1])
+                    l.args = (move[1],) + tuple(l.args[1:])
+                    moved += 1
+        self.n_wgrad_merged = moved
+        return moved
+
     def batch_wgrads(self):
         """Replace the per-conv weight-gradient launches by batched launches, one per (stream, tile
         config) (csrc/conv.hip conv_wgrad_batched_kernel).  Each stream's batch goes after that stream's

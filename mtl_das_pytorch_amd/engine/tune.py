@@ -152,6 +152,8 @@ def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False
     cache = load_cache()
     n0 = len(cache)
     autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose, measure)
+    if batch_wgrads:
+        prog.merge_wgrad_cfgs()
     prog.refresh_wgrad_finalize()
     if batch_wgrads:
         prog.batch_wgrads()

@@ -203,3 +203,26 @@ def test_stream_events_are_recorded_before_they_are_awaited():
                 _check_event_order(ph)
     streams = {l.stream for l in prog.fwd_train.launches}
     assert streams == {0, 1, 2, 3}  # Inception branches spread over four streams
+
+
+def test_merge_wgrad_cfgs_caps_batches_per_stream():
+    """After tuning, small weight-gradient config groups are folded into a valid config of the same
+    stream so that each stream's tail holds at most MDA_WGRAD_MAXB batched launches."""
+    from mtl_das_pytorch_amd.ops.functional import WGRAD_PATCH, WGRAD_TILES
+    p = MTLProgram(MTL_Net(), 32, "cpu")
+    wg = [l for l in p.bwd.launches if l.name == "conv_wgrad"]
+    cfgs = sorted(WGRAD_TILES) + sorted(WGRAD_PATCH)
+    for i, l in enumerate(wg):  # scatter the convs over every config valid for them
+        valid = [c for c in cfgs if l.owner.wgrad_valid(c)]
+        c = valid[i % len(valid)]
+        l.owner.set_wgrad_cfg(c)
+        l.args = (c,) + tuple(l.args[1:])
+    before = {st: len({l.args[0] for l in wg if l.stream == st}) for st in {l.stream for l in wg}}
+    assert max(before.values()) > 3
+    assert p.merge_wgrad_cfgs(3) > 0
+    for st in before:
+        assert len({l.args[0] for l in wg if l.stream == st}) <= 3
+    for l in wg:
+        assert l.owner.wgrad_valid(l.args[0]) and l.args[2]["splits"] == l.owner.splits
+    p.batch_wgrads()
+    _check_event_order(p.bwd)
