@@ -19,7 +19,7 @@ namespace mda {
 // run side by side instead of one after the other, and the label is fetched before the GAP.
 __global__ __launch_bounds__(256) void mtl_head_kernel(HeadArgs a) {
   __shared__ float s_gap[256];
-  __shared__ float s_part[256];
+  __shared__ float s_part8[2048];  // [256 / (C/8) lanes][C]
   __shared__ float s_logit[16], s_prob[16];
   __shared__ int s_lab;
   const int b = blockIdx.x, t = blockIdx.y;
@@ -27,17 +27,35 @@ __global__ __launch_bounds__(256) void mtl_head_kernel(HeadArgs a) {
   const bool valid = a.nvalid == nullptr || b < *a.nvalid;
   {
     const bf16_t* f = a.feat + a.fgs * t + (int64_t)b * a.HW * a.ldf;
-    // GAP: thread -> (channel, pixel-lane)
-    const int lanes = 256 / a.C;  // C in {.., 64, 128, 256}
-    const int c = threadIdx.x % a.C, pl = threadIdx.x / a.C;
-    float s = 0.f;
-    if (pl < lanes)
-      for (int p = pl; p < a.HW; p += lanes) s += bf2f(f[(int64_t)p * a.ldf + c]);
-    s_part[threadIdx.x] = s;
+    // GAP: thread -> (8-channel group, pixel lane), 16-byte loads, 4 independent pixels in flight
+    const int ng = a.C >> 3, lanes = 256 / ng;
+    const int cg = threadIdx.x % ng, pl = threadIdx.x / ng;
+    float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (pl < lanes) {
+      int p = pl;
+      for (; p + 3 * lanes < a.HW; p += 4 * lanes) {
+        float v[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load8(f + (int64_t)(p + u * lanes) * a.ldf + cg * 8, v[u]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s8[j] += (v[0][j] + v[1][j]) + (v[2][j] + v[3][j]);
+      }
+      for (; p < a.HW; p += lanes) {
+        float v[8];
+        load8(f + (int64_t)p * a.ldf + cg * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s8[j] += v[j];
+      }
+    }
+    float* sp = s_part8 + pl * a.C + cg * 8;  // [lanes][C]
+    if (pl < lanes) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sp[j] = s8[j];
+    }
     __syncthreads();
     if (threadIdx.x < a.C) {
       float acc = 0.f;
-      for (int q = 0; q < lanes; ++q) acc += s_part[q * a.C + threadIdx.x];
+      for (int q = 0; q < lanes; ++q) acc += s_part8[q * a.C + threadIdx.x];
       s_gap[threadIdx.x] = acc / (float)a.HW;
     }
     __syncthreads();
@@ -77,17 +95,20 @@ __global__ __launch_bounds__(256) void mtl_head_kernel(HeadArgs a) {
       // d loss_t / d feat[p][c] = w_t * (p_j - y_j) / B / gsz / HW for channel c in group j
       float* d = a.dfeat + a.dgs * t + (int64_t)b * a.HW * a.C;
       const float scale = a.w[t] / ((float)a.B * gsz * a.HW);
-      const int n = a.HW * a.C;
-      for (int i = threadIdx.x; i < n; i += 256) {
-        const int ch = i % a.C;
-        d[i] = s_prob[ch / gsz] * scale;
+      const int n4 = a.HW * a.C / 4;  // 16-byte stores; a group of 4 channels shares its class (gsz % 4 == 0)
+      for (int i = threadIdx.x; i < n4; i += 256) {
+        const int ch = (i * 4) % a.C;
+        const float v = s_prob[ch / gsz] * scale;
+        reinterpret_cast<float4*>(d)[i] = make_float4(v, v, v, v);
       }
     }
   }
 }
 
 int launch_mtl_head(const HeadArgs& a, hipStream_t st) {
-  if (a.C > 256 || 256 % a.C) return -2;
+  if (a.C > 256 || 256 % a.C || a.C % 8 || a.ldf % 8) return -2;
+  for (int t = 0; t < a.T; ++t)
+    if (a.ncls[t] <= 0 || a.C % a.ncls[t] || (a.C / a.ncls[t]) % 4) return -2;
   hipLaunchKernelGGL(mtl_head_kernel, dim3(a.B, a.T), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
