@@ -182,6 +182,9 @@ struct AdamArgs {
   const float* lr; const float* step;  // device scalars (step = number of completed steps)
   float b1, b2, eps, wd, grad_scale;
   int update;  // 0: pack only
+  // fused update (non-null): ONE launch over an OptSeg table of kind 0 (plain Adam ranges) and kind 2
+  // (conv weight tiles: Adam + both bf16 images); the last block to finish advances the step counter
+  unsigned* ticket;
 };
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);

@@ -423,6 +423,17 @@ class ConvLayer:
                              wd=P(self.wd, g * self.Npad_d * self.Kpad_d)))
         return segs
 
+    def fused_segments(self) -> List[dict]:
+        """Fused Adam + pack tiles (csrc/optim.hip adam_pack_fused_kernel): one kind-2 segment per group
+        member that updates the masters and writes both bf16 images."""
+        segs = []
+        for g, m in enumerate(self.mods):
+            segs.append({"off": self.flat.off(m.weight), "Co": self.Co, "Ci": self.Ci, "KH": self.KH, "KW": self.KW,
+                         "Cs": self.Cs, "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d, "kind": 2,
+                         "n": self.Co * self.Ci * self.KH * self.KW,
+                         "wf": P(self.wf, g * self.Npad * self.Kpad), "wd": P(self.wd, g * self.Npad_d * self.Kpad_d)})
+        return segs
+
     def finalize_desc(self) -> dict:
         m0 = self.mods[0]
         return {"slab": P(self.slab), "grad": P(self.flat.grads, self.flat.off(m0.weight)), "ggs": self.wstride,
@@ -494,6 +505,18 @@ def build_wgfin_table(descs: List[dict], device) -> tuple:
 PACK_ROWS = 72  # csrc/kernels.h
 
 
+def plain_ranges(numel: int, covered: List[tuple]) -> List[dict]:
+    """Kind-0 optimizer segments: the parts of [0, numel) not covered by the (off, n) conv-weight ranges."""
+    out, pos = [], 0
+    for off, n in sorted(covered):
+        if off > pos:
+            out.append({"kind": 0, "off": pos, "n": off - pos})
+        pos = max(pos, off + n)
+    if pos < numel:
+        out.append({"kind": 0, "off": pos, "n": numel - pos})
+    return out
+
+
 def build_optseg_table(segs: List[dict], device) -> tuple:
     dt = np.dtype([("off", "<i8"), ("n", "<i8"), ("kind", "<i4"), ("_pad0", "<i4"), ("wf", "<u8"), ("wd", "<u8"),
                    ("Co", "<i4"), ("Ci", "<i4"), ("KH", "<i4"), ("KW", "<i4"), ("Cs", "<i4"), ("Kpad_f", "<i4"),
@@ -505,7 +528,9 @@ def build_optseg_table(segs: List[dict], device) -> tuple:
         for k, v in s.items():
             arr[i][k] = v
         arr[i]["block0"] = b0
-        if s["kind"] == 2:  # LDS-transposed tiles of 64 co x cit ci (csrc/optim.hip pack_dgrad_tile)
+        if s["kind"] == 0:  # plain Adam range, 1024 elements per block
+            b0 += math.ceil(s["n"] / 1024)
+        elif s["kind"] == 2:  # LDS-transposed tiles of 64 co x cit ci (csrc/optim.hip pack_dgrad_tile)
             taps = s["KH"] * s["KW"]
             if taps > PACK_ROWS:
                 raise ValueError(f"pack: {taps} taps exceed the {PACK_ROWS} LDS rows of a tile")
