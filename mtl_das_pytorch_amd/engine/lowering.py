@@ -308,6 +308,15 @@ class LoweredProgram:
                     prev.record = l.record
                 else:
                     self.bwd.alias[l.record] = prev.record
+        import os
+        if os.environ.get("MDA_WGRAD_MAIN", "0") == "1" and len({l.stream for l in wg}) > 1:
+            # every weight gradient at the main stream's tail (after its last join, so every dy is ready):
+            # the side streams' batches no longer contend with the critical backbone chain, and one
+            # merged set of at most MDA_WGRAD_MAXB batches fills the GPU
+            for l in wg:
+                l.stream = 0
+            self.merge_wgrad_cfgs()
+            self.refresh_wgrad_finalize()
         staged = self._stage_wgrads(wg, ls, anchor_of)
         self.wgrad_tables = []
         inserts, tags = [], []

@@ -118,8 +118,13 @@ def test_engine_train_step_matches_autograd(which):
             assert rel(b, ref_bufs[name]) < 3e-2, name
 
 
-def test_adam_matches_torch():
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_adam_matches_torch(monkeypatch, fused):
+    """Flat Adam (and, MDA_FUSED_ADAM=1, the one-launch Adam + pack over conv tiles and plain ranges with
+    its ticket-advanced step counter) against torch.optim.Adam; the fused path must also leave bf16
+    weight images equal to a fresh pack of the updated masters."""
     from mtl_das_pytorch_amd.models import MTL_Net
+    monkeypatch.setenv("MDA_FUSED_ADAM", fused)
     model, ref, prog, X, labels = _setup(MTL_Net)
     g = torch.Generator(device="cpu").manual_seed(5)
     for p in ref.parameters():
@@ -136,6 +141,11 @@ def test_adam_matches_torch():
     assert prog.flat.step.item() == 3
     for (name, p), (_, rp) in zip(model.named_parameters(), ref.named_parameters()):
         assert torch.allclose(p, rp, atol=2e-6, rtol=1e-5), name
+    images = [(c.wf.clone(), c.wd.clone()) for c in prog.convs]
+    prog.opt["pack"].run()
+    torch.cuda.synchronize()
+    for c, (wf, wd) in zip(prog.convs, images):
+        assert torch.equal(c.wf, wf) and torch.equal(c.wd, wd)
 
 
 def test_graph_replay_matches_eager():
