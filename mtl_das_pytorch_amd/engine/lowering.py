@@ -318,6 +318,11 @@ class LoweredProgram:
             self.merge_wgrad_cfgs()
             self.refresh_wgrad_finalize()
         staged = self._stage_wgrads(wg, ls, anchor_of)
+        # MDA_FIN_SPLIT=1 (opt-in; measured neutral: A 31.53-31.58k vs 31.57-31.62k, C 6.89k vs 6.86k): one
+        # finalize per stream, right after that stream's batches
+        split_fin = (os.environ.get("MDA_FIN_SPLIT", "0") == "1" and staged is None and not self._fan_out_wgrads()
+                     and any(l.stream == 0 for l in wg) and all(l.owner is not None for l in wg))
+        self.wgfin_tables = []
         self.wgrad_tables = []
         inserts, tags = [], []
         for st in sorted({l.stream for l in wg}):
@@ -342,6 +347,11 @@ class LoweredProgram:
                 batched = self._fan_out(keep, pos, batched, costs)
                 tags += [l.record for l in batched if l.record is not None]
             else:
+                if split_fin and st != 0:
+                    # this stream's convs are finalized on the stream itself, off the main stream's tail
+                    t, nd, nb = build_wgfin_table([l.owner.finalize_desc() for l in wg if l.stream == st], self.device)
+                    self.wgfin_tables.append(t)
+                    batched.append(Launch("wgrad_finalize", k_wgfin, t, nd, nb, stream=st))
                 batched[-1].record = f"wgrads_s{st}"
                 tags.append(batched[-1].record)
             inserts.append((pos, batched))
@@ -352,6 +362,11 @@ class LoweredProgram:
                 l.record = None
         fin_l = ls[fin]
         fin_l.waits = tuple(tags)
+        if split_fin:  # the main stream's finalize covers its own convs only; the phase end joins the rest
+            t, nd, nb = build_wgfin_table([l.owner.finalize_desc() for l in wg if l.stream == 0], self.device)
+            self.wgfin_tables.append(t)
+            fin_l.args = (t, nd, nb)
+            fin_l.waits = ()
         self.bwd.launches = keep + ls[fin:]
         self.wgrads_batched = True
 

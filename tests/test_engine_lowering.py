@@ -72,18 +72,35 @@ def test_inception_program_structure():
 
 
 def test_wgrad_batching_structure():
-    """All per-conv weight-gradient launches collapse into one launch per tile config, just before the
-    finalize; every conv appears in exactly one job table; the finalize waits for every stream's last
-    batch."""
-    p = MTLProgram(MTL_Net(), 32, "cpu")
-    n_wg = sum(1 for l in p.bwd.launches if l.name == "conv_wgrad")
-    p.batch_wgrads()
-    b = [l for l in p.bwd.launches if l.name == "wgrad_batched"]
-    assert sum(l.args[2] for l in b) == n_wg
-    fin = p.bwd.launches[-1]
-    assert fin.name == "wgrad_finalize"
-    assert set(fin.waits) == {f"wgrads_s{s}" for s in {l.stream for l in b}}
-    _check_event_order(p.bwd)
+    """All per-conv weight-gradient launches collapse into one launch per tile config; every conv appears
+    in exactly one job table.  With MDA_FIN_SPLIT=1 (opt-in) each stream finalizes its own convs right after
+    its batches, so the main stream's tail finalize covers the main stream's convs only; with the split off,
+    one finalize waits for every stream's last batch."""
+    for split in ("1", "0"):
+        import os
+        os.environ["MDA_FIN_SPLIT"] = split
+        try:
+            p = MTLProgram(MTL_Net(), 32, "cpu")
+            n_wg = sum(1 for l in p.bwd.launches if l.name == "conv_wgrad")
+            st_of = {id(l.owner): l.stream for l in p.bwd.launches if l.name == "conv_wgrad"}
+            p.batch_wgrads()
+        finally:
+            del os.environ["MDA_FIN_SPLIT"]
+        b = [l for l in p.bwd.launches if l.name == "wgrad_batched"]
+        assert sum(l.args[2] for l in b) == n_wg
+        fin = p.bwd.launches[-1]
+        assert fin.name == "wgrad_finalize" and fin.stream == 0
+        fins = [l for l in p.bwd.launches if l.name == "wgrad_finalize"]
+        if split == "1":
+            assert fin.waits == () and len(fins) == len({l.stream for l in b})
+            assert sum(f.args[1] for f in fins) == len(p.convs) == len(st_of)
+            for f in fins[:-1]:  # a side stream's finalize follows that stream's last batch
+                assert f.stream != 0 and f.record == f"wgrads_s{f.stream}"
+                last = max(i for i, l in enumerate(p.bwd.launches) if l.name == "wgrad_batched" and l.stream == f.stream)
+                assert p.bwd.launches.index(f) > last
+        else:
+            assert len(fins) == 1 and set(fin.waits) == {f"wgrads_s{s}" for s in {l.stream for l in b}}
+        _check_event_order(p.bwd)
 
 
 def test_wgrad_fanout_structure(monkeypatch):
