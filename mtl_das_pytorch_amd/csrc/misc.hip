@@ -21,9 +21,10 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restri
                                                            bf16_t* __restrict__ out, int64_t* __restrict__ lab_out,
                                                            int B, int Cin, int H, int W, int taps, int off) {
   const int64_t M = (int64_t)B * H * W;
+  const int HW = H * W;
   for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < M; p += (int64_t)gridDim.x * 256) {
-    const int b = (int)(p / (H * W));
-    const int r = (int)(p - (int64_t)b * H * W);
+    const int b = (int)p / HW;  // M < 2^31 (checked by the launcher)
+    const int r = (int)p - b * HW;
     const int64_t src = idx[b];
     float v[8];
     if (taps > 0) {
@@ -48,9 +49,10 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restri
 
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
                         int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, hipStream_t st) {
-  if (Cin > 8 || taps > 8 || (taps > 0 && Cin != 1)) return -2;
+  if (Cin > 8 || taps > 8 || (taps > 0 && Cin != 1) || (int64_t)B * H * W >= (1ll << 31)) return -2;
   const int64_t M = (int64_t)B * H * W;
-  int blocks = (int)std::min<int64_t>((M + 255) / 256, 2048);
+  // one pixel per thread (no grid-stride second round: the idx -> X -> store chain is latency-bound)
+  int blocks = (int)std::min<int64_t>((M + 255) / 256, 65535);
   hipLaunchKernelGGL(gather_batch_kernel, dim3(blocks), dim3(256), 0, st, X, idx, lab, lab_w, out, lab_out, B, Cin, H, W,
                      taps, off);
   return (int)hipGetLastError();
