@@ -369,7 +369,8 @@ class ConvLayer:
     # convs batched into one launch (csrc/conv.hip conv_wgrad_batched_kernel) the grid no longer has to
     # be filled by one conv's splits, and each extra split costs a full Npad x Kpad slab read in the
     # finalize (Model C: ~0.9 GB/step of slab traffic with grid-filling splits)
-    MIN_SPLIT_PX = 1024
+    # (MDA_MIN_SPLIT_PX: 512 / 2048 / 4096 measured within noise on A, C 7.10k at 1024 vs 6.83k at 2048)
+    MIN_SPLIT_PX = int(__import__("os").environ.get("MDA_MIN_SPLIT_PX", "1024"))
 
     def wgrad_valid(self, cfg: int) -> bool:
         """The K tiles of ``cfg`` cover this conv's padded reduction exactly (patch configs: a 3x3 / s1 /
