@@ -287,7 +287,9 @@ void pool3(int is_max, int backward, int64_t stream, py::dict d) {
   a.dx = P<float>(d, "dx"); a.lddx = (int)I(d, "lddx");
   a.B = (int)I(d, "B"); a.H = (int)I(d, "H"); a.W = (int)I(d, "W"); a.C = (int)I(d, "C");
   a.Ho = (int)I(d, "Ho"); a.Wo = (int)I(d, "Wo");
+  a.am = P<uint8_t>(d, "am");
   if (a.C % 8) throw std::runtime_error("pool3: C % 8");
+  if (a.am && !is_max) throw std::runtime_error("pool3: argmax only for max pooling");
   check(launch_pool3(is_max, backward, a, S(stream)), "pool3");
 }
 

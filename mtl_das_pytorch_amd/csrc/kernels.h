@@ -160,6 +160,8 @@ struct PoolArgs {
   GradSrcs g;                   // backward: grad of output = sum of fp32 sources (concat consumers)
   float* dx; int lddx;          // backward: grad of input (fp32)
   int B, H, W, C, Ho, Wo;
+  uint8_t* am;                  // optional max-pool argmax (window position 0..8) [B*Ho*Wo][C]: written by
+                                // the training forward, read by the backward instead of re-reading the windows
 };
 
 struct OptSeg {

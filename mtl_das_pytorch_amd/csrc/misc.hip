@@ -70,8 +70,9 @@ __global__ __launch_bounds__(256) void pool3_fwd_kernel(PoolArgs a) {
     const int r = (int)(p - (int64_t)b * a.Ho * a.Wo);
     const int oh = r / a.Wo, ow = r - oh * a.Wo;
     float acc[8];
+    int am[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = MAX ? -INFINITY : 0.f;
+    for (int j = 0; j < 8; ++j) { acc[j] = MAX ? -INFINITY : 0.f; am[j] = 0; }
     const int s = MAX ? 2 : 1, pd = MAX ? 0 : 1;
     for (int kh = 0; kh < 3; ++kh) {
       const int ih = oh * s - pd + kh;
@@ -82,8 +83,17 @@ __global__ __launch_bounds__(256) void pool3_fwd_kernel(PoolArgs a) {
         float v[8];
         load8(a.x + ((int64_t)(b * a.H + ih) * a.W + iw) * a.ldx + cg * 8, v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = MAX ? fmaxf(acc[j], v[j]) : acc[j] + v[j];
+        for (int j = 0; j < 8; ++j) {
+          if (MAX && v[j] > acc[j]) am[j] = kh * 3 + kw;  // first max in row-major order (torch)
+          acc[j] = MAX ? fmaxf(acc[j], v[j]) : acc[j] + v[j];
+        }
       }
+    }
+    if (MAX && a.am) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { lo |= (uint32_t)am[j] << (8 * j); hi |= (uint32_t)am[j + 4] << (8 * j); }
+      *reinterpret_cast<uint2*>(a.am + p * a.C + cg * 8) = make_uint2(lo, hi);
     }
     if (!MAX) {
 #pragma unroll
@@ -113,6 +123,16 @@ __global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {
       for (int oh = oh0; oh <= oh1; ++oh)
         for (int ow = ow0; ow <= ow1; ++ow) {
           if (ih < 2 * oh || ih > 2 * oh + 2 || iw < 2 * ow || iw > 2 * ow + 2) continue;
+          const int me = (ih - 2 * oh) * 3 + (iw - 2 * ow);
+          if (a.am) {  // argmax stored by the forward: one 8-byte load instead of the 9-pixel window
+            const uint2 w = *reinterpret_cast<const uint2*>(a.am + ((int64_t)(b * a.Ho + oh) * a.Wo + ow) * a.C + cg * 8);
+            float g[8];
+            gsum8(a.g, 0, (int64_t)(b * a.Ho + oh) * a.Wo + ow, cg * 8, g);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if ((int)(((j < 4 ? w.x : w.y) >> (8 * (j & 3))) & 255u) == me) acc[j] += g[j];
+            continue;
+          }
           float mx[8];
           int am[8];
 #pragma unroll
@@ -125,7 +145,6 @@ __global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {
               for (int j = 0; j < 8; ++j)
                 if (v[j] > mx[j]) { mx[j] = v[j]; am[j] = kh * 3 + kw; }
             }
-          const int me = (ih - 2 * oh) * 3 + (iw - 2 * ow);
           float g[8];
           gsum8(a.g, 0, (int64_t)(b * a.Ho + oh) * a.Wo + ow, cg * 8, g);
 #pragma unroll

@@ -96,6 +96,12 @@ class Pool:
         if (Ho, Wo, s.C) != (out.act.H, out.act.W, out.act.C):
             raise ValueError("pool output shape mismatch")
         self.dx = new_act(prog.arena, 1, prog.B, s.H, s.W, s.C, torch.float32) if src.needs_grad else None
+        # max pool: the training forward stores each output's window argmax (1 byte) for the backward
+        # (MDA_POOL_ARGMAX=0: the backward re-reads the 3x3 windows instead)
+        import os
+        self.am = None
+        if is_max and self.dx is not None and os.environ.get("MDA_POOL_ARGMAX", "1") == "1":
+            self.am = prog.arena.zeros((prog.B * Ho * Wo * s.C,), torch.uint8)
 
     def _geom(self, B):
         s, o = self.src.act, self.out.act
@@ -103,12 +109,16 @@ class Pool:
 
     def forward(self, prog, ph: Phase, training: bool):
         d = dict(self._geom(prog.B), y=self.out.act.p, ldy=self.out.act.ld)
+        if training and self.am is not None:
+            d["am"] = P(self.am)
         ph.add("pool_fwd", k_pool, self.is_max, 0, d)
 
     def backward(self, prog, ph: Phase):
         if self.dx is None:
             return
         d = dict(self._geom(prog.B), g=grads_of(self.out.grad_sources()), dx=self.dx.p, lddx=self.dx.ld)
+        if self.am is not None:
+            d["am"] = P(self.am)
         ph.add("pool_bwd", k_pool, self.is_max, 1, d)
         self.src.grads.append(self.dx)
 

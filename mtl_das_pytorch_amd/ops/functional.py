@@ -351,22 +351,30 @@ def bn_tail_backward(kind: int, y: torch.Tensor, bn: dict, grads: Sequence[torch
     return dy, side, dy2
 
 
-def pool3(x: torch.Tensor, is_max: bool):
-    """Inception pools on NHWC bf16: max 3x3/s2 (valid) or avg 3x3/s1/p1 (count_include_pad)."""
+def pool3(x: torch.Tensor, is_max: bool, am: Optional[torch.Tensor] = None):
+    """Inception pools on NHWC bf16: max 3x3/s2 (valid) or avg 3x3/s1/p1 (count_include_pad).  ``am``
+    (max only, uint8 [B, Ho, Wo, C]): receives each output's window argmax for :func:`pool3_backward`."""
     B, H, W, C = x.shape
     Ho, Wo = ((H - 3) // 2 + 1, (W - 3) // 2 + 1) if is_max else (H, W)
     y = torch.empty(B, Ho, Wo, C, device=x.device, dtype=torch.bfloat16)
-    lib().pool3(int(is_max), 0, stream(), {"x": ptr(x), "ldx": C, "y": ptr(y), "ldy": C, "B": B, "H": H, "W": W,
-                                            "C": C, "Ho": Ho, "Wo": Wo})
+    d = {"x": ptr(x), "ldx": C, "y": ptr(y), "ldy": C, "B": B, "H": H, "W": W, "C": C, "Ho": Ho, "Wo": Wo}
+    if am is not None:
+        if am.dtype != torch.uint8 or am.numel() != B * Ho * Wo * C:
+            raise ValueError("am must be uint8 with one entry per output element")
+        d["am"] = ptr(am)
+    lib().pool3(int(is_max), 0, stream(), d)
     return y
 
 
-def pool3_backward(x: torch.Tensor, g: torch.Tensor, is_max: bool):
+def pool3_backward(x: torch.Tensor, g: torch.Tensor, is_max: bool, am: Optional[torch.Tensor] = None):
     B, H, W, C = x.shape
     _, Ho, Wo, _ = g.shape
     dx = torch.empty(B, H, W, C, device=x.device, dtype=torch.float32)
-    lib().pool3(int(is_max), 1, stream(), {"x": ptr(x), "ldx": C, "g": ptr(g), "ldg": C, "dx": ptr(dx), "lddx": C,
-                                            "B": B, "H": H, "W": W, "C": C, "Ho": Ho, "Wo": Wo})
+    d = {"x": ptr(x), "ldx": C, "g": ptr(g), "ldg": C, "dx": ptr(dx), "lddx": C, "B": B, "H": H, "W": W, "C": C,
+         "Ho": Ho, "Wo": Wo}
+    if am is not None:
+        d["am"] = ptr(am)
+    lib().pool3(int(is_max), 1, stream(), d)
     return dx
 
 

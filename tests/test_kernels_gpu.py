@@ -386,6 +386,19 @@ def test_inception_pools(fn, is_max):
     ref.backward(go)
     dx = fn.pool3_backward(nhwc(x.detach()).bfloat16(), nhwc(go), is_max)
     assert rel(nchw(dx), x.grad) < 1e-5
+    if is_max:  # argmax stored by the forward: identical gradient (same first-max tie rule), windows not re-read
+        am = torch.full((y.numel(),), 255, dtype=torch.uint8, device="cuda")
+        y2 = fn.pool3(nhwc(x.detach()).bfloat16(), is_max, am=am)
+        assert torch.equal(y2, y) and int(am.max()) <= 8
+        # ties: a constant patch must route the gradient to the first window position, as torch does
+        xt = x.detach().clone()
+        xt[:, :, :6, :6] = 0.5
+        xt.requires_grad_(True)
+        F.max_pool2d(xt, 3, 2).backward(go)
+        fn.pool3(nhwc(xt.detach()).bfloat16(), is_max, am=am)
+        dx2 = fn.pool3_backward(nhwc(xt.detach()).bfloat16(), nhwc(go), is_max, am=am)
+        assert torch.equal(dx2, fn.pool3_backward(nhwc(xt.detach()).bfloat16(), nhwc(go), is_max))
+        assert rel(nchw(dx2), xt.grad) < 1e-5
 
 
 def test_gather_batch(fn):
