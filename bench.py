@@ -42,7 +42,8 @@ def main():
     ap.add_argument("--model", default="MTL", choices=["MTL", "single_distance", "single_event", "multi_classifier"])
     ap.add_argument("--dataset-size", type=int, default=2048, help="synthetic samples resident per GPU")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per step")
-    ap.add_argument("--bucket-mb", type=float, default=0.0)
+    ap.add_argument("--buckets", type=int, default=None,
+                    help="DP gradient buckets overlapped with the backward (default: the model's, 1 on one GPU)")
     ap.add_argument("--no-tune", action="store_true", help="skip per-layer kernel autotuning (cached table only)")
     args = ap.parse_args()
 
@@ -66,6 +67,12 @@ def main():
     joint = args.model == "multi_classifier"
     prog = InceptionProgram(model, args.batch, dev) if joint else MTLProgram(model, args.batch, dev)
     prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world)
+    if hasattr(prog, "set_rng_stream"):  # Model C dropout: an independent mask stream per rank
+        prog.set_rng_stream(0, ctx.rank)
+    # DP: gradient buckets whose all-reduces overlap the rest of the backward (engine/step.py)
+    # (--buckets K on one GPU runs the same split graphs with no-op collectives: measures the split's cost)
+    nb = prog.dp_buckets(world) if args.buckets is None else args.buckets
+    buckets = prog.segment_backward(nb)
     autotune_program(prog, out_path=os.path.join("gpurun_out", "tuned_cfgs.json") if ctx.is_main else None,
                      measure=not args.no_tune)
     f = prog.flat
@@ -73,7 +80,7 @@ def main():
     X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev)
     labels = encode_joint(d, e) if joint else torch.stack([d, e], 1)
     runner = StepRunner(prog, X, labels, use_graph=not args.no_graph,
-                        allreduce=FlatGradAllReducer(ctx, args.bucket_mb) if world > 1 else None)
+                        allreduce=FlatGradAllReducer(ctx) if (world > 1 or len(buckets) > 1) else None)
     runner.set_lr(1e-3 / 1.5)  # reference: lr/1.5 applied at the epoch-0 validation
     sampler = ShardedIndexSampler(args.dataset_size * world, args.batch, ctx, seed=7)
     # indices address this rank's resident shard
@@ -120,6 +127,7 @@ def main():
                                    "event": round(float(m[-1, 1] / m[-1, 2]), 4)}),
         "vs_eager_pytorch_mi355x": round(value / (EAGER_MI355X_PER_GPU * world), 3) if args.model == "MTL" else None,
         "hip_graph": not args.no_graph,
+        "grad_buckets_mb": [round((hi - lo) * 4 / 2 ** 20, 2) for lo, hi in buckets],
         "baseline_note": "vs_baseline divides by BASELINE.md's 176.1 samples/s (reference on CPU, the only "
                          "throughput number it has); vs_eager_pytorch_mi355x divides by the reference-style "
                          "eager fp32 PyTorch step measured on MI355X (4037 samples/s/GPU)",

@@ -137,7 +137,10 @@ __global__ __launch_bounds__(CLS_T) void cls_head_kernel(ClsArgs a) {
   const int b = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   if (tid == 0) s_lab = (int)a.labels[b];
-  const uint32_t seed = a.seed ? (uint32_t)(*a.seed) : 0u;
+  // 64-bit counter: low word = training step, high word = the RNG stream (run seed and DP rank, set by
+  // InceptionProgram.set_rng_stream) -- every rank and every --seed draws its own masks
+  const uint64_t s64 = a.seed ? (uint64_t)(*a.seed) : 0ull;
+  const uint32_t seed = (uint32_t)s64 ^ hash3((uint32_t)(s64 >> 32), 0x632BE5ABu, 0x1B873593u);
   const float keep_scale = a.p_drop > 0.f ? 1.f / (1.f - a.p_drop) : 1.f;
   float f[CLS_CPT], msk[CLS_CPT], w[CLS_NC][CLS_CPT];
 #pragma unroll

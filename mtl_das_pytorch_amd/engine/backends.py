@@ -168,11 +168,22 @@ class TorchBackend(Backend):
         average_(self.ctx, [b for n, b in self.model.named_buffers() if b.is_floating_point()])
 
     def optimizer_state(self) -> dict:
-        return {"torch_adam": self.opt.state_dict()}
+        names = {id(p): n for n, p in self.model.named_parameters()}
+        moments, step = {}, 0.0
+        for p in self.model.parameters():
+            s = self.opt.state.get(p)
+            if s:
+                moments[names[id(p)]] = (s["exp_avg"].detach().cpu().clone(), s["exp_avg_sq"].detach().cpu().clone())
+                step = float(s["step"])
+        return {"adam_by_name": moments, "adam_step": step}
 
     def load_optimizer_state(self, st: dict):
-        if "torch_adam" in st:
-            self.opt.load_state_dict(st["torch_adam"])
+        moments, step = portable_adam_state(st, self.model)
+        for n, p in self.model.named_parameters():
+            if n in moments:
+                m, v = moments[n]
+                self.opt.state[p] = {"step": torch.tensor(step), "exp_avg": m.to(p.device).view_as(p).clone(),
+                                     "exp_avg_sq": v.to(p.device).view_as(p).clone()}
 
 
 class EngineBackend(Backend):
@@ -181,7 +192,7 @@ class EngineBackend(Backend):
     def __init__(self, model: nn.Module, model_type: str, X: torch.Tensor, labels: torch.Tensor,
                  X_eval: torch.Tensor, labels_eval: torch.Tensor, ctx: DistContext, batch: int, lr: float,
                  weight_decay: float, loss_weights: Sequence[float] = (1.0, 1.0), use_graph: bool = True,
-                 tune: bool = False):
+                 tune: bool = False, seed: int = 0):
         from .inception import InceptionProgram
         from .mtl import MTLProgram
         from .step import StepRunner
@@ -195,6 +206,9 @@ class EngineBackend(Backend):
             w = list(loss_weights) if model_type == "MTL" else [1.0]
             self.prog = MTLProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), loss_weights=w)
         self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world)
+        if hasattr(self.prog, "set_rng_stream"):
+            self.prog.set_rng_stream(seed, ctx.rank)
+        self.prog.segment_backward(self.prog.dp_buckets(ctx.world))
         autotune_program(self.prog, measure=tune)
         f = self.prog.flat
         broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
@@ -244,21 +258,48 @@ class EngineBackend(Backend):
 
     def optimizer_state(self) -> dict:
         f = self.prog.flat
-        return {"engine_adam": {"exp_avg": f.exp_avg.detach().cpu().clone(),
-                                "exp_avg_sq": f.exp_avg_sq.detach().cpu().clone(),
-                                "step": float(f.step.item())}}
+        moments = {}
+        for n, p in self.prog.model.named_parameters():
+            o = f.off(p)
+            moments[n] = (f.exp_avg[o:o + p.numel()].detach().cpu().clone().view_as(p),
+                          f.exp_avg_sq[o:o + p.numel()].detach().cpu().clone().view_as(p))
+        st = {"adam_by_name": moments, "adam_step": float(f.step.item())}
+        if hasattr(self.prog, "seed"):  # Model C's dropout RNG counter (stream + step)
+            st["dropout_counter"] = int(self.prog.seed.item())
+        return st
 
     def load_optimizer_state(self, st: dict):
-        if "engine_adam" in st:
-            f = self.prog.flat
-            s = st["engine_adam"]
-            f.exp_avg.copy_(s["exp_avg"].to(f.exp_avg.device))
-            f.exp_avg_sq.copy_(s["exp_avg_sq"].to(f.exp_avg_sq.device))
-            f.step.fill_(s["step"])
+        f = self.prog.flat
+        moments, step = portable_adam_state(st, self.prog.model)
+        for n, p in self.prog.model.named_parameters():
+            if n in moments:
+                o = f.off(p)
+                f.exp_avg[o:o + p.numel()].copy_(moments[n][0].reshape(-1))
+                f.exp_avg_sq[o:o + p.numel()].copy_(moments[n][1].reshape(-1))
+        f.step.fill_(step)
+        if "dropout_counter" in st and hasattr(self.prog, "seed"):
+            # keep this rank's stream (high word), continue the saved step count (low word)
+            cur = int(self.prog.seed.item())
+            self.prog.seed.fill_((cur & ~0xFFFFFFFF) | (int(st["dropout_counter"]) & 0xFFFFFFFF))
 
     def after_load(self):
         """Re-pack bf16 weight images after the fp32 masters were overwritten (checkpoint load)."""
         self.runner.pack_weights()
+
+
+def portable_adam_state(st: dict, model: nn.Module):
+    """Adam moments keyed by parameter name + the step count, from a resume sidecar written by either
+    backend (so an engine run resumes under --dtype fp32 and vice versa).  Raises when the sidecar holds no
+    optimizer state this model can use, instead of silently restarting the moments."""
+    names = [n for n, _ in model.named_parameters()]
+    if "adam_by_name" in st:
+        moments, step = st["adam_by_name"], float(st["adam_step"])
+    else:
+        raise ValueError(f"resume sidecar has no portable Adam state (keys: {sorted(st)})")
+    missing = [n for n in names if n not in moments]
+    if missing and moments:
+        raise ValueError(f"resume sidecar lacks Adam moments for {len(missing)} parameters, e.g. {missing[:3]}")
+    return moments, step
 
 
 def reduce_metrics(ctx: DistContext, m: Metrics) -> Metrics:

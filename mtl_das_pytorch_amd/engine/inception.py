@@ -127,6 +127,9 @@ class InceptionProgram(LoweredProgram):
     """Static train/eval programs of a :class:`Multi_Classifier` for a fixed per-GPU batch size."""
 
     label_width = 1  # joint label (distance + 16 * event)
+    # DP: 4 buckets of ~22 MB cut at Inception-block boundaries (fc+Mixed_7c, 7b, 7a-6c, the rest); the
+    # first three all-reduces overlap the remaining blocks' backward
+    default_buckets = 4
 
     def __init__(self, model: Multi_Classifier, batch: int, device, in_hw=(100, 250), p_drop: float = 0.5):
         if model.aux_logits:
@@ -283,6 +286,12 @@ class InceptionProgram(LoweredProgram):
         self.convs: List[ConvLayer] = [op.conv for op in self.ops if isinstance(op, CBR)]
         self._plan_nol()
 
+    def set_rng_stream(self, seed: int, rank: int = 0):
+        """Select the dropout RNG stream (high word of the device counter; the low word counts training
+        steps): masks differ across DP ranks and across --seed values, as torch's per-sample dropout does."""
+        stream = (int(seed) * 1000003 + int(rank) * 7919 + 1) & 0x7FFFFFFF
+        self.seed.fill_(stream << 32)
+
     def _plan_nol(self):
         """Normalise-on-load: a BasicConv2d output consumed by exactly one other BasicConv2d (and not a
         slice of a block's concat buffer) is never materialised -- the consumer reads the producer's
@@ -331,6 +340,7 @@ class InceptionProgram(LoweredProgram):
         Returns the side-stream events the caller's next stream-0 launch must wait for.  With
         MDA_STREAMS=0 the annotations are inert and the ops run in list order."""
         owed0: List[str] = []       # last block's side-stream end events (joined at the next fork)
+        self._block_fork = getattr(self, "_block_fork", {})
         cur_block, used = None, set()
 
         def close_block():
@@ -358,6 +368,7 @@ class InceptionProgram(LoweredProgram):
                 cur_block = blk
                 ph.cur_stream = 0
                 ph.fork_point(f"{ph.name}_f{blk}", waits=owed0)
+                self._block_fork[(ph.name, blk)] = ph.launches[-1]
                 owed0 = []
             st = meta[1] % 4
             ph.cur_stream = st
@@ -376,6 +387,23 @@ class InceptionProgram(LoweredProgram):
         owed = self._emit_streamed(ph, range(len(self.ops)), lambda op: op.forward(self, ph, training))
         ph.add("cls_head", k_cls_head, self._head_args(training), waits=owed)
         return ph
+
+    def bucket_cut_candidates(self) -> List[tuple]:
+        """A cut before each Inception block's backward (its fork point, where the later blocks' streams
+        have joined): the fc layer and every later block are complete, i.e. the flat range from that
+        block's successor's first parameter to the end (module order = flat order = forward order)."""
+        f, m = self.flat, self.model
+        out = []
+        for b in range(len(m.mixed) - 1, 0, -1):
+            done = [p for blk in list(m.mixed)[b:] for p in blk.parameters()] + list(m.fc.parameters())
+            lo = min(f.off(p) for p in done)
+            ids = {id(p) for p in done}
+            if any(f.off(p) >= lo for p in m.parameters() if id(p) not in ids):
+                raise ValueError("Inception parameters are not in forward order in the flat buffer")
+            anchor = self._block_fork.get(("backward", b - 1))
+            if anchor is not None:
+                out.append((anchor, lo, f.numel))
+        return out
 
     def _emit_backward(self) -> Phase:
         ph = Phase("backward")

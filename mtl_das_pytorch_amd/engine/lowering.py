@@ -37,6 +37,32 @@ def _refers_to(args, ptr: int) -> bool:
     return isinstance(args, int) and not isinstance(args, bool) and args == ptr
 
 
+_GRAD_KEYS = ("dgamma", "dbeta", "dgamma2", "dbeta2", "dW", "db")
+
+
+def _grad_offsets(l, gbase: int, numel: int) -> List[int]:
+    """Flat-gradient element offsets a launch writes directly (BN affine parameters of every group, the
+    fc layer), found in its argument tree; conv weights are written by the finalize and not listed."""
+    G = l.args[1] if l.name.startswith("tailbwd") else (l.args[2] if l.name.startswith("conv_") else 1)
+    out = []
+
+    def walk(d):
+        if isinstance(d, dict):
+            pgs = d.get("pgs", 0)
+            for k in _GRAD_KEYS:
+                v = d.get(k)
+                if isinstance(v, int) and not isinstance(v, bool) and gbase <= v < gbase + 4 * numel:
+                    out.extend((v - gbase) // 4 + g * pgs for g in range(G))
+            for v in d.values():
+                walk(v)
+        elif isinstance(d, (list, tuple)):
+            for v in d:
+                walk(v)
+
+    walk(l.args)
+    return out
+
+
 def _blocks(M: int, C: int, cap: int = 1024, per_thread: int = 4) -> int:
     cg = max(1, C // 8)
     pl = max(1, 256 // cg)
@@ -49,6 +75,11 @@ class LoweredProgram:
     packing descriptor tables) and ``self.label_width`` the columns of the stored label tensor."""
 
     label_width = 2
+    default_buckets = 1  # gradient buckets under data parallelism (segment_backward); MDA_BUCKETS overrides
+
+    def dp_buckets(self, world: int) -> int:
+        import os
+        return 1 if world <= 1 else int(os.environ.get("MDA_BUCKETS", str(self.default_buckets)))
 
     # -------------------------------------------------------------------------------------------
     def _tail(self, ph: Phase, kind: int, G: int, y: Act, bn: BNLayer, out: Act, training: bool, r: Act = None,
@@ -234,15 +265,115 @@ class LoweredProgram:
                self.W0, *self.stem_pack)
         return ph
 
-    def _wgfin_args(self):
-        self.wgfin_table, nd, nblocks = build_wgfin_table([c.finalize_desc() for c in self.convs], self.device)
-        return self.wgfin_table, nd, nblocks
+    def _wgfin_args(self, convs=None):
+        t, nd, nblocks = build_wgfin_table([c.finalize_desc() for c in (self.convs if convs is None else convs)],
+                                           self.device)
+        if convs is None:
+            self.wgfin_table = t
+        self._fin_tables = getattr(self, "_fin_tables", {})
+        self._fin_tables[id(convs)] = t  # keep the device table alive for the captured graphs
+        return t, nd, nblocks
 
     def refresh_wgrad_finalize(self):
-        """Rebuild the finalize descriptor table after wgrad configs (split counts) changed."""
+        """Rebuild the finalize descriptor table(s) after wgrad configs (split counts) changed.  A finalize
+        launch's ``owner`` lists the convs it reduces (a gradient bucket's); None means every conv."""
         for l in self.bwd.launches:
             if l.name == "wgrad_finalize":
-                l.args = self._wgfin_args()
+                l.args = self._wgfin_args(l.owner)
+
+    # ---- gradient buckets (data parallelism, SURVEY 5.8 / C2) ---------------------------------------
+    def bucket_cut_candidates(self) -> List[tuple]:
+        """Points of the backward where a gradient bucket could end: ``(anchor, lo, hi)`` means that
+        cutting the backward right before launch ``anchor`` completes the gradients of the flat range
+        [lo, hi) (cumulative, in backward order; every later launch writes gradients outside it).
+        Subclasses override; the default offers none (one bucket)."""
+        return []
+
+    def segment_backward(self, n_buckets: int) -> List[tuple]:
+        """Split the flat gradient into up to ``n_buckets`` contiguous buckets that complete one after the
+        other during the backward, and cut the backward phase accordingly.
+
+        Bucket k's weight gradients (batched per stream by batch_wgrads) and its finalize run at the end of
+        backward piece k; the DP step (engine/step.py) replays piece k, issues bucket k's RCCL all-reduce
+        on the communication stream and replays piece k+1 meanwhile, so all but the last bucket's
+        all-reduce overlap the rest of the backward.  Cuts are chosen among bucket_cut_candidates so that
+        the buckets have about equal size.  Must run before autotune_program (which batches the weight
+        gradients).  Returns the buckets [(lo, hi)] in completion order."""
+        f = self.flat
+        self.buckets = [(0, f.numel)]
+        if n_buckets <= 1 or any(l.name == "cut" for l in self.bwd.launches):
+            return self.buckets
+        ls = self.bwd.launches
+        cands = [c for c in self.bucket_cut_candidates() if 0 < c[2] - c[1] < f.numel]
+        chosen, start = [], 0
+        for k in range(1, n_buckets):
+            target = k * f.numel / n_buckets
+            best = None
+            for j in range(start, len(cands)):
+                if best is None or abs((cands[j][2] - cands[j][1]) - target) < abs(
+                        (cands[best][2] - cands[best][1]) - target):
+                    best = j
+            if best is None:
+                break
+            chosen.append(cands[best])
+            start = best + 1
+        if not chosen:
+            return self.buckets
+        buckets, prev = [], None
+        for _, lo, hi in chosen + [(None, 0, f.numel)]:
+            if prev is None:
+                b = (lo, hi)
+            elif lo == prev[0] and hi >= prev[1]:
+                b = (prev[1], hi)
+            elif hi == prev[1] and lo <= prev[0]:
+                b = (lo, prev[0])
+            else:
+                raise ValueError(f"bucket ranges are not nested intervals: {prev} then {(lo, hi)}")
+            if b[1] > b[0]:
+                buckets.append(b)
+            prev = (lo, hi)
+        bucket_of = lambda off: next(i for i, (lo, hi) in enumerate(buckets) if lo <= off < hi)  # noqa: E731
+        anchors = [next(i for i, l in enumerate(ls) if l is a) for a, _, _ in chosen]
+        if anchors != sorted(anchors):
+            raise ValueError("bucket cut anchors out of backward order")
+        seg_of = lambda i: sum(1 for a in anchors if a <= i)  # noqa: E731
+        fin = next(i for i, l in enumerate(ls) if l.name == "wgrad_finalize")
+        if fin != len(ls) - 1:
+            raise ValueError("the weight-gradient finalize must be the backward's last launch")
+        # every gradient writer must run no later than its bucket's piece
+        gbase = P(f.grads)
+        for i, l in enumerate(ls[:fin]):
+            seg = seg_of(i)
+            if l.name == "conv_wgrad":
+                bs = {bucket_of(f.off(m.weight)) for m in l.owner.mods}
+                if len(bs) != 1 or seg > min(bs):
+                    raise ValueError(f"weight gradient of a bucket-{bs} conv runs in backward piece {seg}")
+                l.bucket = bs.pop()
+            for off in _grad_offsets(l, gbase, f.numel):
+                if seg > bucket_of(off):
+                    raise ValueError(f"{l.name} writes bucket {bucket_of(off)} gradients in piece {seg}")
+        # cut markers + one finalize per bucket at the end of its piece (waiting for the piece's streams)
+        new, bounds = [], anchors + [fin]
+        for k in range(len(buckets)):
+            lo_i = 0 if k == 0 else bounds[k - 1]
+            piece = ls[lo_i:bounds[k]]
+            waits = []
+            for st in sorted({l.stream for l in piece} - {0}):
+                last = [l for l in piece if l.stream == st][-1]
+                if last.record is None:
+                    last.record = f"bwd_piece{k}_s{st}"
+                waits.append(last.record)
+            convs = [c for c in self.convs if bucket_of(f.off(c.mods[0].weight)) == k]
+            if not convs:
+                raise ValueError(f"gradient bucket {k} holds no conv weights")
+            new += piece
+            new.append(Launch("wgrad_finalize", k_wgfin, *self._wgfin_args(convs), owner=convs, waits=waits,
+                              bucket=k))
+            if k < len(buckets) - 1:
+                new.append(Launch("cut", None))
+        self.bwd.launches = new
+        self.buckets = buckets
+        return buckets
 
     def merge_wgrad_cfgs(self, max_batches: Optional[int] = None) -> int:
         """Cap the number of distinct weight-gradient tile configs per stream (= batched launches, which run
@@ -256,8 +387,9 @@ class LoweredProgram:
             max_batches = int(os.environ.get("MDA_WGRAD_MAXB", "3"))
         wg = [l for l in self.bwd.launches if l.name == "conv_wgrad" and l.owner is not None]
         moved = 0
-        for st in sorted({l.stream for l in wg}):
-            mine = [l for l in wg if l.stream == st and not l.args[2].get("aol")]
+        # one batch set per (gradient bucket, stream): a segmented backward batches each bucket separately
+        for bk, st in sorted({(l.bucket, l.stream) for l in wg}):
+            mine = [l for l in wg if l.stream == st and l.bucket == bk and not l.args[2].get("aol")]
             while True:
                 groups = {}
                 for l in mine:
@@ -290,6 +422,8 @@ class LoweredProgram:
         wg = [l for l in ls if l.name == "conv_wgrad"]
         if not wg:
             return
+        if any(l.name == "cut" for l in ls):
+            return self._batch_wgrads_segmented()
         fin = next(i for i, l in enumerate(ls) if l.name == "wgrad_finalize")
         keep = []
         anchor_of = {}  # stream-0 wgrad -> the last kept stream-0 launch before it (its dy producer)
@@ -368,6 +502,71 @@ class LoweredProgram:
             fin_l.args = (t, nd, nb)
             fin_l.waits = ()
         self.bwd.launches = keep + ls[fin:]
+        self.wgrads_batched = True
+
+    def _batch_wgrads_segmented(self):
+        """batch_wgrads for a backward cut into gradient-bucket pieces (segment_backward): in every piece,
+        the weight gradients of that piece's bucket are batched per (stream, tile config) after the
+        stream's last launch of the piece (a stream without launches there uses stream 0), and the piece's
+        finalize waits for those batches.  Weight gradients of a later bucket whose launches sat in an
+        earlier piece move to their bucket's piece (their dy is complete by then)."""
+        ls = self.bwd.launches
+        pieces, cur = [], []
+        for l in ls:
+            if l.name == "cut":
+                pieces.append(cur)
+                cur = []
+            else:
+                cur.append(l)
+        pieces.append(cur)
+        by_bucket: Dict[int, List[Launch]] = {}
+        kept_pieces = []
+        for piece in pieces:
+            keep = []
+            for l in piece:
+                if l.name != "conv_wgrad":
+                    keep.append(l)
+                    continue
+                by_bucket.setdefault(l.bucket, []).append(l)
+                if l.record is not None:  # the event now stands for the stream's previous kept launch
+                    prev = next((k for k in reversed(keep) if k.stream == l.stream), None)
+                    if prev is None:
+                        raise RuntimeError(f"cannot re-anchor event {l.record}")
+                    if prev.record is None:
+                        prev.record = l.record
+                    else:
+                        self.bwd.alias[l.record] = prev.record
+            kept_pieces.append(keep)
+        self.wgrad_tables = []
+        key_of = lambda l: l.args[0] + (WGRAD_AOL_CFG if l.args[2].get("aol") else 0)  # noqa: E731
+        out = []
+        for k, keep in enumerate(kept_pieces):
+            fin = keep.pop()  # segment_backward put the bucket's finalize last in its piece
+            assert fin.name == "wgrad_finalize" and fin.bucket == k, fin.name
+            mine = by_bucket.get(k, [])
+            streams_here = {l.stream for l in keep}
+            for l in mine:
+                if l.stream not in streams_here:
+                    l.stream = 0
+            tags = []
+            for st in sorted({l.stream for l in mine}):
+                batched = []
+                for key in sorted({key_of(l) for l in mine if l.stream == st}):
+                    group = [l for l in mine if l.stream == st and key_of(l) == key]
+                    raw, nblocks = lib().wgrad_table(key, [l.args[2] for l in group], [l.args[1] for l in group])
+                    table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+                    self.wgrad_tables.append(table)
+                    batched.append(Launch("wgrad_batched", k_wgrad_batched, key, table, len(group), nblocks,
+                                          stream=st, bucket=k))
+                batched[-1].record = f"wgrads_b{k}_s{st}"
+                tags.append(batched[-1].record)
+                pos = max((i for i, l in enumerate(keep) if l.stream == st), default=len(keep) - 1) + 1
+                keep[pos:pos] = batched
+            fin.waits = tuple(fin.waits) + tuple(tags)
+            out += keep + [fin]
+            if k < len(kept_pieces) - 1:
+                out.append(Launch("cut", None))
+        self.bwd.launches = out
         self.wgrads_batched = True
 
     STAGE_STREAM = 2

@@ -35,6 +35,10 @@ from .program import Phase, k_head, k_wgfin
 class MTLProgram(LoweredProgram):
     """Static train/eval programs of an :class:`MTLNet` for a fixed per-GPU batch size."""
 
+    # DP: the task-branch gradients (38% of the 4.5 MB buffer) are all-reduced while RB1, the stem and
+    # the backbone's weight gradients still run; the backbone bucket follows (bucket_cut_candidates)
+    default_buckets = 2
+
     def __init__(self, model: MTLNet, batch: int, device, in_hw=(100, 250), loss_weights: Optional[Sequence[float]] = None):
         self.model = model
         self.B = B = batch
@@ -223,6 +227,24 @@ class MTLProgram(LoweredProgram):
         ph.add("mtl_head", k_head, hd)
         return ph
 
+    def bucket_cut_candidates(self) -> List[tuple]:
+        """One cut: right before residual block 1's backward, every task-branch (level) gradient is
+        complete -- the level parameters lead the flat buffer (FlatState param_groups), so they form the
+        first bucket and its all-reduce overlaps RB1, conv1 and the backbone's weight gradients."""
+        f = self.flat
+        lv = [p for c in self.convs if c not in self._backbone_convs() for m in c.mods for p in m.parameters()]
+        lv += [p for L in self.levels for k in ("bn0", "bn3", "bno") if k in L for m in L[k].mods
+               for p in m.parameters()]
+        hi = max(f.off(p) + p.numel() for p in lv)
+        hi = (hi + 3) // 4 * 4
+        rest = [p for p in self.model.parameters() if all(p is not q for q in lv)]
+        if any(f.off(p) < hi for p in rest) or min(f.off(p) for p in lv) != 0:
+            raise ValueError("task-branch parameters do not lead the flat buffer")
+        return [(self._rb1_anchor, 0, hi)]
+
+    def _backbone_convs(self) -> list:
+        return [self.conv1] + [L[k] for L in self.rbs for k in ("ca", "cb", "cs") if k in L]
+
     def _emit_backward(self) -> Phase:
         ph = Phase("backward")
         T, lv = self.T, self.levels
@@ -270,6 +292,8 @@ class MTLProgram(LoweredProgram):
         for i in range(7, -1, -1):
             R = self.rbs[i]
             g = sources(i + 1)
+            if i == 0:  # bucket cut candidate: every task-branch gradient is complete before RB1's backward
+                self._rb1_bwd_first = len(ph.launches)
             # F_{i+1}'s task-branch gradients: for F_{2l+2} (i odd) the mask-target gradient dF, ready right
             # after the level's sigmoid-mask backward; for F_{2l+1} the concat gradient of the whole level
             ph.pending_waits.append(f"dF{i // 2}" if i % 2 == 1 else f"lvl{i // 2}")
@@ -288,6 +312,7 @@ class MTLProgram(LoweredProgram):
         self.dy0 = new_act(self.arena, 1, self.B, self.y0.H, self.y0.W, self.y0.C)
         self._tail_bwd(ph, ACT_RELU, 1, self.y0, self.bn1, sources(0), self.dy0)
         self._conv_bwd(ph, self.conv1, src_dict(self.xin), self.dy0, None)
+        self._rb1_anchor = ph.launches[self._rb1_bwd_first]
         # weight-gradient slabs -> flat fp32 gradients (one launch for every conv), after all wgrads
         ph.launches[self._last_wgrad].record = "wgrads"
         ph.add("wgrad_finalize", k_wgfin, *self._wgfin_args(), waits=("wgrads",))

@@ -29,10 +29,12 @@ MAX_STREAMS = max(1, min(4, int(os.environ.get("MDA_MAX_STREAMS", "4"))))
 
 
 class Launch:
-    __slots__ = ("name", "fn", "args", "owner", "stream", "waits", "record")
+    __slots__ = ("name", "fn", "args", "owner", "stream", "waits", "record", "bucket")
 
-    def __init__(self, name: str, fn: Callable, *args, owner=None, stream: int = 0, waits=(), record=None):
+    def __init__(self, name: str, fn: Callable, *args, owner=None, stream: int = 0, waits=(), record=None,
+                 bucket: int = 0):
         self.name = name
+        self.bucket = bucket  # gradient bucket whose finalize this launch feeds (segmented backward, DP)
         self.fn = fn
         self.args = args
         self.owner = owner  # the layer object that emitted it (used by the autotuner)
@@ -108,6 +110,35 @@ class Phase:
 
     def __len__(self):
         return len(self.launches)
+
+    def split(self) -> List["Phase"]:
+        """Cut the phase at its pseudo-launches named ``cut`` into consecutive phases.
+
+        Each piece is run (or captured) on its own: its side streams fork from stream 0 at its start and
+        are joined back at its end, so an event recorded in an earlier piece is already ordered before
+        the later one -- such waits are dropped.  Used to end the backward at gradient-bucket boundaries
+        (DP: a bucket's all-reduce is issued between two pieces and overlaps the next one)."""
+        pieces, cur = [], []
+        for l in self.launches:
+            if l.name == "cut":
+                pieces.append(cur)
+                cur = []
+            else:
+                cur.append(l)
+        pieces.append(cur)
+        out, recorded = [], set()
+        for i, ls in enumerate(pieces):
+            ph = Phase(f"{self.name}_{i}")
+            ph.alias = dict(self.alias)
+            for l in ls:
+                w = tuple(t for t in l.waits if self.alias.get(t, t) not in recorded)
+                ph.launches.append(Launch(l.name, l.fn, *l.args, owner=l.owner, stream=l.stream, waits=w,
+                                          record=l.record, bucket=l.bucket))
+            for l in ls:
+                if l.record is not None:
+                    recorded.add(l.record)
+            out.append(ph)
+        return out
 
 
 # thin adapters giving every launch the signature fn(*args, stream)

@@ -3,12 +3,15 @@
 A training step is
 
     [memset zeroed arena] [gather batch] [forward] [backward]  ->  (DP: RCCL all-reduce of the flat
-    gradient bucket)  ->  [fused Adam + bf16 re-pack] [step++]
+    gradient buckets)  ->  [fused Adam + bf16 re-pack] [step++]
 
 Single GPU: the whole step is ONE captured HIP graph (``torch.cuda.CUDAGraph`` is a hipGraph on ROCm),
-so a step costs one graph launch from the host.  Data parallel: the all-reduce sits between two graphs
-(compute graph, optimizer graph) so RCCL runs eagerly on the same stream -- no reliance on collective
-capture -- and its ~4.5 MB bucket (Model A) is a single call.
+so a step costs one graph launch from the host.  Data parallel: RCCL runs eagerly between graphs -- no
+reliance on collective capture.  With one bucket the compute graph is followed by one all-reduce and the
+optimizer graph.  With several (LoweredProgram.segment_backward) the backward is captured as one graph
+per bucket piece; after replaying piece k the host issues bucket k's all-reduce asynchronously (RCCL's
+stream waits for piece k) and replays piece k+1, which then runs concurrently with the collective; the
+optimizer graph waits for every bucket.
 
 The batch indices live in a persistent device buffer that the host refreshes (device-to-device copy)
 before each replay; the learning rate is a device scalar, so the reference's LR schedule never forces
@@ -49,6 +52,8 @@ class StepRunner:
             self.sources["eval"] = (X_eval, labels_eval)
         self.graphs: Dict[str, torch.cuda.CUDAGraph] = {}
         self._packed = False
+        self._bwd_pieces = None
+        self.buckets = list(getattr(program, "buckets", None) or [(0, program.flat.numel)])
 
     # -------------------------------------------------------------------------------------------
     def _mutable_state(self) -> List[torch.Tensor]:
@@ -61,10 +66,20 @@ class StepRunner:
         self.p.opt["pack"].run()
         self._packed = True
 
+    def _pieces(self):
+        """The backward cut at its gradient-bucket boundaries (LoweredProgram.segment_backward)."""
+        if self._bwd_pieces is None:
+            self._bwd_pieces = self.p.bwd.split()
+        return self._bwd_pieces
+
     def _phases(self, kind: str) -> List[Callable[[], None]]:
         p = self.p
         X, lab = self.sources["train" if kind.startswith("train") else "eval"]
         gather = p.gather_phase(X, lab, self.idx)
+        if kind.startswith("train_piece"):
+            k = int(kind[len("train_piece"):])
+            pieces = self._pieces()
+            return ([p.arena.clear, gather.run, p.fwd_train.run] if k == 0 else []) + [pieces[k].run]
         if kind == "train_compute":
             return [p.arena.clear, gather.run, p.fwd_train.run, p.bwd.run]
         if kind == "train_opt":
@@ -76,13 +91,18 @@ class StepRunner:
         raise ValueError(kind)
 
     def _run(self, kind: str):
-        fns = self._phases(kind)
         if not self.use_graph:
-            for f in fns:
+            for f in self._phases(kind):
                 f()
             return
+        self._ensure_graph(kind)
+        self.graphs[kind].replay()
+
+    def _ensure_graph(self, kind: str):
+        """Warm up (side effects rolled back) and capture the graph of ``kind`` once."""
         g = self.graphs.get(kind)
         if g is None:
+            fns = self._phases(kind)
             snap = StateSnapshot(self._mutable_state())
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -99,7 +119,6 @@ class StepRunner:
                     f()
             torch.cuda.synchronize()
             self.graphs[kind] = g
-        g.replay()
 
     # -------------------------------------------------------------------------------------------
     def set_lr(self, lr: float):
@@ -111,9 +130,22 @@ class StepRunner:
         self.idx.copy_(idx, non_blocking=True)
         if self.allreduce is None:
             self._run("train_full")
-        else:
+        elif len(self.buckets) == 1:
             self._run("train_compute")
             self.allreduce(self.p.flat.grads)
+            self._run("train_opt")
+        else:
+            # piece k completes bucket k: its all-reduce is issued on the communication stream (after the
+            # piece, in stream order) while piece k+1 is replayed -- overlapped with the rest of the backward
+            g = self.p.flat.grads
+            if self.use_graph:  # capture every piece before any collective is in flight (the capture's
+                for k in range(len(self.buckets)):  # state snapshot/restore must not race an all-reduce)
+                    self._ensure_graph(f"train_piece{k}")
+                self._ensure_graph("train_opt")
+            for k, (lo, hi) in enumerate(self.buckets):
+                self._run(f"train_piece{k}")
+                self.allreduce.start(g[lo:hi])
+            self.allreduce.finish()
             self._run("train_opt")
 
     def eval_step(self, idx: torch.Tensor):

@@ -140,7 +140,8 @@ class Trainer:
                   loss_weights=cfg.loss_weights)
         if self.backend_name == "engine":
             self.model.to(self.device)
-            self.backend = EngineBackend(self.model, cfg.model, X, Y, Xv, Yv, use_graph=cfg.graph, tune=cfg.tune, **kw)
+            self.backend = EngineBackend(self.model, cfg.model, X, Y, Xv, Yv, use_graph=cfg.graph, tune=cfg.tune,
+                                         seed=cfg.seed, **kw)
         else:
             if cfg.sync_bn and self.ctx.enabled:
                 self.model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(self.model)

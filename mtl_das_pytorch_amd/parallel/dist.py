@@ -116,6 +116,21 @@ class FlatGradAllReducer:
     def __init__(self, ctx: DistContext, bucket_mb: float = 0.0):
         self.ctx = ctx
         self.bucket_elems = int(bucket_mb * 2 ** 20 / 4) if bucket_mb > 0 else 0
+        self._pending = []
+
+    def start(self, t: torch.Tensor):
+        """Issue an asynchronous all-reduce(SUM) of one gradient bucket (a contiguous view of the flat
+        buffer).  The communication stream waits for the work already queued on the current stream, so
+        the bucket must be complete in stream order; the current stream is free to continue."""
+        if self.ctx.enabled:
+            self._pending.append(dist.all_reduce(t, async_op=True))
+
+    def finish(self):
+        """Make the current stream wait for every bucket issued by ``start`` (no host synchronisation on
+        RCCL: Work.wait() inserts a stream dependency)."""
+        for h in self._pending:
+            h.wait()
+        self._pending = []
 
     def __call__(self, grads: torch.Tensor):
         if not self.ctx.enabled:
