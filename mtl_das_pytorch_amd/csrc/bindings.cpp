@@ -103,7 +103,22 @@ AolArgs parse_aol(const py::dict& o, int C, bool dgrad) {
   return r;
 }
 
+ConvArgs parse_conv(int mode, py::dict d);
+
 void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
+  ConvArgs a = parse_conv(mode, d);
+  check(launch_conv(mode, a, G, cfg, S(stream)), "conv");
+}
+
+// (workspace floats, tickets) an LDS-staged conv config needs for these arguments; raises if invalid
+py::tuple conv_workspace(int mode, int cfg, int G, py::dict d) {
+  ConvArgs a = parse_conv(mode, d);
+  int64_t ws = 0, nt = 0;
+  const int rc = cfg >= CONV_LDS_CFG0 ? conv_lds_workspace(mode, a, G, cfg, ws, nt) : 0;
+  return py::make_tuple(rc, ws, nt);
+}
+
+ConvArgs parse_conv(int mode, py::dict d) {
   ConvArgs a{};
   a.src = parse_src(d["src"].cast<py::dict>());
   a.w = P<const bf16_t>(d, "w");
@@ -143,7 +158,9 @@ void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
     a.ao = parse_aol(d["aol"].cast<py::dict>(), a.Cs, true);
     a.aol = 1;
   }
-  check(launch_conv(mode, a, G, cfg, S(stream)), "conv");
+  a.ws = P<float>(d, "ws");
+  a.cnt = P<unsigned>(d, "cnt");
+  return a;
 }
 
 WgradArgs parse_wgrad(const py::dict& d);
@@ -318,6 +335,9 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.attr("SIZEOF_WGFIN") = (int)sizeof(WgFinDesc);
   m.attr("SIZEOF_OPTSEG") = (int)sizeof(OptSeg);
   m.def("conv", &conv);
+  m.def("conv_workspace", &conv_workspace);
+  m.attr("CONV_LDS_CFG0") = CONV_LDS_CFG0;
+  m.attr("CONV_LDS_NCFG") = CONV_LDS_NCFG;
   m.def("wgrad", &wgrad);
   m.def("wgrad_finalize", &wgrad_finalize);
   m.def("tail_fwd", &tail_fwd);

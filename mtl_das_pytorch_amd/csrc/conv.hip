@@ -900,6 +900,10 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
 }
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
+  if (cfg >= CONV_LDS_CFG0) {  // LDS-staged kernels (conv_lds.hip)
+    const int m = mode == MODE_FWD ? (a.nol ? MODE_FWD_NOL : MODE_FWD) : (a.bpart ? MODE_DGRAD_BNS : MODE_DGRAD);
+    return launch_conv_lds(m, a, G, cfg, st);
+  }
   if (mode == MODE_FWD) return a.nol ? launch_conv_cfg<MODE_FWD_NOL>(a, G, cfg, st) : launch_conv_cfg<MODE_FWD>(a, G, cfg, st);
   if (a.aol)
     return a.bpart ? launch_conv_cfg<MODE_DGRAD_AOL_BNS>(a, G, cfg, st) : launch_conv_cfg<MODE_DGRAD_AOL>(a, G, cfg, st);

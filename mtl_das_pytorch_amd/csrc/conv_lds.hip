@@ -1,0 +1,503 @@
+// LDS-staged implicit-GEMM convolution on gfx950 MFMA (v_mfma_f32_16x16x32_bf16): forward and data
+// gradient, NHWC bf16 operands, fp32 accumulation.  Replaces the same reference ops as conv.hip
+// (every nn.Conv2d of model/modelA_MTL.py, model/modelB_singleTask.py and the Inception blocks of
+// model/modelC_multiClassifier.py, and their autograd grad_input).
+//
+// Why a second conv kernel: conv.hip's conv_igemm loads every wave's MFMA fragments straight from
+// global memory, 32 k at a time, two stages deep.  On Model C's deep layers (M = B*H*W of 192..8960
+// pixels, K = 576..4032) a launch is a chain of ~10-40 dependent load round trips per wave and ran at
+// 25..150 TF/s (profiles/r2_conv_layer_times_before.txt).  Here
+//
+//   * a block's whole K chunk (KC = 64 or 128) of BOTH operands is staged in LDS: 256 threads issue
+//     16-byte loads cooperatively (8 pixels x 128 contiguous bytes per wave instruction: full lines),
+//     the im2col gather / zero padding / normalise-on-load BN+ReLU happens once per element while
+//     storing, and every wave reads its fragments with conflict-free ds_read_b128 -- the tile is read
+//     from global memory once per block instead of once per wave;
+//   * the next chunk's loads are in flight while the MFMAs of the current one run (double-buffered
+//     LDS, one barrier per chunk);
+//   * K is split ACROSS blocks (splits = 1..8): short dependency chains and enough blocks to fill the
+//     256 CUs on small-M layers.  Partial fp32 tiles go to a workspace; the last block to arrive at a
+//     tile (agent-scope release/acquire ticket) sums them in split order -- deterministic -- and runs
+//     the epilogue;
+//   * a stride-2 data gradient is decomposed into its sub-pixel phases (output parities): each phase
+//     reduces over the taps that actually hit a dy element, instead of the gather form's masking of
+//     3/4 of the MFMA work (conv.hip conv_load_stage).
+//
+// LDS image of an operand chunk: [k-group g (8 channels)][row][8 bf16] (16-byte units).  The MFMA
+// fragment read of lane (r = lane & 15, q = lane >> 4) at k-step s is row r, group 4s + q: within a
+// ds_read_b128 lane group the 16 rows are distinct, so each group touches 16 distinct 16-byte slots of
+// a 256-byte bank row (conflict-free).  Staging writes go 8 consecutive lanes -> 8 consecutive rows
+// (one 128-byte ds_write_b128 group, conflict-free); the matching global loads read 8 pixels x 8
+// k-groups = 8 full 128-byte lines per wave instruction.
+//
+// Modes: MODE_FWD, MODE_FWD_NOL (normalise-on-load of the input), MODE_DGRAD, MODE_DGRAD_BNS (fused
+// BN-backward statistics in the epilogue); the epilogues match conv.hip's (bias, bf16 store, fp64
+// replica BN sums / fp32 gradient store, dz statistics).
+#include "kernels.h"
+
+namespace mda {
+
+namespace {
+
+template <int MODE>
+constexpr bool lds_fwd() { return MODE == MODE_FWD || MODE == MODE_FWD_NOL; }
+
+// (BM pixels, BN channels, waves along M, waves along N) of each tile config
+constexpr int LDS_BM[8] = {64, 128, 64, 128, 32, 64, 32, 128};
+constexpr int LDS_BN[8] = {64, 64, 128, 128, 64, 32, 32, 16};
+constexpr int LDS_WAM[8] = {2, 2, 2, 2, 2, 2, 2, 4};
+
+// Field of phase p (wave-uniform) without indexing the by-value kernel argument at run time (a dynamic
+// index would copy the argument struct to scratch memory).
+#define PSEL(f) (p == 0 ? pl.ph[0].f : p == 1 ? pl.ph[1].f : p == 2 ? pl.ph[2].f : pl.ph[3].f)
+
+template <int MODE, int BM, int BN, int WAM, int KC>
+__global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
+  constexpr int WAN = 4 / WAM;
+  constexpr int WM = BM / WAM, WN = BN / WAN, FM = WM / 16, FN = WN / 16;
+  static_assert(FM >= 1 && FN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
+  constexpr int NG = KC / 8, NKS = KC / 32;
+  constexpr int UA = BN * NG, UB = BM * NG;  // 16-byte staging units of a chunk
+  constexpr int NA = (UA + 255) / 256, NB = (UB + 255) / 256;
+  constexpr int BUF = (BN + BM) * KC;       // bf16 elements of one stage buffer
+  constexpr bool NOL = MODE == MODE_FWD_NOL;
+  constexpr bool BNS = MODE == MODE_DGRAD_BNS;
+  constexpr bool FWD = lds_fwd<MODE>();
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* s_buf = reinterpret_cast<bf16_t*>(smem);
+  int* s_tx = reinterpret_cast<int*>(smem + 2 * BUF * 2);  // input coordinates / channel per k-group
+  int* s_tw = s_tx + pl.ntab;                              // weight column per k-group
+  float* s_st = reinterpret_cast<float*>(s_tw + pl.ntab);  // [WAM][BN][2] epilogue sums
+  float* s_k = s_st + WAM * BN * 2;                         // NOL: [2][Cs] / BNS: [4][BN] constants
+  int* s_flag = reinterpret_cast<int*>(s_k + (NOL ? 2 * a.Cs : (BNS ? 4 * BN : 0)));
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, kgl = lane >> 4;
+  const int wn = wid % WAN, wm = wid / WAN;
+  int p = 0;
+#pragma unroll
+  for (int q = 1; q < 4; ++q)
+    if (q < pl.nph && (int)blockIdx.x >= pl.ph[q].m0) p = q;
+  const int oy0 = PSEL(oy0), ox0 = PSEL(ox0), Hq = PSEL(Hq), Wq = PSEL(Wq);
+  const int rh = PSEL(rh), nh = PSEL(nh), rw = PSEL(rw), nw = PSEL(nw), ay = PSEL(ay), ax = PSEL(ax);
+  const int Kp = PSEL(Kp), m0t = PSEL(m0);
+  const int S = pl.splits;
+  const int ntn = (a.N + BN - 1) / BN;
+  const int nt = blockIdx.y / S, split = blockIdx.y - nt * S;
+  const int z = blockIdx.z;
+  const int HWq = Hq * Wq;
+  const int Mq = a.B * HWq;
+  const int mbase = ((int)blockIdx.x - m0t) * BM, nbase = nt * BN;
+  const int nch = Kp / KC;
+  const int cps = (nch + S - 1) / S;
+  const int cb = min(nch, split * cps), ce = min(nch, cb + cps);
+
+  // ---- per-block k-group tables for this split's chunks
+  {
+    const int cs8 = a.Cs >> 3, ntap = nh * nw;
+    const int ng = (ce - cb) * NG;
+    for (int i = tid; i < ng; i += 256) {
+      const int gabs = cb * NG + i;
+      const int t = gabs / cs8;
+      const int c = (gabs - t * cs8) * 8;
+      int ex = 0, ew = -1;
+      if (t < ntap) {
+        const int u = t / nw, v = t - u * nw;
+        const int kh = rh + pl.th * u, kw = rw + pl.tw * v;
+        const int dyo = ay + pl.by * u, dxo = ax + pl.bx * v;
+        const int seg = (a.src.C1 > 0 && c >= a.src.C0) ? 1 : 0;
+        ex = (c - seg * a.src.C0) | ((dyo + 64) << 14) | ((dxo + 64) << 21) | (seg << 28) | (1 << 29);
+        ew = (kh * a.KW + kw) * a.Cs + c;
+      }
+      s_tx[i] = ex;
+      s_tw[i] = ew;
+    }
+  }
+  if (NOL) bn_prepare(a.nbn, z, s_k, s_k + a.Cs, nullptr, nullptr, blockIdx.x == 0 && blockIdx.y == 0);
+  if (BNS) {
+    for (int i = tid; i < BN; i += 256) {
+      const int n = nbase + i;
+      float sc = 0.f, sh = 0.f, mu = 0.f, inv = 0.f;
+      if (n < a.N) bn_channel_bwd(a.bbn, z, n, sc, sh, mu, inv);
+      s_k[i] = sc; s_k[BN + i] = sh; s_k[2 * BN + i] = mu; s_k[3 * BN + i] = inv;
+    }
+  }
+
+  // ---- staging units: unit u -> (row = 8 * (u / (8 NG)) + (u & 7), k-group g = (u >> 3) % NG)
+  const bf16_t* wz = a.w + a.wgs * z;
+  const bf16_t* base0 = a.src.p[0] + a.src.gs[0] * z;
+  const bf16_t* base1 = a.src.p[1] ? a.src.p[1] + a.src.gs[1] * z : base0;
+  const int ld0 = a.src.ld[0], ld1 = a.src.ld[1];
+  int an[NA], aoff[NA];  // weight row (-1: none), LDS offset (16-byte units)
+  int ag[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int u = tid + 256 * j;
+    const int rest = u >> 3, g = rest % NG, row = (rest / NG) * 8 + (u & 7);
+    const int n = nbase + row;
+    an[j] = (u < UA && n < a.Npad) ? n : -1;
+    ag[j] = g;
+    aoff[j] = g * BN + row;
+  }
+  int pb[NB], pih[NB], piw[NB], bg[NB], boff[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int u = tid + 256 * j;
+    const int rest = u >> 3, g = rest % NG, row = (rest / NG) * 8 + (u & 7);
+    const int m = mbase + row;
+    const bool ok = u < UB && m < Mq;
+    const int mm = ok ? m : 0;
+    const int b = mm / HWq, r = mm - b * HWq;
+    const int i = r / Wq, jj = r - i * Wq;
+    pb[j] = ok ? b : -1;
+    pih[j] = i * pl.mh;
+    piw[j] = jj * pl.mw;
+    bg[j] = g;
+    boff[j] = g * BM + row;
+  }
+
+  uint4 ra[NA], rb[NB];
+  uint32_t bok = 0;
+  auto load_chunk = [&](int ch) {
+    const int t0 = (ch - cb) * NG;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int e = s_tw[t0 + ag[j]];
+      ra[j] = (an[j] >= 0 && e >= 0) ? *reinterpret_cast<const uint4*>(wz + (int64_t)an[j] * a.Kpad + e)
+                                      : make_uint4(0, 0, 0, 0);
+    }
+    bok = 0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int e = s_tx[t0 + bg[j]];
+      const int ih = pih[j] + ((e >> 14) & 127) - 64, iw = piw[j] + ((e >> 21) & 127) - 64;
+      const bool ok = ((e >> 29) & 1) && pb[j] >= 0 && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+      rb[j] = make_uint4(0, 0, 0, 0);
+      if (ok) {
+        const int seg = (e >> 28) & 1;
+        const bf16_t* sb = seg ? base1 : base0;
+        rb[j] = *reinterpret_cast<const uint4*>(sb + ((int64_t)(pb[j] * a.Hs + ih) * a.Ws + iw) * (seg ? ld1 : ld0) +
+                                                (e & 16383));
+      }
+      bok |= (uint32_t)ok << j;
+    }
+  };
+  const bool nol_relu = a.nol_kind == ACT_RELU;
+  auto store_chunk = [&](int buf, int ch) {
+    bf16_t* A = s_buf + buf * BUF;
+    bf16_t* B = A + BN * KC;
+#pragma unroll
+    for (int j = 0; j < NA; ++j)
+      if (tid + 256 * j < UA) *reinterpret_cast<uint4*>(A + aoff[j] * 8) = ra[j];
+    const int t0 = (ch - cb) * NG;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (tid + 256 * j >= UB) continue;
+      uint4 v = rb[j];
+      if (NOL && ((bok >> j) & 1)) {  // act(BN(y)) of the producing conv, rounded as its tail would
+        const int c = s_tx[t0 + bg[j]] & 16383;
+        uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          float lo = __uint_as_float(w4[h] << 16) * s_k[c + 2 * h] + s_k[a.Cs + c + 2 * h];
+          float hi = __uint_as_float(w4[h] & 0xffff0000u) * s_k[c + 2 * h + 1] + s_k[a.Cs + c + 2 * h + 1];
+          if (nol_relu) { lo = fmaxf(lo, 0.f); hi = fmaxf(hi, 0.f); }
+          w4[h] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+        }
+        v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+      *reinterpret_cast<uint4*>(B + boff[j] * 8) = v;
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int f = 0; f < FM; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  __syncthreads();  // tables and constants
+  if (cb < ce) {
+    load_chunk(cb);
+    store_chunk(0, cb);
+  }
+  __syncthreads();
+  for (int ch = cb; ch < ce; ++ch) {
+    const int cur = (ch - cb) & 1;
+    if (ch + 1 < ce) load_chunk(ch + 1);  // in flight during this chunk's MFMAs
+    const bf16_t* A = s_buf + cur * BUF;
+    const bf16_t* B = A + BN * KC;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      bf16x8 afr[FN], bfr[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        afr[i] = *reinterpret_cast<const bf16x8*>(A + ((s * 4 + kgl) * BN + wn * WN + i * 16 + l16) * 8);
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+        bfr[f] = *reinterpret_cast<const bf16x8*>(B + ((s * 4 + kgl) * BM + wm * WM + f * 16 + l16) * 8);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int f = 0; f < FM; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], bfr[f], acc[i][f], 0, 0, 0);
+    }
+    if (ch + 1 < ce) store_chunk(cur ^ 1, ch + 1);  // that buffer's last reader finished before the barrier
+    __syncthreads();
+  }
+
+  // ---- cross-block split of K: deterministic last-arriver reduction
+  if (S > 1) {
+    const int64_t tile = ((int64_t)z * gridDim.x + blockIdx.x) * ntn + nt;
+    float4* slab = reinterpret_cast<float4*>(a.ws) + tile * S * (BM * BN / 4);
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+        slab[(int64_t)split * (BM * BN / 4) + ((wid * FN + i) * FM + f) * 64 + lane] =
+            make_float4(acc[i][f][0], acc[i][f][1], acc[i][f][2], acc[i][f][3]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_flag[0] = t == (unsigned)(S - 1);
+    }
+    __syncthreads();
+    if (!s_flag[0]) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reusable next launch
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < S; ++s) {
+          const float4 t = slab[(int64_t)s * (BM * BN / 4) + ((wid * FN + i) * FM + f) * 64 + lane];
+          v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
+        }
+        acc[i][f] = v;
+      }
+  }
+
+  // ---- epilogue (lane: pixel l16 of each fragment, channels 4*kgl .. +3)
+  int orow[FM];
+  bool pv[FM];
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    const int m = mbase + wm * WM + f * 16 + l16;
+    pv[f] = m < Mq;
+    const int mm = pv[f] ? m : 0;
+    const int b = mm / HWq, r = mm - b * HWq;
+    const int i = r / Wq, jj = r - i * Wq;
+    orow[f] = (b * a.Ho + oy0 + i * pl.qy) * a.Wo + ox0 + jj * pl.qx;
+  }
+  const bool want_stats = FWD && a.stats != nullptr;
+  const bool want_red = want_stats || BNS;
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int n0 = nbase + wn * WN + i * 16 + 4 * kgl;
+    const int cl = wn * WN + i * 16 + 4 * kgl;
+    const bool nok = n0 < a.N;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (FWD && a.bias && nok) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[r] = a.bias[a.bgs * z + n0 + r];
+    }
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < FM; ++f) {
+      if (!(nok && pv[f])) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] + bias[r];
+      if (FWD) {
+        bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + a.ogs * z + (int64_t)orow[f] * a.ldo + n0;
+        uint2 w;
+        w.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        w.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(o) = w;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { s[r] += v[r]; ss[r] += v[r] * v[r]; }
+      } else {
+        float* o = reinterpret_cast<float*>(a.out) + a.ogs * z + (int64_t)orow[f] * a.ldo + n0;
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        if (BNS) {  // dz of the BN tail whose output gradient this is, and its statistics
+          const uint2 u = *reinterpret_cast<const uint2*>(a.by + a.bygs * z + (int64_t)orow[f] * a.ldby + n0);
+          const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                               __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float t = yv[r] * s_k[cl + r] + s_k[BN + cl + r];
+            float dz = v[r];
+            if (a.bkind == ACT_RELU) {
+              dz = t > 0.f ? dz : 0.f;
+            } else if (a.bkind == ACT_SIGMOID) {
+              const float sg = sigmoidf_(t);
+              dz *= sg * (1.f - sg);
+            }
+            const float xh = (yv[r] - s_k[2 * BN + cl + r]) * s_k[3 * BN + cl + r];
+            s[r] += dz;
+            ss[r] += dz * xh;
+          }
+        }
+      }
+    }
+    if (want_red) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // the 16 pixels of a lane row -> lane 15 (DPP, common.h)
+        s[r] = row16_sum(s[r]);
+        ss[r] = row16_sum(ss[r]);
+      }
+      if (l16 == 15) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s_st[(wm * BN + cl + r) * 2 + 0] = s[r];
+          s_st[(wm * BN + cl + r) * 2 + 1] = ss[r];
+        }
+      }
+    }
+  }
+  if (want_red) {
+    __syncthreads();
+    const int rep = blockIdx.x % NREP;
+    double* dst = BNS ? a.bpart : a.stats;
+    const int rows = BNS ? 3 : 2;
+    for (int q = tid; q < BN * 2; q += 256) {
+      const int c = q >> 1, which = q & 1;
+      const int n = nbase + c;
+      if (n < a.N) {
+        float v = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < WAM; ++w2) v += s_st[(w2 * BN + c) * 2 + which];
+        atomicAdd(dst + ((int64_t)z * NREP + rep) * rows * a.N + which * a.N + n, (double)v);
+      }
+    }
+  }
+}
+
+#undef PSEL
+
+// ---- host-side plan
+struct LdsCfg {
+  int tile, BM, BN, WAM, KC, splits;
+};
+
+int decode_cfg(int cfg, LdsCfg& c) {
+  const int k = cfg - CONV_LDS_CFG0;
+  if (k < 0 || k >= CONV_LDS_NCFG) return -1;
+  c.tile = k / 8;
+  c.KC = (k / 4) % 2 ? 128 : 64;
+  c.splits = 1 << (k % 4);
+  c.BM = LDS_BM[c.tile]; c.BN = LDS_BN[c.tile]; c.WAM = LDS_WAM[c.tile];
+  if (c.KC == 128 && c.BM + c.BN > 192) return -2;  // LDS: two 128-deep stages of a 256-row tile
+  return 0;
+}
+
+// Phases, grid and table size of a launch.  dgrad: ConvArgs Hs/Ws = dy, Ho/Wo = dx (the conv's input).
+int make_plan(int mode, const ConvArgs& a, const LdsCfg& c, LdsPlan& pl, int& gx) {
+  pl = LdsPlan{};
+  pl.splits = c.splits;
+  int maxch = 0;
+  if (mode == MODE_FWD || mode == MODE_FWD_NOL) {
+    pl.nph = 1;
+    pl.mh = a.sh; pl.mw = a.sw; pl.by = 1; pl.bx = 1; pl.th = 1; pl.tw = 1; pl.qy = 1; pl.qx = 1;
+    LdsPhase& P = pl.ph[0];
+    P.oy0 = 0; P.ox0 = 0; P.Hq = a.Ho; P.Wq = a.Wo;
+    P.rh = 0; P.nh = a.KH; P.rw = 0; P.nw = a.KW;
+    P.ay = -a.ph; P.ax = -a.pw;
+  } else {
+    pl.mh = 1; pl.mw = 1; pl.by = -1; pl.bx = -1; pl.th = a.sh; pl.tw = a.sw; pl.qy = a.sh; pl.qx = a.sw;
+    int n = 0;
+    for (int py = 0; py < std::min(a.sh, a.Ho); ++py)
+      for (int px = 0; px < std::min(a.sw, a.Wo); ++px) {
+        LdsPhase& P = pl.ph[n++];
+        P.oy0 = py; P.ox0 = px;
+        P.Hq = (a.Ho - py + a.sh - 1) / a.sh;
+        P.Wq = (a.Wo - px + a.sw - 1) / a.sw;
+        P.rh = (py + a.ph) % a.sh;
+        P.rw = (px + a.pw) % a.sw;
+        P.nh = P.rh < a.KH ? (a.KH - P.rh + a.sh - 1) / a.sh : 0;
+        P.nw = P.rw < a.KW ? (a.KW - P.rw + a.sw - 1) / a.sw : 0;
+        P.ay = (py + a.ph - P.rh) / a.sh;
+        P.ax = (px + a.pw - P.rw) / a.sw;
+      }
+    pl.nph = n;
+    if (n < 1 || n > 4) return -2;
+  }
+  gx = 0;
+  for (int p = 0; p < pl.nph; ++p) {
+    LdsPhase& P = pl.ph[p];
+    const int k = P.nh * P.nw * a.Cs;
+    P.Kp = (k + c.KC - 1) / c.KC * c.KC;
+    P.m0 = gx;
+    gx += (a.B * P.Hq * P.Wq + c.BM - 1) / c.BM;
+    maxch = std::max(maxch, (P.Kp / c.KC + c.splits - 1) / c.splits);
+    if (std::abs(P.ay) > 56 || std::abs(P.ax) > 56 || a.KH > 56 || a.KW > 56) return -2;
+  }
+  pl.ntab = std::max(4, maxch * (c.KC / 8));
+  return 0;
+}
+
+template <int MODE>
+int launch_mode(const ConvArgs& a, int G, const LdsCfg& c, hipStream_t st) {
+  LdsPlan pl;
+  int gx;
+  int rc = make_plan(MODE, a, c, pl, gx);
+  if (rc) return rc;
+  const int ntn = (a.N + c.BN - 1) / c.BN;
+  if (c.splits > 1 && (!a.ws || !a.cnt)) return -3;
+  const bool nol = MODE == MODE_FWD_NOL, bns = MODE == MODE_DGRAD_BNS;
+  const size_t lds = (size_t)2 * (c.BM + c.BN) * c.KC * 2 + (size_t)2 * pl.ntab * 4 +
+                     ((size_t)c.WAM * c.BN * 2 + (nol ? 2 * a.Cs : (bns ? 4 * c.BN : 0))) * 4 + 16;
+  if (lds > 160 * 1024) return -2;
+  dim3 grid(gx, ntn * c.splits, G);
+#define LDS_LAUNCH(T, KC_)                                                                               \
+  if (c.tile == T && c.KC == KC_) {                                                                      \
+    hipLaunchKernelGGL((conv_lds_kernel<MODE, LDS_BM[T], LDS_BN[T], LDS_WAM[T], KC_>), grid, dim3(256), lds, st, a, pl); \
+    return (int)hipGetLastError();                                                                       \
+  }
+  LDS_LAUNCH(0, 64) LDS_LAUNCH(0, 128) LDS_LAUNCH(1, 64) LDS_LAUNCH(1, 128) LDS_LAUNCH(2, 64) LDS_LAUNCH(2, 128)
+  LDS_LAUNCH(3, 64) LDS_LAUNCH(4, 64) LDS_LAUNCH(4, 128) LDS_LAUNCH(5, 64) LDS_LAUNCH(5, 128) LDS_LAUNCH(6, 64)
+  LDS_LAUNCH(6, 128) LDS_LAUNCH(7, 64) LDS_LAUNCH(7, 128)
+#undef LDS_LAUNCH
+  return -1;
+}
+
+}  // namespace
+
+int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_floats, int64_t& ntickets) {
+  LdsCfg c;
+  int rc = decode_cfg(cfg, c);
+  if (rc) return rc;
+  if (a.aol) return -2;
+  LdsPlan pl;
+  int gx;
+  rc = make_plan(mode, a, c, pl, gx);
+  if (rc) return rc;
+  const int64_t tiles = (int64_t)G * gx * ((a.N + c.BN - 1) / c.BN);
+  ws_floats = c.splits > 1 ? tiles * c.splits * c.BM * c.BN : 0;
+  ntickets = c.splits > 1 ? tiles : 0;
+  return 0;
+}
+
+int launch_conv_lds(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
+  LdsCfg c;
+  int rc = decode_cfg(cfg, c);
+  if (rc) return rc;
+  if (a.aol) return -2;  // apply-on-load dgrads (opt-in, conv.hip) are not staged here
+  switch (mode) {
+    case MODE_FWD: return launch_mode<MODE_FWD>(a, G, c, st);
+    case MODE_FWD_NOL: return launch_mode<MODE_FWD_NOL>(a, G, c, st);
+    case MODE_DGRAD: return launch_mode<MODE_DGRAD>(a, G, c, st);
+    case MODE_DGRAD_BNS: return launch_mode<MODE_DGRAD_BNS>(a, G, c, st);
+    default: return -1;
+  }
+}
+
+}  // namespace mda

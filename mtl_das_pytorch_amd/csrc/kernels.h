@@ -56,6 +56,30 @@ struct ConvArgs {
   // DGRAD only, optional (aol = 0 off): the dy operand is applied on load (AolArgs)
   AolArgs ao;
   int aol;
+  // LDS-staged kernels (cfg >= CONV_LDS_CFG0, conv_lds.hip) with a cross-block split of K: fp32 partial
+  // tiles [G][tiles][splits][BM*BN] and one arrival ticket per output tile (zero-initialised; the reducing
+  // block resets it), sized by conv_lds_workspace
+  float* ws;
+  unsigned* cnt;
+};
+
+// One output-pixel phase of an LDS-staged conv launch (conv_lds.hip): output pixels (b, oy0 + i*qy,
+// ox0 + j*qx) for i < Hq, j < Wq, reduced over taps (kh, kw) = (rh + th*u, rw + tw*v), u < nh, v < nw,
+// whose input pixel is (i*mh + ay + by*u, j*mw + ax + bx*v).  The forward is one phase; a strided data
+// gradient has one phase per output parity (sub-pixel decomposition: only the taps that hit a real dy).
+struct LdsPhase {
+  int oy0, ox0, Hq, Wq;
+  int rh, nh, rw, nw;
+  int ay, ax;
+  int m0;   // first blockIdx.x of the phase
+  int Kp;   // nh * nw * Cs padded to the K chunk
+};
+struct LdsPlan {
+  LdsPhase ph[4];
+  int nph;
+  int mh, mw, by, bx, th, tw, qy, qx;
+  int splits;  // cross-block split of the K chunks
+  int ntab;    // per-block k-group table entries (LDS)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -190,6 +214,11 @@ struct AdamArgs {
 };
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
+// LDS-staged implicit GEMM (conv_lds.hip): cfg = CONV_LDS_CFG0 + 8 * tile + 4 * (KC == 128) + log2(splits)
+constexpr int CONV_LDS_CFG0 = 16, CONV_LDS_NCFG = 64;
+int launch_conv_lds(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
+// fp32 workspace floats and ticket count a cfg needs (0 when it does not split K); < 0: cfg invalid for a
+int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_floats, int64_t& ntickets);
 int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st);
 int wgrad_tile_shape(int cfg, int& TN, int& TK);
 constexpr int WGRAD_PATCH_CFG0 = 12;  // wgrad cfgs 12-15: 3x3/s1 patch kernels (conv.hip wgrad_patch_block)

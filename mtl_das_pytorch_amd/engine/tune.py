@@ -15,10 +15,11 @@ from typing import Dict, Iterable, Optional
 
 import torch
 
-from ..ops.functional import WGRAD_PATCH, WGRAD_TILES
+from ..ops.functional import CONV_LDS_CFG0, CONV_LDS_NCFG, WGRAD_PATCH, WGRAD_TILES, conv_workspace
 from ..ops.hip import lib
 
-CONV_CFGS = list(range(14))
+# conv.hip register-pipelined tiles 0-13, then conv_lds.hip LDS-staged tiles x K chunk x K split
+CONV_CFGS = list(range(14)) + list(range(CONV_LDS_CFG0, CONV_LDS_CFG0 + CONV_LDS_NCFG))
 
 
 def fused_max_m(kind: int) -> int:
@@ -74,6 +75,7 @@ def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, ve
     cache = load_cache() if cache is None else cache
     L = lib()
     for ph in phases:
+        keep = ph.__dict__.setdefault("ws_keep", {})  # split-K workspaces of the chosen LDS configs
         for launch in ph.launches:
             if launch.name not in ("conv_fwd", "conv_dgrad"):
                 continue
@@ -83,14 +85,25 @@ def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, ve
                 continue
             if sig not in cache:
                 best, best_t = cfg, float("inf")
+                dev = torch.device("cuda", torch.cuda.current_device())
                 for c in CONV_CFGS:
-                    t = _time(lambda: L.conv(mode, c, G, torch.cuda.current_stream().cuda_stream, d))
+                    dc = dict(d)
+                    ws = conv_workspace(mode, c, G, dc, dev)
+                    if ws is None:
+                        continue
+                    t = _time(lambda: L.conv(mode, c, G, torch.cuda.current_stream().cuda_stream, dc))
+                    del ws
                     if t < best_t:
                         best, best_t = c, t
                 cache[sig] = best
                 if verbose:
                     print(f"tuned {sig}: cfg {best} ({best_t * 1e3:.1f} us)", flush=True)
-            launch.args = (mode, cache[sig], G, d)
+            cfg = cache[sig]
+            ws = conv_workspace(mode, cfg, G, d, torch.device("cuda", torch.cuda.current_device()))
+            if ws is None:
+                raise RuntimeError(f"cached conv config {cfg} is invalid for {sig}")
+            keep[id(launch)] = ws
+            launch.args = (mode, cfg, G, d)
     for ph in phases:
         for launch in ph.launches:
             if launch.name != "conv_wgrad" or launch.owner is None:
@@ -149,7 +162,7 @@ def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False
     weight-gradient launches per tile config (``batch_wgrads``)."""
     if prog.device.type != "cuda":
         return {}
-    cache = load_cache()
+    cache = {} if os.environ.get("MDA_RETUNE") == "1" else load_cache()
     n0 = len(cache)
     autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose, measure)
     if batch_wgrads:

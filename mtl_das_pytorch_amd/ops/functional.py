@@ -71,11 +71,44 @@ def _fwd_cfg(N, M):
     return 3 if M >= 64 * 128 else 4
 
 
+CONV_LDS_CFG0, CONV_LDS_NCFG = 16, 64  # csrc/kernels.h: LDS-staged conv configs (conv_lds.hip)
+LDS_TILES = [(64, 64), (128, 64), (64, 128), (128, 128), (32, 64), (64, 32), (32, 32), (128, 16)]
+
+
+def lds_cfg(tile: int, kc: int = 64, splits: int = 1) -> int:
+    """Config id of the LDS-staged conv kernel: tile index into LDS_TILES (BM pixels x BN channels), K chunk
+    64 / 128, cross-block split of K into 1 / 2 / 4 / 8."""
+    return CONV_LDS_CFG0 + 8 * tile + 4 * (kc == 128) + {1: 0, 2: 1, 4: 2, 8: 3}[splits]
+
+
+def conv_workspace(mode: int, cfg: int, G: int, d: dict, device) -> Optional[tuple]:
+    """Attach the split-K workspace an LDS-staged conv config needs (fp32 partial tiles + zeroed arrival
+    tickets) to the argument dict ``d``; returns the tensors to keep alive, or None when ``cfg`` cannot run
+    these arguments."""
+    if cfg < CONV_LDS_CFG0:
+        return ()
+    rc, ws, nt = lib().conv_workspace(mode, cfg, G, d)
+    if rc != 0:
+        return None
+    if ws == 0:
+        d.pop("ws", None)
+        d.pop("cnt", None)
+        return ()
+    w = torch.empty(ws, device=device, dtype=torch.float32)
+    c = torch.zeros(nt, device=device, dtype=torch.int32)
+    d["ws"], d["cnt"] = w.data_ptr(), c.data_ptr()
+    return (w, c)
+
+
 class ConvCall:
     """A prepared convolution launch (packed weights + argument dict); ``run()`` enqueues it again."""
 
     def __init__(self, mode, cfg, d, out, keep):
         self.mode, self.cfg, self.d, self.out, self._keep = mode, cfg, d, out, keep
+        ws = conv_workspace(mode, cfg, 1, d, out.device)
+        if ws is None:
+            raise ValueError(f"conv config {cfg} cannot run this geometry")
+        self._ws = ws
 
     def run(self):
         lib().conv(self.mode, self.cfg, 1, stream(), self.d)

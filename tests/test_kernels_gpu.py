@@ -138,10 +138,15 @@ def test_conv_wgrad_patch(fn, case, cfg, nol):
     assert rel(dw, ref) < 1e-5  # same bf16 operands, fp32 accumulation: only the summation order differs
 
 
+# conv.hip default tile, and conv_lds.hip LDS-staged configs (tile, K chunk, K split) -- see test_conv_lds_gpu.py
+LDS_SAMPLE = [None, 16 + 8 * 0 + 0 + 0, 16 + 8 * 1 + 4 + 2, 16 + 8 * 7 + 0 + 3]
+
+
+@pytest.mark.parametrize("cfg", LDS_SAMPLE)
 @pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("case", [(4, 17, 42, 32, 32, 3, 1, 1), (2, 33, 83, 16, 16, 3, 1, 1), (4, 9, 21, 64, 128, 3, 2, 1),
                                   (4, 5, 11, 64, 128, 3, 1, 1)])
-def test_conv_normalise_on_load(fn, kind, case):
+def test_conv_normalise_on_load(fn, kind, case, cfg):
     """Forward conv reading a pre-BN y and applying act(BN(y)) to its operand (training statistics from the
     replicas; running statistics updated and batch constants published by block 0), and the matching
     weight gradient that rebuilds the operand from the published constants."""
@@ -155,7 +160,7 @@ def test_conv_normalise_on_load(fn, kind, case):
     z = _torch_bn(y, gamma, beta)
     act = (z if kind == 0 else F.relu(z)).bfloat16().float()  # the engine's operand is bf16
     ref = F.conv2d(act, w, stride=s, padding=p)
-    out = fn.conv2d(nhwc(y).bfloat16(), w, stride=s, padding=p, nol=(bn, kind))
+    out = fn.conv2d(nhwc(y).bfloat16(), w, stride=s, padding=p, nol=(bn, kind), cfg=cfg)
     assert rel(nchw(out), ref) < 6e-3
     assert torch.allclose(rm, 0.1 * y.mean((0, 2, 3)), atol=1e-4, rtol=1e-3) and int(nbt.item()) == 1
     inv = torch.rsqrt(y.var((0, 2, 3), unbiased=False) + 1e-5)
@@ -167,13 +172,14 @@ def test_conv_normalise_on_load(fn, kind, case):
     assert rel(dw, wr.grad) < 5e-3
 
 
-def test_conv_two_segment_input(fn):
+@pytest.mark.parametrize("cfg", LDS_SAMPLE)
+def test_conv_two_segment_input(fn, cfg):
     g = torch.Generator().manual_seed(3)
     a = torch.randn(2, 32, 17, 42, generator=g).bfloat16().float().cuda()
     bb = torch.randn(2, 32, 17, 42, generator=g).bfloat16().float().cuda()
     w = (torch.randn(16, 64, 1, 1, generator=g) / 8).bfloat16().float().cuda()
     ref = F.conv2d(torch.cat([a, bb], 1), w)
-    y = fn.conv2d(nhwc(a).bfloat16(), w, x2=nhwc(bb).bfloat16())
+    y = fn.conv2d(nhwc(a).bfloat16(), w, x2=nhwc(bb).bfloat16(), cfg=cfg)
     assert rel(nchw(y), ref) < 6e-3
     dy = torch.randn_like(ref).bfloat16().float()
     dw = fn.conv2d_wgrad(nhwc(a).bfloat16(), nhwc(dy).bfloat16(), w.shape, x2=nhwc(bb).bfloat16())
@@ -265,10 +271,11 @@ def test_bn_tail_forward_backward(fn, kind, C, fused):
         assert rel(nchw(side), rr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("cfg", LDS_SAMPLE)
 @pytest.mark.parametrize("kind", [0, 1, 2])
 @pytest.mark.parametrize("case", [(4, 17, 42, 32, 16, 3, 1, 1), (4, 9, 21, 64, 128, 3, 2, 1),
                                   (2, 33, 83, 16, 16, 3, 1, 1), (4, 5, 11, 128, 64, 1, 1, 0)])
-def test_dgrad_fused_bn_backward_stats(fn, kind, case):
+def test_dgrad_fused_bn_backward_stats(fn, kind, case, cfg):
     """conv(act(BN(y))): the dgrad epilogue accumulates the BN-backward sums, the tail runs its apply pass
     only; dy / dgamma / dbeta against autograd, and against the two-pass (reduce + apply) backward."""
     B, H, W, C, Co, k, s, p = case
@@ -286,7 +293,7 @@ def test_dgrad_fused_bn_backward_stats(fn, kind, case):
     out.backward(go)
     yb = nhwc(y).bfloat16()
     part = torch.zeros(NREP, 3, C, device="cuda", dtype=torch.float64)
-    dx = fn.conv2d_dgrad(nhwc(go).bfloat16(), w, (H, W), stride=s, padding=p, bn_stats=(yb, bn, part, kind))
+    dx = fn.conv2d_dgrad(nhwc(go).bfloat16(), w, (H, W), stride=s, padding=p, bn_stats=(yb, bn, part, kind), cfg=cfg)
     dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
     dy, _, _ = fn.bn_tail_backward(kind, yb, bn, [dx], dg, db, part=part)
     assert rel(nchw(dy), yr.grad) < 1e-2
