@@ -33,6 +33,13 @@ MODEL_NAMES = {"MTL": "modelA_MTL", "single_distance": "modelB_singleTask_distan
                "single_event": "modelB_singleTask_event", "multi_classifier": "modelC_multiClassifier"}
 
 
+def _accs(m, joint):
+    """distance / event accuracy from the head's metric rows (Model C: decoded joint rows 1, 2)."""
+    if joint:
+        return {"distance": round(float(m[1, 1] / m[1, 2]), 4), "event": round(float(m[2, 1] / m[2, 2]), 4)}
+    return {"distance": round(float(m[0, 1] / m[0, 2]), 4), "event": round(float(m[-1, 1] / m[-1, 2]), 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -44,6 +51,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per step")
     ap.add_argument("--buckets", type=int, default=None,
                     help="DP gradient buckets overlapped with the backward (default: the model's, 1 on one GPU)")
+    ap.add_argument("--heldout", type=int, default=1024, help="held-out samples per GPU evaluated after timing")
     ap.add_argument("--no-tune", action="store_true", help="skip per-layer kernel autotuning (cached table only)")
     args = ap.parse_args()
 
@@ -104,6 +112,15 @@ def main():
     dt = ctx.max_scalar(dt)
     m = prog.metrics.clone()
     ctx.all_reduce_(m)
+    # after the timed region: held-out accuracy of the model the timed steps produced (the metric's
+    # "event-cls accuracy" half) on samples no rank trained on, BN in eval mode (running statistics)
+    Xh, dh, eh = generate(args.heldout, seed=500000 + ctx.rank, device=dev)
+    runner.set_eval_source(Xh, encode_joint(dh, eh) if joint else torch.stack([dh, eh], 1))
+    runner.reset_metrics()
+    for i in range(0, args.heldout - args.batch + 1, args.batch):
+        runner.eval_step(torch.arange(i, i + args.batch, device=dev))
+    mh = prog.metrics.clone()
+    ctx.all_reduce_(mh)
     value = world * args.batch * args.steps / dt
     out = {
         "metric": METRIC,
@@ -121,10 +138,10 @@ def main():
         "config": {"model": MODEL_NAMES.get(args.model, args.model),
                    "global_batch": args.batch * world, "seq_len": 250, "input_shape": [1, 100, 250],
                    "parallelism": f"dp{world}"},
-        "train_acc_timed_steps": ({"distance": round(float(m[1, 1] / m[1, 2]), 4),
-                                   "event": round(float(m[2, 1] / m[2, 2]), 4)} if joint else
-                                  {"distance": round(float(m[0, 1] / m[0, 2]), 4),
-                                   "event": round(float(m[-1, 1] / m[-1, 2]), 4)}),
+        "train_acc_timed_steps": _accs(m, joint),
+        "heldout_acc_after_timed_steps": _accs(mh, joint),
+        "heldout_samples": (args.heldout // args.batch) * args.batch * world,
+        "train_steps_before_heldout": args.warmup + args.steps,
         "vs_eager_pytorch_mi355x": round(value / (EAGER_MI355X_PER_GPU * world), 3) if args.model == "MTL" else None,
         "hip_graph": not args.no_graph,
         "grad_buckets_mb": [round((hi - lo) * 4 / 2 ** 20, 2) for lo, hi in buckets],

@@ -329,6 +329,10 @@ void adam_pack(int64_t stream, py::dict d) {
 
 }  // namespace
 
+namespace mda {
+void register_matio(py::module& m);  // matio.cpp: native MAT-file batch loader
+}
+
 PYBIND11_MODULE(_mda_hip, m) {
   m.doc() = "gfx950 HIP kernels of mtl_das_pytorch_amd";
   m.attr("NREP") = NREP;
@@ -356,4 +360,5 @@ PYBIND11_MODULE(_mda_hip, m) {
   });
   m.def("adam_pack", &adam_pack);
   m.def("hip_device_sync", []() { return (int)hipDeviceSynchronize(); });
+  register_matio(m);
 }

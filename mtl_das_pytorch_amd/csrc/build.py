@@ -27,7 +27,8 @@ def so_path() -> str:
 
 
 def _sources():
-    return sorted(glob.glob(os.path.join(HERE, "*.hip"))) + [os.path.join(HERE, "bindings.cpp")]
+    return (sorted(glob.glob(os.path.join(HERE, "*.hip"))) + [os.path.join(HERE, "bindings.cpp")]
+            + [os.path.join(HERE, "matio.cpp")])
 
 
 def needs_build() -> bool:
@@ -55,8 +56,10 @@ def build(force: bool = False, debug: bool = False, verbose: bool = True, jobs: 
     def compile_one(src):
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
         cmd = [HIPCC] + common + ["-c", src, "-o", obj]
-        if src.endswith(".cpp"):
+        if src.endswith("bindings.cpp"):
             cmd = [HIPCC] + common + ["-x", "hip", "-c", src, "-o", obj]
+        elif src.endswith(".cpp"):  # host-only C++ (native data loader): no device code objects
+            cmd = [HIPCC] + [c for c in common if not c.startswith("--offload-arch")] + ["-x", "c++", "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
@@ -68,7 +71,7 @@ def build(force: bool = False, debug: bool = False, verbose: bool = True, jobs: 
     with cf.ThreadPoolExecutor(max_workers=min(jobs, len(srcs))) as ex:
         objs = list(ex.map(compile_one, srcs))
     tmp = so + ".tmp"
-    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs + ["-lz", "-lpthread"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")

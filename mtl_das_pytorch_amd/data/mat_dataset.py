@@ -175,6 +175,10 @@ class Datasetram(_MatDatasetBase):
 
     def __init__(self, mat_list, label_list, key="data", paper_single=False, snr_db=None, progress=True):
         super().__init__(mat_list, label_list, key, paper_single, snr_db)
+        self._arr = self._load_native() if snr_db is None else None
+        if self._arr is not None:
+            self.mat_file_list = list(self._arr)
+            return
         it = range(len(self.mat_list))
         if progress:
             try:
@@ -184,12 +188,35 @@ class Datasetram(_MatDatasetBase):
                 pass
         self.mat_file_list = [self._load(i) for i in it]
 
+    def _load_native(self):
+        """All files in one call of the native multi-threaded MAT reader (csrc/matio.cpp) into one
+        contiguous float32 array; files it does not parse are read with scipy.  None if unavailable."""
+        if not self.mat_list:
+            return None
+        try:
+            from ..ops.hip import available, lib
+            if not available():
+                return None
+            L = lib()
+        except Exception:  # pragma: no cover
+            return None
+        first = self._load(0)
+        arr = np.empty((len(self.mat_list),) + first.shape, np.float32)
+        st = L.MatBatchLoader(self.mat_list, self.key, first.size, min(16, os.cpu_count() or 1)).load(
+            list(range(len(self.mat_list))), arr.ctypes.data)
+        for j, rc in enumerate(st):
+            if rc != 0:
+                arr[j] = self._load(j)
+        return arr
+
     def __getitem__(self, item):
         return self._item(self.mat_file_list[item], item)
 
     def as_arrays(self):
         if not self.mat_file_list:
             return np.zeros((0, 1, 100, 250), np.float32), self.labels_array()
+        if self._arr is not None:
+            return self._arr, self.labels_array()
         return np.stack(self.mat_file_list), self.labels_array()
 
 

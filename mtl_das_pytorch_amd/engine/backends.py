@@ -150,6 +150,9 @@ class TorchBackend(Backend):
                 o += n
         self.opt.step()
 
+    def set_eval_data(self, X: torch.Tensor, labels: torch.Tensor):
+        self.X_eval, self.labels_eval = X, labels
+
     @torch.no_grad()
     def eval_batch(self, idx: torch.Tensor, nvalid: int):
         self.model.eval()
@@ -224,6 +227,9 @@ class EngineBackend(Backend):
 
     def train_batch(self, idx: torch.Tensor):
         self.runner.train_step(idx)
+
+    def set_eval_data(self, X: torch.Tensor, labels: torch.Tensor):
+        self.runner.set_eval_source(X, labels)
 
     def eval_batch(self, idx: torch.Tensor, nvalid: int):
         if idx.numel() < self.B:  # pad the last batch (BN uses running stats in eval: padding is inert)

@@ -34,6 +34,7 @@ import numpy as np
 import torch
 
 from ..data.mat_dataset import Dataset_mat_MTL
+from ..data.stream import DiskBatchStream
 from ..data.synthetic import N_DIST, generate
 from ..models import build_model
 from ..parallel.dist import DistContext, ShardedIndexSampler, init_distributed
@@ -50,8 +51,27 @@ def _labels_tensor(label_list, joint: bool) -> torch.Tensor:
     return torch.as_tensor(np.asarray(label_list, dtype=np.int64))
 
 
+class ResidentSource:
+    """A split resident in device memory (HBM on the GPU): batches are index tensors into ``X``."""
+
+    def __init__(self, X: torch.Tensor, labels: torch.Tensor):
+        self.X, self.labels = X, labels
+
+    def __len__(self):
+        return len(self.X)
+
+    def batches(self, index_batches):
+        for b in index_batches:
+            yield b.to(self.X.device), int(b.numel())
+
+    def close(self):
+        pass
+
+
 def load_datasets(cfg: TrainConfig, device):
-    """(X_train, lab_train, X_val, lab_val) resident on ``device``; labels [N,2] or joint [N]."""
+    """``(train, val)`` data sources (``ResidentSource`` or, with ``--dataset_ram False``, a
+    ``DiskBatchStream``); labels are ``[N,2]`` (distance, event) or joint ``[N]``.  Test mode returns
+    ``(None, test_set)``."""
     joint = cfg.model == "multi_classifier"
     if cfg.synthetic > 0:
         per = cfg.synthetic
@@ -61,25 +81,29 @@ def load_datasets(cfg: TrainConfig, device):
         X, d_, e_ = generate(len(d), seed=seed, device="cpu", in_channels=cfg.in_channels, distance=d, event=e)
         lab = (d_ + N_DIST * e_) if joint else torch.stack([d_, e_], 1)
         if cfg.is_test:
-            return None, None, X.to(device), lab.to(device)
+            return None, ResidentSource(X.to(device), lab.to(device))
         # per-class KFold-like split: every 5th sample of each class goes to validation
         g = torch.Generator().manual_seed(cfg.random_state)
         perm = torch.randperm(len(d), generator=g)
         nval = max(1, len(d) // 5)
         val_idx, tr_idx = perm[:nval], perm[nval:]
-        return X[tr_idx].to(device), lab[tr_idx].to(device), X[val_idx].to(device), lab[val_idx].to(device)
+        return (ResidentSource(X[tr_idx].to(device), lab[tr_idx].to(device)),
+                ResidentSource(X[val_idx].to(device), lab[val_idx].to(device)))
     if cfg.is_test:
         dirs = (cfg.test_set_striking, cfg.test_set_excavating)
     else:
         dirs = (cfg.trainVal_set_striking, cfg.trainVal_set_excavating)
-    ds = Dataset_mat_MTL(dirs[0], dirs[1], random_state=cfg.random_state, ram=True, is_test=cfg.is_test,
+    ds = Dataset_mat_MTL(dirs[0], dirs[1], random_state=cfg.random_state, ram=cfg.dataset_ram, is_test=cfg.is_test,
                          fold_index=cfg.fold_index, multi_categories=joint, snr_db=cfg.snr_db, progress=False)
-    xtr, ytr = ds.dataset["train"].as_arrays()
-    xva, yva = ds.dataset["val"].as_arrays()
-    if cfg.is_test:
-        return None, None, torch.as_tensor(xva).to(device), torch.as_tensor(yva).to(device)
-    return (torch.as_tensor(xtr).to(device), torch.as_tensor(ytr).to(device),
-            torch.as_tensor(xva).to(device), torch.as_tensor(yva).to(device))
+    if not cfg.dataset_ram:  # reference DatasetDisk: stream every epoch from disk through a bounded ring
+        mk = lambda split: DiskBatchStream(ds.dataset[split], cfg.batch_size, device, ring=cfg.stream_ring,
+                                           threads=cfg.loader_threads)
+        return (None if cfg.is_test else mk("train")), mk("val")
+    sources = []
+    for split in ("train", "val"):
+        x, y = ds.dataset[split].as_arrays()
+        sources.append(ResidentSource(torch.as_tensor(x).to(device), torch.as_tensor(y).to(device)))
+    return (None if cfg.is_test else sources[0]), sources[1]
 
 
 class Trainer:
@@ -133,9 +157,10 @@ class Trainer:
     def run(self):
         cfg = self.cfg
         self.print(os.path.abspath(__file__))
-        X, Y, Xv, Yv = load_datasets(cfg, self.device)
-        if X is None:  # test mode evaluates the (whole) test set
-            X, Y = Xv, Yv
+        self.train_src, self.val_src = load_datasets(cfg, self.device)
+        if self.train_src is None:  # test mode evaluates the (whole) test set
+            self.train_src = self.val_src
+        X, Y, Xv, Yv = self.train_src.X, self.train_src.labels, self.val_src.X, self.val_src.labels
         kw = dict(ctx=self.ctx, batch=cfg.batch_size, lr=cfg.lr, weight_decay=cfg.weight_decay,
                   loss_weights=cfg.loss_weights)
         if self.backend_name == "engine":
@@ -147,7 +172,7 @@ class Trainer:
                 self.model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(self.model)
             self.model.to(self.device)
             self.backend = TorchBackend(self.model, cfg.model, X, Y, Xv, Yv, **kw)
-        self.n_train, self.n_val = len(X), len(Xv)
+        self.n_train, self.n_val = len(self.train_src), len(self.val_src)
         self.print(f"backend: {self.backend_name}  device: {self.device}  world: {self.ctx.world}  "
                    f"train samples: {0 if cfg.is_test else self.n_train}  val samples: {self.n_val}")
         start_epoch, lr, val_done = 0, cfg.lr, False
@@ -187,6 +212,8 @@ class Trainer:
                         np.save(p, self._train_line(name))
                 plot_curves(self.save_dir, cfg.model)
         self.ctx.barrier()
+        for src in {id(self.train_src): self.train_src, id(self.val_src): self.val_src}.values():
+            src.close()
         self.logger.save()
         self.logger.close()
         return self.save_dir
@@ -200,12 +227,12 @@ class Trainer:
 
     def train_epoch(self, epoch: int, sampler: ShardedIndexSampler):
         cfg, be = self.cfg, self.backend
-        batches = sampler.epoch(epoch, self.device)
+        batches = sampler.epoch(epoch, "cpu")
         be.reset_metrics()
         last = be.read_metrics()
         prof = self._maybe_profiler(epoch)
         t_log = time.perf_counter()
-        for bi, idx in enumerate(batches):
+        for bi, (idx, _) in enumerate(self.train_src.batches(batches)):
             if self.fault is not None and self.global_step == self.fault:
                 print(f"fault injection: rank {self.ctx.rank} exits at global step {self.global_step}",
                       file=sys.stderr, flush=True)
@@ -246,29 +273,61 @@ class Trainer:
                     np.save(os.path.join(self.save_dir, "trainAccLine"), self._train_line("trainAccLine"))
 
     @torch.no_grad()
-    def validate(self, epoch: int):
+    def _eval_pass(self, src):
+        """Evaluate a whole data source (sharded over ranks); returns the rank-summed metrics and the
+        reference's validation loss numerator (sum of batch-mean losses, per task)."""
         cfg, be = self.cfg, self.backend
-        be.sync_bn_stats()
         be.reset_metrics()
-        n = self.n_val
-        # shard the validation set over ranks; every rank runs full batches (the last one masked)
-        order = torch.arange(n, device=self.device)
+        n = len(src)
+        B = cfg.batch_size
+        order = torch.arange(n)
         per = (n + self.ctx.world - 1) // self.ctx.world
         mine = order[self.ctx.rank * per:min(n, (self.ctx.rank + 1) * per)]
+        chunks = [mine[i:i + B] for i in range(0, len(mine), B)]
+        # reference loss: sum over batches of the batch-mean loss.  Every batch but the last is full, so
+        # the sum is (loss over the full batches) / B + (last batch's loss) / its size: the metrics are read
+        # back twice per validation instead of once per batch
         batch_means = np.zeros(len(be.names))
-        prev = be.read_metrics()
-        for i in range(0, len(mine), cfg.batch_size):
-            idx = mine[i:i + cfg.batch_size]
-            be.eval_batch(idx, idx.numel())
-            cur = be.read_metrics()
-            d = cur - prev
-            prev = cur
-            batch_means += d.loss / np.maximum(d.count, 1)  # reference: sum of batch-mean losses
-        m = reduce_metrics(self.ctx, be.read_metrics())
+        before_tail = None
+        for idx, nv in src.batches(chunks):
+            if nv < B:
+                before_tail = be.read_metrics()
+            be.eval_batch(idx, nv)
+        cur = be.read_metrics()
+        if before_tail is None:
+            batch_means += cur.loss / B
+        else:
+            batch_means += before_tail.loss / B + (cur.loss - before_tail.loss) / max(len(chunks[-1]), 1)
+        m = reduce_metrics(self.ctx, cur)
         if self.ctx.enabled:
             bm = torch.tensor(batch_means, dtype=torch.float64, device=self.ctx.device)
             self.ctx.all_reduce_(bm)
             batch_means = bm.cpu().numpy()
+        return m, batch_means
+
+    @torch.no_grad()
+    def evaluate(self, X: torch.Tensor, labels: torch.Tensor) -> dict:
+        """Accuracy / MAE / loss of the current model on an arbitrary resident set (e.g. a held-out test
+        set, or one at a given SNR) without touching curves, checkpoints or the LR schedule."""
+        self.backend.sync_bn_stats()
+        self.backend.set_eval_data(X, labels)
+        try:
+            m, batch_means = self._eval_pass(ResidentSource(X, labels))
+        finally:
+            self.backend.set_eval_data(self.val_src.X, self.val_src.labels)
+        n = len(X)
+        out = {"acc": {m.names[t]: m.acc(t) for t in range(len(m.names))},
+               "loss": {m.names[t]: float(batch_means[t] / n) for t in range(len(m.names))}}
+        if "distance" in m.names:
+            out["mae_m"] = mae_from_confusion(m.cm[m.names.index("distance")])
+        return out
+
+    @torch.no_grad()
+    def validate(self, epoch: int):
+        cfg, be = self.cfg, self.backend
+        be.sync_bn_stats()
+        n = self.n_val
+        m, batch_means = self._eval_pass(self.val_src)
         nt = len(m.names)
         accs = [m.acc(t) for t in range(nt)]
         if cfg.model == "multi_classifier":

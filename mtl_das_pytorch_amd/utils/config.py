@@ -62,6 +62,8 @@ class TrainConfig:
     sync_bn: bool = False                 # all-reduce BN batch statistics across ranks (torch backend)
     profile_steps: int = 0                # >0: torch.profiler trace of that many train steps (rank 0)
     debug: bool = False                   # serialised kernels + blocking launches, no HIP graphs
+    stream_ring: int = 4                  # --dataset_ram False: batches in flight (disk -> pinned -> HBM ring)
+    loader_threads: int = 8               # native .mat reader threads (csrc/matio.cpp)
     is_test: bool = False
 
     @property
@@ -121,6 +123,9 @@ def build_parser(is_test: bool) -> argparse.ArgumentParser:
     g.add_argument("--profile_steps", type=int, default=0, help="write a torch.profiler trace of N train steps")
     g.add_argument("--debug", type=str2bool, default=False,
                    help="debug mode: AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING=1, no HIP graphs")
+    g.add_argument("--stream_ring", type=int, default=4,
+                   help="--dataset_ram False: batches in flight in the disk -> pinned host -> HBM ring")
+    g.add_argument("--loader_threads", type=int, default=8, help="threads of the native .mat batch reader")
     return ap
 
 

@@ -49,3 +49,24 @@ def test_single_task_engine_trainer(tmp_path):
     tr = Trainer(cfg)
     tr.run()
     assert set(tr.last_val["acc"]) == {"event"}
+
+
+def test_engine_disk_stream_matches_ram(tmp_path):
+    """--dataset_ram False on the engine: batches arrive through the pinned host ring, the copy stream and
+    the HBM ring (csrc/matio.cpp reader) and train bitwise like the HBM-resident dataset."""
+    from mtl_das_pytorch_amd.data import write_mat_tree
+    from mtl_das_pytorch_amd.engine.trainer import Trainer
+    from mtl_das_pytorch_amd.utils.config import TrainConfig
+    tree = write_mat_tree(str(tmp_path / "das"), n_per_class=5, n_test_per_class=1, seed=5, splits=("train",))
+    res = {}
+    for ram in (True, False):
+        torch.manual_seed(0)
+        cfg = TrainConfig(model="MTL", batch_size=8, epoch_num=2, val_every=2, log_every=4,
+                          output_savedir=str(tmp_path / str(ram)), save_threshold=2.0, backend="engine",
+                          dataset_ram=ram, stream_ring=3, trainVal_set_striking=tree["striking_train"],
+                          trainVal_set_excavating=tree["excavating_train"])
+        tr = Trainer(cfg)
+        tr.run()
+        res[ram] = (tr.last_val, tr.backend.prog.flat.params.detach().clone())
+    assert res[True][0]["acc"] == res[False][0]["acc"]
+    assert torch.equal(res[True][1], res[False][1])
