@@ -140,8 +140,16 @@ ConvArgs parse_conv(int mode, py::dict d) {
     a.bbn = parse_bn(b["bn"].cast<py::dict>());
     a.bpart = P<double>(b, "part");
     a.bkind = (int)I(b, "kind");
-    if (mode != MODE_DGRAD || !a.bpart || !a.by || !a.bbn.stats || !a.bbn.training || a.bbn.C != a.N ||
-        a.ldby % 4 || a.bkind < ACT_NONE || a.bkind > ACT_SIGMOID)
+    a.bN = (int)I(b, "C", a.N);
+    a.bpgs = I(b, "pgs", -1);
+    if (a.bkind == ADD_RELU) {
+      a.br = P<const bf16_t>(b, "r"); a.brgs = I(b, "rgs"); a.ldbr = (int)I(b, "ldr");
+      if (b.contains("bn2") && !b["bn2"].is_none()) { a.bbn2 = parse_bn(b["bn2"].cast<py::dict>()); a.br_bn = 1; }
+    }
+    if (mode != MODE_DGRAD || !a.bpart || !a.by || !a.bbn.stats || !a.bbn.training || a.bbn.C != a.bN ||
+        a.bN > a.N || a.bN % 8 || a.ldby % 4 || (a.bkind > ACT_SIGMOID && a.bkind != ADD_RELU) || a.bkind < ACT_NONE ||
+        (a.bkind == ADD_RELU && (!a.br || a.ldbr % 4 || (a.br_bn && (a.bbn2.C != a.bN || !a.bbn2.training)))) ||
+        (a.bpgs == 0 && (a.bygs != 0 || a.brgs != 0)))
       throw std::runtime_error("conv: bad fused BN-backward statistics arguments");
   }
   if (d.contains("nol") && !d["nol"].is_none()) {  // normalise-on-load of the input (forward)
@@ -245,6 +253,17 @@ TailArgs parse_tail(const py::dict& d) {
   a.dgamma2 = P<float>(d, "dgamma2"); a.dbeta2 = P<float>(d, "dbeta2");
   a.pgs = I(d, "pgs");
   a.tsc = P<uint64_t>(d, "tsc");
+  if (d.contains("prev") && !d["prev"].is_none()) {  // apply pass: partial statistics of the previous tail
+    py::dict q = d["prev"].cast<py::dict>();
+    a.py = P<const bf16_t>(q, "y"); a.ldpy = (int)I(q, "ldy");
+    a.pr = P<const bf16_t>(q, "r"); a.ldpr = (int)I(q, "ldr");
+    a.pbn = parse_bn(q["bn"].cast<py::dict>());
+    if (q.contains("bn2") && !q["bn2"].is_none()) { a.pbn2 = parse_bn(q["bn2"].cast<py::dict>()); a.pr_bn = 1; }
+    a.pkind = (int)I(q, "kind");
+    a.ppart = P<double>(q, "part");
+    if (!a.ppart || a.pbn.C != a.C || (a.pr_bn && a.pbn2.C != a.C) || a.ldpy % 8 || a.ldpr % 8)
+      throw std::runtime_error("tail: bad previous-tail statistics arguments");
+  }
   if (a.C % 8 || a.C > 2048) throw std::runtime_error("tail: C must be a multiple of 8 and <= 2048");
   return a;
 }

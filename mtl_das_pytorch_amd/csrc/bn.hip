@@ -328,16 +328,29 @@ __global__ __launch_bounds__(BNB_T) void bnb_reduce_kernel(TailArgs a) {
   }
 }
 
-template <int KIND, int CGB>
+// PREV (ADD_RELU with identity shortcut, apply-only backward): the side output dz is also a gradient
+// source of the previous tail (TailArgs::ppart); its partial statistics are accumulated here, so that tail
+// needs no reduce pass of its own over this source.
+template <int KIND, int CGB, bool PREV>
 __global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
   constexpr int PL = BNB_T / CGB, CB = 8 * CGB;
   __shared__ float s_x[2][5][CB];
   __shared__ float s_red[BNB_T];
   __shared__ float s_coef[2][3][CB];
+  __shared__ float s_p[PREV ? 8 : 1][CB];              // previous tail: BN, BN2 (scale, shift, mean, invstd)
+  __shared__ float s_pp[PREV ? 16 : 1][3][CB];         // its partial sums per 16-lane row
   const int z = blockIdx.z, chunk = blockIdx.x;
   const int cgl = threadIdx.x % CGB, pl = threadIdx.x / CGB;
   const int cblk = blockIdx.y * CB, c = cblk + cgl * 8;
   const bool two = (KIND == ADD_RELU && a.r_bn);
+  if (PREV) {
+    for (int t = threadIdx.x; t < 2 * CB; t += BNB_T) {
+      const int k = t / CB, j = t - k * CB;
+      float sc = 0.f, sh = 0.f, mu = 0.f, inv = 0.f;
+      if (k == 0 || a.pr_bn) bn_channel_bwd(k ? a.pbn2 : a.pbn, 0, cblk + j, sc, sh, mu, inv);
+      s_p[4 * k][j] = sc; s_p[4 * k + 1][j] = sh; s_p[4 * k + 2][j] = mu; s_p[4 * k + 3][j] = inv;
+    }
+  }
   BwdCtx X;
   bnb_ctx<KIND, CGB>(a, z, cblk, cgl, X, s_x);
   // the NREP replicas of this block's channels: item = (stat, channel), Q threads per item
@@ -384,6 +397,9 @@ __global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
   const int p0 = chunk * a.chunk_px, p1 = min(M, p0 + a.chunk_px);
   const bf16_t* yz = a.y + a.ygs * z;
   const float* dzz = a.dzbuf ? a.dzbuf + a.dzgs * z : nullptr;
+  float q0[8], q1[8], q2[8];  // PREV partial sums
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { q0[j] = 0.f; q1[j] = 0.f; q2[j] = 0.f; }
   for (int p = p0 + pl; p < p1; p += PL) {
     float dz[8], y[8], o[8];
     if (dzz) {
@@ -391,6 +407,26 @@ __global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
     } else {
       float xh[8], xh2[8], side[8];
       compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
+      if ((KIND == SIGMUL || (KIND == ADD_RELU && !a.r_bn)) && a.side && a.apply_side)
+        store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
+      if (PREV) {  // side (= dz, identity shortcut) through the previous tail's activation derivative
+        float pyv[8], prv[8];
+        load8(a.py + (int64_t)p * a.ldpy + c, pyv);
+        if (a.pkind == ADD_RELU) load8(a.pr + (int64_t)p * a.ldpr + c, prv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int q = cgl * 8 + j;
+          const float t = pyv[j] * s_p[0][q] + s_p[1][q];
+          float f = 0.f, x2 = 0.f;
+          if (a.pkind == ADD_RELU) {
+            f = prv[j];
+            if (a.pr_bn) { x2 = (f - s_p[6][q]) * s_p[7][q]; f = f * s_p[4][q] + s_p[5][q]; }
+          }
+          const float d = (t + f) > 0.f ? side[j] : 0.f;
+          const float x1 = (pyv[j] - s_p[2][q]) * s_p[3][q];
+          q0[j] += d; q1[j] += d * x1; q2[j] += d * x2;
+        }
+      }
     }
     load8(yz + (int64_t)p * a.ldy + c, y);
 #pragma unroll
@@ -402,6 +438,24 @@ __global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = A2[j] * dz[j] + B2[j] * y2[j] + C2[j];
       store8(a.dy2 + a.d2gs * z + (int64_t)p * a.ldd2 + c, o);
+    }
+  }
+  if (PREV) {  // block reduction of the previous tail's partial sums -> fp64 replica chunk % NREP
+    const int lane = threadIdx.x & 63, row = threadIdx.x >> 4;
+    const bool top = (lane & 15) >= 16 - CGB;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float t0 = row_stride_sum<CGB>(q0[j]), t1 = row_stride_sum<CGB>(q1[j]), t2 = row_stride_sum<CGB>(q2[j]);
+      if (top) { s_pp[row][0][cgl * 8 + j] = t0; s_pp[row][1][cgl * 8 + j] = t1; s_pp[row][2][cgl * 8 + j] = t2; }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < 3 * CB; t += BNB_T) {
+      const int k = t / CB, q = t - k * CB;
+      if (k == 2 && !a.pr_bn) continue;
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v += s_pp[r][k][q];
+      atomicAdd(a.ppart + ((int64_t)(chunk % NREP) * 3 + k) * a.C + cblk + q, (double)v);
     }
   }
 }
@@ -530,8 +584,16 @@ int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t 
 
 // fused: 0 = reduce + apply, 1 = single-launch kernel (small maps), 2 = apply only -- the statistics were
 // accumulated into `part` by the epilogue of the dgrad that produced the (single) gradient source.
+// 3 = reduce only: partial statistics over a SUBSET of the gradient sources (the rest are added by their
+// producers), no side / dz / dy outputs -- the tail's own launch is then fused == 2.
 int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, hipStream_t st) {
-  if (fused == 2 && (kind > ACT_SIGMOID || a.dzbuf || a.g.n != 1)) return -5;
+  if (fused == 2 && (kind == SIGMUL || kind == POOL_RELU || a.dzbuf)) return -5;
+  if (fused == 3 && (a.dzbuf || a.dy || a.side || a.dgamma || a.dbeta)) return -5;
+  if (a.ppart && (kind != ADD_RELU || a.r_bn || G != 1 || !a.side || fused != 2 || !a.py ||
+                  (a.pkind != ADD_RELU && a.pkind != ACT_RELU) || (a.pkind == ADD_RELU && !a.pr)))
+    return -6;
+  TailArgs b = a;
+  b.apply_side = fused == 2;
   if (fused == 1) {
     const int M = a.B * a.H * a.W;
     const int R = (M + FUSED_T - 1) / FUSED_T;
@@ -557,8 +619,10 @@ int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, h
   const int cgb = bnb_cgb(a.C);
   dim3 grid(nchunk, a.C / (8 * cgb), G);
 #define KC(X, CG)                                                                                    \
-  if (fused != 2) hipLaunchKernelGGL((bnb_reduce_kernel<X, CG>), grid, dim3(BNB_T), 0, st, a);       \
-  hipLaunchKernelGGL((bnb_apply_kernel<X, CG>), grid, dim3(BNB_T), 0, st, a);
+  if (fused != 2) hipLaunchKernelGGL((bnb_reduce_kernel<X, CG>), grid, dim3(BNB_T), 0, st, b);       \
+  if (fused == 3) break;                                                                             \
+  if (X == ADD_RELU && b.ppart) hipLaunchKernelGGL((bnb_apply_kernel<X, CG, (X == ADD_RELU)>), grid, dim3(BNB_T), 0, st, b); \
+  else hipLaunchKernelGGL((bnb_apply_kernel<X, CG, false>), grid, dim3(BNB_T), 0, st, b);
 #define K(X)                                                   \
   case X:                                                      \
     if (cgb == 1) { KC(X, 1) } else if (cgb == 2) { KC(X, 2) } \

@@ -157,12 +157,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   constexpr int FN = WN / 16, FM = WM / 16;
   constexpr int BN_T = WN * WAVES_N, BM_T = WM * WAVES_M;
   constexpr int TILE = FN * FM * 4 * 64;  // floats per wave accumulator tile
-  constexpr int RED = (KSPLIT - 1) * WAVES_N * WAVES_M * TILE, ST2 = WAVES_M * BN_T * 2;
+  constexpr int RED = (KSPLIT - 1) * WAVES_N * WAVES_M * TILE, ST2 = WAVES_M * BN_T * 3;
   extern __shared__ __attribute__((aligned(16))) int s_dyn[];
   int* s_tab = s_dyn;  // [Kpad/8]
   const int nkg = a.Kpad >> 3;
   float* s_red = reinterpret_cast<float*>(s_dyn + ((nkg + 3) & ~3));  // KSPLIT partials, then stats
-  float* s_bn = s_red + (RED > ST2 ? RED : ST2);  // [4][BN_T] fused BN-backward: scale, shift, mean, invstd
+  float* s_bn = s_red + (RED > ST2 ? RED : ST2);  // [8][BN_T] fused BN-backward: scale, shift, mean, invstd
+                                                  // of the tail's BN, then of its residual's BN2
   float* s_nol = s_bn;                             // [2][Cs] normalise-on-load scale, shift (forward only)
   const int z = blockIdx.z;
   const int Ktot = a.KH * a.KW * a.Cs;
@@ -170,12 +171,18 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // MODE_DGRAD_BNS: dgrad + fused BN-backward statistics -- its own instantiation, so the extra registers
   // never lower the occupancy of the plain dgrads (104 -> 142 VGPRs measured when they shared one)
   constexpr bool want_bnb = has_bns<MODE>();
+  const int bN = a.bN > 0 ? a.bN : a.N;  // the tail's channels (a concat gradient has more)
+  const int zb = a.bpgs == 0 ? 0 : z;    // one tail shared by every group: its constants are group 0's
   if (want_bnb) {
     for (int i = threadIdx.x; i < BN_T; i += 256) {
       const int n = blockIdx.y * BN_T + i;
-      float sc = 0.f, sh = 0.f, mu = 0.f, inv = 0.f;
-      if (n < a.N) bn_channel_bwd(a.bbn, z, n, sc, sh, mu, inv);
-      s_bn[i] = sc; s_bn[BN_T + i] = sh; s_bn[2 * BN_T + i] = mu; s_bn[3 * BN_T + i] = inv;
+      float k[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (n < bN) {
+        bn_channel_bwd(a.bbn, zb, n, k[0], k[1], k[2], k[3]);
+        if (a.br_bn) bn_channel_bwd(a.bbn2, zb, n, k[4], k[5], k[6], k[7]);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s_bn[q * BN_T + i] = k[q];
     }
   }
   // MODE_FWD_NOL: the input is the previous conv's pre-BN y; its BN constants for all Cs channels go to
@@ -188,7 +195,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // fused statistics (rows 0/1 of ao.part) and the BN constants give dy = A*dz + B*y + C; block (0, 0)
   // writes d(gamma), d(beta) and the coefficient table the weight gradient uses.
   constexpr bool AOL = has_aol<MODE>();
-  float* s_aol = s_bn + (want_bnb ? 4 * BN_T : 0);  // [5][Cs], after the fused-statistics constants
+  float* s_aol = s_bn + (want_bnb ? 8 * BN_T : 0);  // [5][Cs], after the fused-statistics constants
   if (AOL) {
     const AolArgs& o = a.ao;
     const int C = a.Cs;
@@ -256,16 +263,21 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // for small tiles; for large ones loaded at the epilogue (when the K-loop buffers are dead), so the
   // prefetch does not cost occupancy
   constexpr bool PREFETCH_Y = want_bnb && FN * FM <= 4;
-  uint2 ypre[FN][FM];
+  const bool bres = want_bnb && a.bkind == ADD_RELU;  // residual tail: its r' enters the dz mask
+  uint2 ypre[FN][FM], rpre[FN][FM];
   auto load_y = [&]() {
 #pragma unroll
     for (int i = 0; i < FN; ++i)
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
         ypre[i][f] = make_uint2(0, 0);
+        rpre[i][f] = make_uint2(0, 0);
         const int n0 = n_base + i * 16 + 4 * kgl;
-        if (wk == 0 && n0 < a.N && pv[f])
-          ypre[i][f] = *reinterpret_cast<const uint2*>(a.by + a.bygs * z + (int64_t)(m_base + f * 16 + l16) * a.ldby + n0);
+        const int64_t m = m_base + f * 16 + l16;
+        if (wk == 0 && n0 < bN && pv[f]) {
+          ypre[i][f] = *reinterpret_cast<const uint2*>(a.by + a.bygs * z + m * a.ldby + n0);
+          if (bres) rpre[i][f] = *reinterpret_cast<const uint2*>(a.br + a.brgs * z + m * a.ldbr + n0);
+        }
       }
   };
   if (PREFETCH_Y) load_y();
@@ -323,7 +335,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // ---------------------------------------------------------------- epilogue
   // BN partial sums are reduced across the block's pixel-waves in LDS and published with ONE atomic per
   // (channel, statistic) per block into replica blockIdx.x % NREP.
-  float* s_st = s_red;  // [WAVES_M][BN_T][2]
+  float* s_st = s_red;  // [WAVES_M][BN_T][3]
   const bool want_stats = is_fwd<MODE>() && a.stats != nullptr;
   const bool want_red = want_stats || want_bnb;
   if (want_bnb && !PREFETCH_Y) load_y();
@@ -337,7 +349,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) bias[r] = a.bias[a.bgs * z + n0 + r];
       }
-      float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+      float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
         const int m = m_base + f * 16 + l16;
@@ -356,24 +368,34 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
           } else {
             float* o = reinterpret_cast<float*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
             *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-            if (want_bnb) {  // dz of the BN tail whose output gradient this is, and its statistics
-              const uint2 u = ypre[i][f];
+            if (want_bnb && n0 < bN) {  // dz of the BN tail this gradient feeds, and its statistics
+              const uint2 u = ypre[i][f], q = rpre[i][f];
               const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
                                    __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+              const float rv[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                                   __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u)};
               const int cl = wn * WN + i * 16 + 4 * kgl;
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float t = yv[r] * s_bn[cl + r] + s_bn[BN_T + cl + r];
-                float dz = v[r];
+                float dz = v[r], xh2 = 0.f;
                 if (a.bkind == ACT_RELU) {
                   dz = t > 0.f ? dz : 0.f;
                 } else if (a.bkind == ACT_SIGMOID) {
                   const float sg = sigmoidf_(t);
                   dz *= sg * (1.f - sg);
+                } else if (a.bkind == ADD_RELU) {
+                  float rr = rv[r];
+                  if (a.br_bn) {
+                    xh2 = (rr - s_bn[6 * BN_T + cl + r]) * s_bn[7 * BN_T + cl + r];
+                    rr = rr * s_bn[4 * BN_T + cl + r] + s_bn[5 * BN_T + cl + r];
+                  }
+                  dz = (t + rr) > 0.f ? dz : 0.f;
                 }
                 const float xh = (yv[r] - s_bn[2 * BN_T + cl + r]) * s_bn[3 * BN_T + cl + r];
                 s[r] += dz;
                 ss[r] += dz * xh;
+                s2[r] += dz * xh2;
               }
             }
           }
@@ -384,13 +406,15 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         for (int r = 0; r < 4; ++r) {  // pixels of a 16-lane row -> lane 15 (DPP, common.h)
           s[r] = row16_sum(s[r]);
           ss[r] = row16_sum(ss[r]);
+          if (bres) s2[r] = row16_sum(s2[r]);
         }
         if (l16 == 15) {
           const int cl = wn * WN + i * 16 + 4 * kgl;  // channel within the block tile
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            s_st[(wm * BN_T + cl + r) * 2 + 0] = s[r];
-            s_st[(wm * BN_T + cl + r) * 2 + 1] = ss[r];
+            s_st[(wm * BN_T + cl + r) * 3 + 0] = s[r];
+            s_st[(wm * BN_T + cl + r) * 3 + 1] = ss[r];
+            s_st[(wm * BN_T + cl + r) * 3 + 2] = s2[r];
           }
         }
       }
@@ -399,17 +423,21 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   if (want_red) {
     __syncthreads();
     const int rep = blockIdx.x % NREP;
-    // forward: [G][NREP][2][N] (sum y, sum y^2); fused BN backward: rows 0/1 of [G][NREP][3][N]
+    // forward: [G][NREP][2][N] (sum y, sum y^2); fused BN backward: rows 0/1 (2 with a BN2 residual) of
+    // the tail's [G][NREP][3][bN]
+    const int nrow = want_bnb ? (a.br_bn ? 3 : 2) : 2;
+    const int nlim = want_bnb ? bN : a.N;
+    const int64_t gb = want_bnb ? (a.bpgs < 0 ? (int64_t)z * NREP * 3 * bN : (int64_t)z * a.bpgs)
+                                : (int64_t)z * NREP * 2 * a.N;
     double* dst = want_bnb ? a.bpart : a.stats;
-    const int rows = want_bnb ? 3 : 2;
-    for (int q = threadIdx.x; q < BN_T * 2; q += 256) {
-      const int cl = q >> 1, which = q & 1;
+    for (int q = threadIdx.x; q < BN_T * 3; q += 256) {
+      const int cl = q / 3, which = q - cl * 3;
       const int n = blockIdx.y * BN_T + cl;
-      if (n < a.N) {
+      if (n < nlim && which < nrow) {
         float v = 0.f;
 #pragma unroll
-        for (int w2 = 0; w2 < WAVES_M; ++w2) v += s_st[(w2 * BN_T + cl) * 2 + which];
-        atomicAdd(dst + ((int64_t)z * NREP + rep) * rows * a.N + which * a.N + n, (double)v);
+        for (int w2 = 0; w2 < WAVES_M; ++w2) v += s_st[(w2 * BN_T + cl) * 3 + which];
+        atomicAdd(dst + gb + ((int64_t)rep * (want_bnb ? 3 : 2) + which) * nlim + n, (double)v);
       }
     }
   }
@@ -871,9 +899,9 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
   {                                                                                                     \
     constexpr int TILE = (WN / 16) * (WM / 16) * 4 * 64;                                                \
     size_t red = (size_t)(KS - 1) * WAN * WAM * TILE;                                                   \
-    size_t st2 = (size_t)WAM * WN * WAN * 2;                                                            \
+    size_t st2 = (size_t)WAM * WN * WAN * 3;                                                            \
     size_t lds = (size_t)nkg4 * 4 + (red > st2 ? red : st2) * 4 +                                        \
-                 (a.nol ? 2 * a.Cs * 4 : (a.bpart ? 4 * WN * WAN * 4 : 0) + (a.aol ? 5 * a.Cs * 4 : 0));    \
+                 (a.nol ? 2 * a.Cs * 4 : (a.bpart ? 8 * WN * WAN * 4 : 0) + (a.aol ? 5 * a.Cs * 4 : 0));    \
     dim3 grid((M + WM * WAM - 1) / (WM * WAM), (a.N + WN * WAN - 1) / (WN * WAN), G);                    \
     hipLaunchKernelGGL((conv_igemm_kernel<MODE, WN, WM, WAN, WAM, KS>), grid, dim3(256), lds, st, a);   \
     break;                                                                                              \

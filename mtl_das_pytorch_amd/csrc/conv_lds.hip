@@ -68,9 +68,9 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
   bf16_t* s_buf = reinterpret_cast<bf16_t*>(smem);
   int* s_tx = reinterpret_cast<int*>(smem + 2 * BUF * 2);  // input coordinates / channel per k-group
   int* s_tw = s_tx + pl.ntab;                              // weight column per k-group
-  float* s_st = reinterpret_cast<float*>(s_tw + pl.ntab);  // [WAM][BN][2] epilogue sums
-  float* s_k = s_st + WAM * BN * 2;                         // NOL: [2][Cs] / BNS: [4][BN] constants
-  int* s_flag = reinterpret_cast<int*>(s_k + (NOL ? 2 * a.Cs : (BNS ? 4 * BN : 0)));
+  float* s_st = reinterpret_cast<float*>(s_tw + pl.ntab);  // [WAM][BN][3] epilogue sums
+  float* s_k = s_st + WAM * BN * 3;                         // NOL: [2][Cs] / BNS: [8][BN] constants
+  int* s_flag = reinterpret_cast<int*>(s_k + (NOL ? 2 * a.Cs : (BNS ? 8 * BN : 0)));
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, kgl = lane >> 4;
@@ -115,12 +115,18 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
     }
   }
   if (NOL) bn_prepare(a.nbn, z, s_k, s_k + a.Cs, nullptr, nullptr, blockIdx.x == 0 && blockIdx.y == 0);
+  const int bN = a.bN > 0 ? a.bN : a.N;  // fused BN statistics: the tail's channels, its group
+  const int zb = a.bpgs == 0 ? 0 : z;
   if (BNS) {
     for (int i = tid; i < BN; i += 256) {
       const int n = nbase + i;
-      float sc = 0.f, sh = 0.f, mu = 0.f, inv = 0.f;
-      if (n < a.N) bn_channel_bwd(a.bbn, z, n, sc, sh, mu, inv);
-      s_k[i] = sc; s_k[BN + i] = sh; s_k[2 * BN + i] = mu; s_k[3 * BN + i] = inv;
+      float k[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (n < bN) {
+        bn_channel_bwd(a.bbn, zb, n, k[0], k[1], k[2], k[3]);
+        if (a.br_bn) bn_channel_bwd(a.bbn2, zb, n, k[4], k[5], k[6], k[7]);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s_k[q * BN + i] = k[q];
     }
   }
 
@@ -309,7 +315,7 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) bias[r] = a.bias[a.bgs * z + n0 + r];
     }
-    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
       if (!(nok && pv[f])) continue;
@@ -327,23 +333,35 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
       } else {
         float* o = reinterpret_cast<float*>(a.out) + a.ogs * z + (int64_t)orow[f] * a.ldo + n0;
         *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-        if (BNS) {  // dz of the BN tail whose output gradient this is, and its statistics
+        if (BNS && n0 < bN) {  // dz of the BN tail this gradient feeds, and its statistics
           const uint2 u = *reinterpret_cast<const uint2*>(a.by + a.bygs * z + (int64_t)orow[f] * a.ldby + n0);
           const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
                                __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+          uint2 q = make_uint2(0, 0);
+          if (a.bkind == ADD_RELU) q = *reinterpret_cast<const uint2*>(a.br + a.brgs * z + (int64_t)orow[f] * a.ldbr + n0);
+          const float rv[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                               __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u)};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float t = yv[r] * s_k[cl + r] + s_k[BN + cl + r];
-            float dz = v[r];
+            float dz = v[r], xh2 = 0.f;
             if (a.bkind == ACT_RELU) {
               dz = t > 0.f ? dz : 0.f;
             } else if (a.bkind == ACT_SIGMOID) {
               const float sg = sigmoidf_(t);
               dz *= sg * (1.f - sg);
+            } else if (a.bkind == ADD_RELU) {
+              float rr = rv[r];
+              if (a.br_bn) {
+                xh2 = (rr - s_k[6 * BN + cl + r]) * s_k[7 * BN + cl + r];
+                rr = rr * s_k[4 * BN + cl + r] + s_k[5 * BN + cl + r];
+              }
+              dz = (t + rr) > 0.f ? dz : 0.f;
             }
             const float xh = (yv[r] - s_k[2 * BN + cl + r]) * s_k[3 * BN + cl + r];
             s[r] += dz;
             ss[r] += dz * xh;
+            s2[r] += dz * xh2;
           }
         }
       }
@@ -353,12 +371,14 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
       for (int r = 0; r < 4; ++r) {  // the 16 pixels of a lane row -> lane 15 (DPP, common.h)
         s[r] = row16_sum(s[r]);
         ss[r] = row16_sum(ss[r]);
+        if (BNS) s2[r] = row16_sum(s2[r]);
       }
       if (l16 == 15) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          s_st[(wm * BN + cl + r) * 2 + 0] = s[r];
-          s_st[(wm * BN + cl + r) * 2 + 1] = ss[r];
+          s_st[(wm * BN + cl + r) * 3 + 0] = s[r];
+          s_st[(wm * BN + cl + r) * 3 + 1] = ss[r];
+          s_st[(wm * BN + cl + r) * 3 + 2] = s2[r];
         }
       }
     }
@@ -367,15 +387,17 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
     __syncthreads();
     const int rep = blockIdx.x % NREP;
     double* dst = BNS ? a.bpart : a.stats;
-    const int rows = BNS ? 3 : 2;
-    for (int q = tid; q < BN * 2; q += 256) {
-      const int c = q >> 1, which = q & 1;
+    const int rows = BNS ? 3 : 2, nrow = BNS && a.br_bn ? 3 : 2, nlim = BNS ? bN : a.N;
+    const int64_t gb = BNS ? (a.bpgs < 0 ? (int64_t)z * NREP * 3 * bN : (int64_t)z * a.bpgs)
+                           : (int64_t)z * NREP * 2 * a.N;
+    for (int q = tid; q < BN * 3; q += 256) {
+      const int c = q / 3, which = q - c * 3;
       const int n = nbase + c;
-      if (n < a.N) {
+      if (n < nlim && which < nrow) {
         float v = 0.f;
 #pragma unroll
-        for (int w2 = 0; w2 < WAM; ++w2) v += s_st[(w2 * BN + c) * 2 + which];
-        atomicAdd(dst + ((int64_t)z * NREP + rep) * rows * a.N + which * a.N + n, (double)v);
+        for (int w2 = 0; w2 < WAM; ++w2) v += s_st[(w2 * BN + c) * 3 + which];
+        atomicAdd(dst + gb + ((int64_t)rep * rows + which) * nlim + n, (double)v);
       }
     }
   }
@@ -454,7 +476,7 @@ int launch_mode(const ConvArgs& a, int G, const LdsCfg& c, hipStream_t st) {
   if (c.splits > 1 && (!a.ws || !a.cnt)) return -3;
   const bool nol = MODE == MODE_FWD_NOL, bns = MODE == MODE_DGRAD_BNS;
   const size_t lds = (size_t)2 * (c.BM + c.BN) * c.KC * 2 + (size_t)2 * pl.ntab * 4 +
-                     ((size_t)c.WAM * c.BN * 2 + (nol ? 2 * a.Cs : (bns ? 4 * c.BN : 0))) * 4 + 16;
+                     ((size_t)c.WAM * c.BN * 3 + (nol ? 2 * a.Cs : (bns ? 8 * c.BN : 0))) * 4 + 16;
   if (lds > 160 * 1024) return -2;
   dim3 grid(gx, ntn * c.splits, G);
 #define LDS_LAUNCH(T, KC_)                                                                               \

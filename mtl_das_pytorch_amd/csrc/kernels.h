@@ -47,6 +47,16 @@ struct ConvArgs {
   BNArgs bbn;
   double* bpart;
   int bkind;
+  // ... generalised to ONE OF SEVERAL gradient sources (statistics are linear in the gradient, so every
+  // producer adds its share): bkind ACT_RELU or ADD_RELU, whose dz mask is relu'(BN(y) + r') with the
+  // residual r' = r (identity shortcut) or BN2(r) (projection, br_bn = 1: third row sum(dz * xhat2)).
+  // bN = the tail's channels (a concatenation gradient may have more: channels >= bN are not the tail's),
+  // bpgs = group stride of bpart (-1: z * NREP * 3 * bN; 0: every group adds into the ONE tail of a
+  // shared feature, whose BN constants are then group 0's).
+  const bf16_t* br; int64_t brgs; int ldbr;
+  BNArgs bbn2;
+  int br_bn, bN;
+  int64_t bpgs;
   // FWD only, optional (nol = 0 off): normalise-on-load.  The (single-segment) input is the previous
   // conv's pre-BN output y and the im2col operand is act(BN(y)) computed on load (act = nol_kind: ACT_NONE
   // or ACT_RELU), so the forward BN tail that materialised act(BN(y)) is not launched.  Block (0, 0) of each
@@ -144,6 +154,18 @@ struct TailArgs {
   bf16_t* dy2; int64_t d2gs; int ldd2;
   float* dgamma; float* dbeta; float* dgamma2; float* dbeta2; int64_t pgs;
   uint64_t* tsc;                    // optional phase timestamps (profiling; null in production)
+  // apply-only backward (fused = 2) of a multi-source tail: no reduce pass ran, so the apply pass stores
+  // the side output itself (apply_side)
+  int apply_side;
+  // apply pass, optional (ppart non-null, ADD_RELU with identity shortcut): the side output dz is also a
+  // gradient source of the PREVIOUS tail (the block input's own ACT_RELU / ADD_RELU tail, same pixel grid
+  // and channels): accumulate that tail's partial statistics sum(dz'), sum(dz' xhat'), sum(dz' xhat2')
+  // with dz' = side * relu'(BN(py) + pr') into ppart ([NREP][3][C], group 0)
+  const bf16_t* py; int ldpy;
+  const bf16_t* pr; int ldpr;
+  BNArgs pbn, pbn2;
+  int pkind, pr_bn;
+  double* ppart;
 };
 
 struct HeadArgs {

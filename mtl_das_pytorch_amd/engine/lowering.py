@@ -94,10 +94,14 @@ class LoweredProgram:
         ph.add(f"tail{kind}", k_tail_fwd, kind, G, _blocks(M, y.C, per_thread=2), d)
 
     def _tail_bwd(self, ph: Phase, kind: int, G: int, y: Act, bn: BNLayer, g: list, dy: Act, r: Act = None,
-                  bn2: BNLayer = None, side: Act = None, dy2: Act = None):
+                  bn2: BNLayer = None, side: Act = None, dy2: Act = None, apply_only: bool = False):
+        """BN-tail backward launch.  ``apply_only``: the tail's statistics are accumulated by the producers
+        of its gradient sources (and partial reduces, ``_tail_partial``), so only the apply pass runs."""
         d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(True), "B": self.B, "H": y.H, "W": y.W, "C": y.C,
              "g": g, "part": P(bn.part), "chunk_px": bn.chunk_px, "dy": dy.p, "dgs": dy.gs, "ldd": dy.ld}
-        if kind in (SIGMUL, POOL_RELU) or len(g) > 1:
+        if apply_only:
+            d["fused"] = 2
+        elif kind in (SIGMUL, POOL_RELU) or len(g) > 1:
             # the apply pass reads the stored dz instead of re-reading several gradient sources /
             # re-evaluating the pool window
             if bn.dzbuf is None:
@@ -115,6 +119,30 @@ class LoweredProgram:
         if bn.count != y.M:
             raise ValueError("BN backward chunking assumes the BN count equals the tail's pixel count")
         ph.add(f"tailbwd{kind}", k_tail_bwd, kind, G, bn.nchunk, d)
+
+    def _tail_partial(self, ph: Phase, kind: int, y: Act, bn: BNLayer, g: list, r: Act = None, bn2: BNLayer = None,
+                      stream: int = 0, waits=(), record=None):
+        """Reduce-only launch (csrc/bn.hip fused = 3): the statistics sum(dz), sum(dz xhat) (, sum(dz xhat2))
+        of a G = 1 tail over the gradient sources ``g`` only, accumulated into the tail's replica rows; the
+        tail's other sources add theirs in their producers' epilogues and the tail runs apply-only."""
+        d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(True), "B": self.B, "H": y.H, "W": y.W, "C": y.C,
+             "g": g, "part": P(bn.part), "chunk_px": bn.chunk_px, "fused": 3}
+        if r is not None:
+            d.update({"r": r.p, "rgs": r.gs, "ldr": r.ld})
+        if bn2 is not None:
+            d["bn2"] = bn2.args(True)
+        ph.add(f"tailpart{kind}", k_tail_bwd, kind, 1, bn.nchunk, d, stream=stream, waits=waits, record=record)
+
+    @staticmethod
+    def _tail_stats_args(kind: int, y: Act, bn: BNLayer, r: Act = None, bn2: BNLayer = None) -> dict:
+        """Producer-side description of a G = 1 BN tail whose statistics a gradient producer accumulates:
+        ConvArgs::bnb of a dgrad (csrc/conv.hip) or TailArgs::prev of an apply pass (csrc/bn.hip)."""
+        d = {"y": y.p, "ygs": 0, "ldy": y.ld, "bn": bn.args(True), "part": P(bn.part), "kind": kind, "C": y.C}
+        if r is not None:
+            d.update({"r": r.p, "rgs": 0, "ldr": r.ld})
+        if bn2 is not None:
+            d["bn2"] = bn2.args(True)
+        return d
 
     @staticmethod
     def nol_enabled() -> bool:

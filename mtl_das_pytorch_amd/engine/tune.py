@@ -134,7 +134,7 @@ def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, ve
             if not launch.name.startswith("tailbwd"):
                 continue
             kind, G, blocks, d = launch.args
-            if d.get("fused") == 2:  # statistics come from the producing dgrad: apply pass only
+            if d.get("fused") in (2, 3):  # statistics from the producers (apply only) / a partial reduce
                 continue
             sig = tail_bwd_signature(kind, G, d)
             if sig not in cache and not measure:

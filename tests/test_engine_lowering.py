@@ -6,7 +6,8 @@ from mtl_das_pytorch_amd.engine.mtl import MTLProgram
 from mtl_das_pytorch_amd.models import MTL_Net, Single_Task_Net
 
 
-def test_mtl_program_structure():
+def test_mtl_program_structure(monkeypatch):
+    monkeypatch.setenv("MDA_MSBNS", "1")  # opt-in multi-source BN statistics (checked below)
     m = MTL_Net()
     sd_before = {k: v.clone() for k, v in m.state_dict().items()}
     p = MTLProgram(m, 32, "cpu")
@@ -16,7 +17,16 @@ def test_mtl_program_structure():
     assert p.flat.numel >= sum(x.numel() for x in m.parameters())
     n = p.num_launches()
     # forward: 12 BN+ReLU tails are folded into their consumer conv (normalise-on-load)
-    assert n["forward_train"] == 48 and n["backward"] == 90
+    assert n["forward_train"] == 48 and n["backward"] == 98
+    # multi-source BN statistics (MDA_MSBNS): one reduce-only launch per residual tail on stream 2, every
+    # residual tail and conv1's tail apply-only, their producers carry the statistics descriptors
+    parts = [l for l in p.bwd.launches if l.name.startswith("tailpart")]
+    assert len(parts) == 8 and all(l.stream == 2 and l.args[3]["fused"] == 3 for l in parts)
+    tails = [l for l in p.bwd.launches if l.name == "tailbwd4"]
+    assert len(tails) == 8 and all(l.args[3]["fused"] == 2 and "dzbuf" not in l.args[3] for l in tails)
+    assert [R["ca_dgrad"].args[3]["bnb"]["kind"] for R in p.rbs] == [1] + [4] * 7
+    assert [("prev" in R["tail_bwd"].args[3]) for R in p.rbs] == [not R["proj"] for R in p.rbs]
+    assert all("bn2" in R["ca_dgrad"].args[3]["bnb"] for j, R in enumerate(p.rbs) if j and p.rbs[j - 1]["proj"])
     # both task branches of a level are ONE grouped launch with an even parameter stride
     L = p.levels[1]
     assert L["c0"].G == 2 and L["c0"].wstride > 0
@@ -133,6 +143,7 @@ def test_dgrad_fused_bn_stats_wiring(monkeypatch):
     from mtl_das_pytorch_amd.engine.inception import InceptionProgram
     from mtl_das_pytorch_amd.models import Multi_Classifier
     monkeypatch.setenv("MDA_AOL", "0")  # keep the apply-only tails in the program
+    monkeypatch.setenv("MDA_MSBNS", "0")  # single-source tails only (multi-source: test_mtl_program_structure)
     p = MTLProgram(MTL_Net(), 8, "cpu")
     assert p.n_dgrad_bnstats == 12
     fused = [l for l in p.bwd.launches if l.name.startswith("tailbwd") and l.args[3].get("fused") == 2]
@@ -154,6 +165,7 @@ def test_apply_on_load_wiring(monkeypatch):
     from mtl_das_pytorch_amd.engine.inception import InceptionProgram
     from mtl_das_pytorch_amd.models import Multi_Classifier
     monkeypatch.setenv("MDA_AOL", "1")  # opt-in
+    monkeypatch.setenv("MDA_MSBNS", "1")
     for p in (MTLProgram(MTL_Net(), 8, "cpu"), InceptionProgram(Multi_Classifier(), 4, "cpu")):
         ls = p.bwd.launches
         assert p.n_aol > 0 and p.n_aol <= p.n_dgrad_bnstats
@@ -168,9 +180,10 @@ def test_apply_on_load_wiring(monkeypatch):
             assert a["dgamma"] and a["dbeta"] and a["part"]
         _check_event_order(p.bwd)
     p = MTLProgram(MTL_Net(), 8, "cpu")
+    # every single-source apply-only tail is folded; the multi-source ones (MDA_MSBNS) stay
     assert p.n_aol == 12 and not any(l.name.startswith("tailbwd") and l.args[3].get("fused") == 2
-                                     for l in p.bwd.launches)
-    assert p.num_launches()["backward"] == 90 - 12
+                                     and len(l.args[3]["g"]) == 1 for l in p.bwd.launches)
+    assert p.num_launches()["backward"] == 98 - 12
     monkeypatch.setenv("MDA_AOL", "pw")
     c = InceptionProgram(Multi_Classifier(), 4, "cpu")
     assert 0 < c.n_aol < 43 and all(l.args[3]["KH"] * l.args[3]["KW"] == 1 for l in c.bwd.launches

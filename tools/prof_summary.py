@@ -8,8 +8,9 @@ import sys
 
 d = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 24
-if os.path.exists(f"{d}/run_kernel_trace.csv"):
-    rows = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
+traces = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)
+if traces:
+    rows = [r for t in traces for r in csv.DictReader(open(t))]
 else:  # rocprofv3's default rocpd (SQLite) output
     db = sqlite3.connect(glob.glob(f"{d}/**/*.db", recursive=True)[0])
     rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
