@@ -1,0 +1,223 @@
+"""Model A (MTL_Net) backward, layer by layer, against the closed-form / autograd math of each single op.
+
+Every op of the lowered backward (engine/mtl.py ``_emit_backward``: residual tails ADD_RELU with identity
+or projection shortcut, the inner BN+ReLU tails, every conv's data and weight gradient, the level
+branches' max-pool / sigmoid-mask tails, the two-segment attention-generator input and the MTL head) is
+fed with the ENGINE's own inputs -- its stored bf16 activations, its published BN constants and the sum of
+its gradient sources -- and compared per tensor with fp32 PyTorch math at tolerances set by bf16 output
+rounding, independent of the network's error amplification at init.  The program runs at the bench's
+batch (32) with the tuned kernel configs the bench uses (LDS-staged convs, split-K, fused statistics,
+normalise-on-load).  Reference: model/modelA_MTL.py:7-174.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+# measured worst (MI355X, B = 32): dy 1.7e-3 (bf16 output), dW 3.9e-5, dx 3.3e-7, dgamma 5.5e-7, side 3.2e-8
+TOL = {"dy": 6e-3, "dx": 1e-5, "dW": 2e-4, "dgamma": 1e-5, "dbeta": 1e-5, "side": 1e-6, "dhead": 1e-6}
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-20)).item()
+
+
+def q(t):
+    return t.bfloat16().float()
+
+
+def nchw(a, z=0, c0=0, C=None):
+    """Group z, channels [c0, c0 + C) of an engine NHWC activation as dense fp32 NCHW."""
+    C = a.C - c0 if C is None else C
+    t = a.t.reshape(-1)[a.off + z * a.gs + c0:]
+    M = a.B * a.H * a.W
+    idx = torch.arange(M, device=t.device)[:, None] * a.ld + torch.arange(C, device=t.device)[None]
+    return t[idx].float().view(a.B, a.H, a.W, C).permute(0, 3, 1, 2)
+
+
+def k4(bn, z=0):
+    """(scale, shift, mean, invstd) the forward published for BN layer ``bn`` (group z), NCHW-broadcastable."""
+    return [v.view(1, -1, 1, 1) for v in bn.consts[z]]
+
+
+def bn_backward(dz, y, bn, z=0):
+    """Closed-form training-BN backward on the stored bf16 y with the forward's constants."""
+    _, _, mu, inv = k4(bn, z)
+    gam = bn.mods[z].weight.detach().view(1, -1, 1, 1)
+    xh = (y - mu) * inv
+    dy = gam * inv * (dz - dz.mean((0, 2, 3), keepdim=True) - xh * (dz * xh).mean((0, 2, 3), keepdim=True))
+    return dy, (dz * xh).sum((0, 2, 3)), dz.sum((0, 2, 3))
+
+
+@pytest.fixture(scope="module")
+def engine_step():
+    from mtl_das_pytorch_amd.data.synthetic import generate
+    from mtl_das_pytorch_amd.engine.mtl import MTLProgram
+    from mtl_das_pytorch_amd.engine.tune import autotune_program
+    from mtl_das_pytorch_amd.models import MTL_Net
+    torch.backends.cudnn.allow_tf32 = False  # the fp32 references must be fp32 (MIOpen / hipBLASLt)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.manual_seed(0)
+    B = 32
+    model = MTL_Net()
+    prog = MTLProgram(model, B, "cuda")
+    autotune_program(prog, measure=False)  # the bench's tuned kernel configs
+    X, d, e = generate(B, seed=11, device="cuda")
+    labels = torch.stack([d, e], 1)
+    idx = torch.arange(B, device="cuda")
+    prog.opt["pack"].run()
+    prog.arena.clear()
+    prog.gather_phase(X, labels, idx).run()
+    prog.fwd_train.run()
+    prog.bwd.run()
+    torch.cuda.synchronize()
+    prog.flat.sync_module_grads()
+    return model, prog, X, labels
+
+
+class Checker:
+    def __init__(self):
+        self.worst, self.bad = {}, []
+
+    def __call__(self, kind, what, e, r):
+        err = rel(e, r)
+        self.worst[kind] = max(self.worst.get(kind, 0.0), err)
+        if not err < TOL[kind]:
+            self.bad.append((what, kind, f"{err:.2e}"))
+
+    def exact_zero(self, what, e, ref_noise):
+        self.worst["db_ref_noise"] = max(self.worst.get("db_ref_noise", 0.0), ref_noise)
+        if e.abs().max().item() != 0.0 or not ref_noise < 1e-3:  # noise of sum(dy) over bf16-rounded dy
+            self.bad.append((what, "db", f"engine max {e.abs().max().item():.1e}, reference noise {ref_noise:.1e}"))
+
+    def done(self):
+        print("worst layer-local errors", {k: f"{v:.1e}" for k, v in self.worst.items()})
+        assert not self.bad, self.bad
+
+
+def conv_check(chk, name, conv, z, x, dy, dx_act=None, x_requires=True):
+    """Autograd of the single conv (bf16-rounded weights, the engine's input and dy)."""
+    m = conv.mods[z]
+    x = x.clone().requires_grad_(x_requires and dx_act is not None)
+    w = q(m.weight.detach()).requires_grad_(True)
+    y = F.conv2d(x, w, None, m.stride, m.padding)
+    y.backward(dy)
+    chk("dW", f"{name}.weight", m.weight.grad, w.grad)
+    if m.bias is not None:
+        # every biased conv of Model A feeds a training-mode BN, so d(bias) = sum(dy) = 0 exactly (the BN
+        # backward removes the mean); the engine writes exact zeros, autograd leaves rounding noise
+        db = dy.sum((0, 2, 3))
+        chk.exact_zero(f"{name}.bias", m.bias.grad, db.norm().item() / dy.abs().sum((0, 2, 3)).norm().item())
+    if dx_act is not None:
+        chk("dx", f"{name} dx", dx_act, x.grad)
+
+
+def bn_grads_check(chk, name, bn, z, dgam, dbet):
+    chk("dgamma", f"{name}.weight", bn.mods[z].weight.grad, dgam)
+    chk("dbeta", f"{name}.bias", bn.mods[z].bias.grad, dbet)
+
+
+def test_mtl_backward_layer_local(engine_step):
+    model, prog, X, labels = engine_step
+    chk = Checker()
+    T, lv, rbs = prog.T, prog.levels, prog.rbs
+
+    def sources(k):  # gradient sources of F_k (mirrors MTLProgram._emit_backward)
+        g = 0
+        if k >= 1:
+            L = lv[(k - 1) // 2]
+            for t in range(T):
+                g = g + (nchw(L["dcat"], t, 0, L["C"]) if k % 2 == 1 else nchw(L["dF"], t))
+        if k < 8:
+            R = rbs[k]
+            g = g + nchw(R["dxa"]) + (nchw(R["dxs"]) if R["proj"] else nchw(R["side"]))
+        return g
+
+    # ---- task levels (per task t, group z = t)
+    for li in range(3, -1, -1):
+        L = lv[li]
+        for t in range(T):
+            nm = f"level{li + 1}.task{t}"
+            if "co" in L:
+                nxt = lv[li + 1]
+                g = nchw(nxt["dcat"], t, nxt["Fa"].C, L["co"].Co)   # B_l part of d cat[F, B_l]
+                yo = nchw(L["yo"], t)
+                sc, sh, _, _ = k4(L["bno"], t)
+                zin = (yo * sc + sh).requires_grad_(True)
+                F.max_pool2d(torch.relu(zin), 2, 2, ceil_mode=True).backward(g)
+                dyo, dgam, dbet = bn_backward(zin.grad, yo, L["bno"], t)
+                chk("dy", f"{nm} pool tail dy", nchw(L["dyo"], t), dyo)
+                bn_grads_check(chk, f"{nm}.out_bn", L["bno"], t, dgam, dbet)
+                conv_check(chk, f"{nm}.out_conv", L["co"], t, nchw(L["Aout"], t), nchw(L["dyo"], t), nchw(L["dA"], t))
+            g = nchw(L["dA"], t)
+            ym2, Fb = nchw(L["ym2"], t), nchw(L["Fb"])
+            sc, sh, _, _ = k4(L["bn3"], t)
+            s = torch.sigmoid(ym2 * sc + sh)
+            chk("side", f"{nm} dF", nchw(L["dF"], t), g * s)
+            dym2, dgam, dbet = bn_backward(g * Fb * s * (1 - s), ym2, L["bn3"], t)
+            chk("dy", f"{nm} mask tail dy", nchw(L["dym2"], t), dym2)
+            bn_grads_check(chk, f"{nm}.gen_bn3", L["bn3"], t, dgam, dbet)
+            ym1 = nchw(L["ym1"], t)
+            sc0, sh0, _, _ = k4(L["bn0"], t)
+            hm = q(torch.relu(ym1 * sc0 + sh0))  # normalise-on-load operand of c3
+            conv_check(chk, f"{nm}.gen_conv3", L["c3"], t, hm, nchw(L["dym2"], t), nchw(L["dhm"], t))
+            dym1, dgam, dbet = bn_backward(nchw(L["dhm"], t) * ((ym1 * sc0 + sh0) > 0), ym1, L["bn0"], t)
+            chk("dy", f"{nm} gen tail dy", nchw(L["dym1"], t), dym1)
+            bn_grads_check(chk, f"{nm}.gen_bn0", L["bn0"], t, dgam, dbet)
+            x = nchw(L["Fa"]) if L["prevB"] is None else torch.cat([nchw(L["Fa"]), nchw(L["prevB"], t)], 1)
+            conv_check(chk, f"{nm}.gen_conv0", L["c0"], t, x, nchw(L["dym1"], t), nchw(L["dcat"], t))
+
+    # ---- residual blocks RB8 -> RB1
+    for i in range(7, -1, -1):
+        R = rbs[i]
+        nm = f"resblock{i + 1}"
+        g = sources(i + 1)
+        yb = nchw(R["yb"])
+        sc, sh, _, _ = k4(R["bnb"])
+        if R["proj"]:
+            ys = nchw(R["ys"])
+            sc2, sh2, _, _ = k4(R["bns"])
+            rr = ys * sc2 + sh2
+        else:
+            rr = nchw(R["in"])
+        dz = g * ((yb * sc + sh + rr) > 0)
+        dyb, dgam, dbet = bn_backward(dz, yb, R["bnb"])
+        chk("dy", f"{nm} tail dy", nchw(R["dyb"]), dyb)
+        bn_grads_check(chk, f"{nm}.left.4", R["bnb"], 0, dgam, dbet)
+        if R["proj"]:
+            dys, dgam2, dbet2 = bn_backward(dz, ys, R["bns"])
+            chk("dy", f"{nm} shortcut dy", nchw(R["dys"]), dys)
+            bn_grads_check(chk, f"{nm}.shortcut.1", R["bns"], 0, dgam2, dbet2)
+        else:
+            chk("side", f"{nm} shortcut grad", nchw(R["side"]), dz)
+        ya = nchw(R["ya"])
+        sca, sha, _, _ = k4(R["bna"])
+        ha = q(torch.relu(ya * sca + sha))  # normalise-on-load operand of conv b
+        conv_check(chk, f"{nm}.left.3", R["cb"], 0, ha, nchw(R["dyb"]), nchw(R["dha"]))
+        dya, dgam, dbet = bn_backward(nchw(R["dha"]) * ((ya * sca + sha) > 0), ya, R["bna"])
+        chk("dy", f"{nm} inner tail dy", nchw(R["dya"]), dya)
+        bn_grads_check(chk, f"{nm}.left.1", R["bna"], 0, dgam, dbet)
+        conv_check(chk, f"{nm}.left.0", R["ca"], 0, nchw(R["in"]), nchw(R["dya"]), nchw(R["dxa"]))
+        if R["proj"]:
+            conv_check(chk, f"{nm}.shortcut.0", R["cs"], 0, nchw(R["in"]), nchw(R["dys"]), nchw(R["dxs"]))
+
+    # ---- stem: conv1 tail (sources of f0) and the conv1 weight gradient on the real (unpacked) input
+    y0 = nchw(prog.y0)
+    sc, sh, _, _ = k4(prog.bn1)
+    dy0, dgam, dbet = bn_backward(sources(0) * ((y0 * sc + sh) > 0), y0, prog.bn1)
+    chk("dy", "conv1 tail dy", nchw(prog.dy0), dy0)
+    bn_grads_check(chk, "conv1.1", prog.bn1, 0, dgam, dbet)
+    conv_check(chk, "conv1.0", prog.conv1, 0, q(X), nchw(prog.dy0))
+
+    # ---- head: d loss / d A4 = w_t (softmax - onehot) / (B * group size * HW), broadcast per channel group
+    A4 = lv[3]["Aout"]
+    for t in range(T):
+        K = model.task_cate_num[t]
+        p = prog.logp[t, :, :K].exp()
+        p[torch.arange(prog.B), labels[:, t]] -= 1
+        gsz = A4.C // K
+        scale = prog.loss_weights[t] / (prog.B * gsz * A4.H * A4.W)
+        ref = (p * scale).repeat_interleave(gsz, 1)[:, :, None, None].expand(-1, -1, A4.H, A4.W)
+        chk("dhead", f"head task{t} dA4", nchw(prog.dA4, t), ref)
+    chk.done()
