@@ -84,8 +84,12 @@ __global__ __launch_bounds__(256) void pool3_fwd_kernel(PoolArgs a) {
         load8(a.x + ((int64_t)(b * a.H + ih) * a.W + iw) * a.ldx + cg * 8, v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          if (MAX && v[j] > acc[j]) am[j] = kh * 3 + kw;  // first max in row-major order (torch)
-          acc[j] = MAX ? fmaxf(acc[j], v[j]) : acc[j] + v[j];
+          // torch semantics: first max in row-major order, and a NaN wins (propagates; last NaN's index)
+          if (MAX) {
+            if (v[j] > acc[j] || isnan(v[j])) { acc[j] = v[j]; am[j] = kh * 3 + kw; }
+          } else {
+            acc[j] += v[j];
+          }
         }
       }
     }
@@ -143,7 +147,7 @@ __global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {
               load8(a.x + ((int64_t)(b * a.H + 2 * oh + kh) * a.W + 2 * ow + kw) * a.ldx + cg * 8, v);
 #pragma unroll
               for (int j = 0; j < 8; ++j)
-                if (v[j] > mx[j]) { mx[j] = v[j]; am[j] = kh * 3 + kw; }
+                if (v[j] > mx[j] || isnan(v[j])) { mx[j] = v[j]; am[j] = kh * 3 + kw; }
             }
           float g[8];
           gsum8(a.g, 0, (int64_t)(b * a.Ho + oh) * a.Wo + ow, cg * 8, g);

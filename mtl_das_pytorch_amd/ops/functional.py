@@ -405,7 +405,9 @@ def pool3_backward(x: torch.Tensor, g: torch.Tensor, is_max: bool, am: Optional[
     dx = torch.empty(B, H, W, C, device=x.device, dtype=torch.float32)
     d = {"x": ptr(x), "ldx": C, "g": ptr(g), "ldg": C, "dx": ptr(dx), "lddx": C, "B": B, "H": H, "W": W, "C": C,
          "Ho": Ho, "Wo": Wo}
-    if am is not None:
+    if am is not None:  # the kernel reads the argmax with 8-byte loads per 8-channel group
+        if am.dtype != torch.uint8 or am.numel() != B * Ho * Wo * C or C % 8 or not is_max:
+            raise ValueError("am must be the uint8 [B, Ho, Wo, C] argmax of a max pool with C % 8 == 0")
         d["am"] = ptr(am)
     lib().pool3(int(is_max), 1, stream(), d)
     return dx

@@ -38,8 +38,11 @@ def test_fault_injection_elastic_restart_resumes(tmp_path):
         if r.returncode == 0 or "connectFullMesh failed" not in r.stdout + r.stderr:
             break
         # gloo's full-mesh connect of a restarted group occasionally fails under host load (refused /
-        # timed-out TCP connect in gloo itself); that is not what this test checks: run the scenario again
+        # timed-out TCP connect in gloo itself); that is not what this test checks: run the scenario again,
+        # visibly (a warning in the test report), at most once
         import shutil
+        import warnings
+        warnings.warn("known gloo connectFullMesh flake in the restarted group: re-running the scenario once")
         shutil.rmtree(out, ignore_errors=True)
         port = _free_port()
         cmd[cmd.index("--rdzv-endpoint") + 1] = f"127.0.0.1:{port}"

@@ -406,6 +406,18 @@ def test_inception_pools(fn, is_max):
         dx2 = fn.pool3_backward(nhwc(xt.detach()).bfloat16(), nhwc(go), is_max, am=am)
         assert torch.equal(dx2, fn.pool3_backward(nhwc(xt.detach()).bfloat16(), nhwc(go), is_max))
         assert rel(nchw(dx2), xt.grad) < 1e-5
+        # NaN propagates like torch: the output is NaN and the gradient goes to the NaN's position
+        xn = x.detach().clone()
+        xn[0, 3, 4, 5] = float("nan")
+        xn.requires_grad_(True)
+        rn = F.max_pool2d(xn, 3, 2)
+        rn.backward(go)
+        yn = nchw(fn.pool3(nhwc(xn.detach()).bfloat16(), is_max, am=am))
+        assert torch.equal(torch.isnan(yn), torch.isnan(rn))
+        dxn = nchw(fn.pool3_backward(nhwc(xn.detach()).bfloat16(), nhwc(go), is_max, am=am))
+        assert rel(dxn, xn.grad) < 1e-5
+        with pytest.raises(ValueError):  # the argmax buffer is validated before the kernel reads it
+            fn.pool3_backward(nhwc(x.detach()).bfloat16(), nhwc(go), is_max, am=am[:-8])
 
 
 def test_gather_batch(fn):
