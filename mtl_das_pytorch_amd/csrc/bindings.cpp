@@ -252,6 +252,7 @@ TailArgs parse_tail(const py::dict& d) {
   a.dgamma = P<float>(d, "dgamma"); a.dbeta = P<float>(d, "dbeta");
   a.dgamma2 = P<float>(d, "dgamma2"); a.dbeta2 = P<float>(d, "dbeta2");
   a.pgs = I(d, "pgs");
+  a.gscale = (float)F(d, "gscale", 1.0);
   a.tsc = P<uint64_t>(d, "tsc");
   if (d.contains("prev") && !d["prev"].is_none()) {  // apply pass: partial statistics of the previous tail
     py::dict q = d["prev"].cast<py::dict>();

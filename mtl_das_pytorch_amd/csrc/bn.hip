@@ -381,8 +381,8 @@ __global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
     if (chunk == 0) {
       float* dg = k ? a.dgamma2 : a.dgamma;
       float* db = k ? a.dbeta2 : a.dbeta;
-      if (dg) dg[a.pgs * z + cblk + j] = sx;
-      if (db) db[a.pgs * z + cblk + j] = sd;
+      if (dg) dg[a.pgs * z + cblk + j] = sx * a.gscale;
+      if (db) db[a.pgs * z + cblk + j] = sd * a.gscale;
     }
   }
   __syncthreads();
@@ -587,7 +587,7 @@ int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t 
 // 3 = reduce only: partial statistics over a SUBSET of the gradient sources (the rest are added by their
 // producers), no side / dz / dy outputs -- the tail's own launch is then fused == 2.
 int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, hipStream_t st) {
-  if (fused == 2 && (kind == SIGMUL || kind == POOL_RELU || a.dzbuf)) return -5;
+  if (fused == 2 && a.dzbuf) return -5;  // apply-only recomputes dz from the sources (every kind)
   if (fused == 3 && (a.dzbuf || a.dy || a.side || a.dgamma || a.dbeta)) return -5;
   if (a.ppart && (kind != ADD_RELU || a.r_bn || G != 1 || !a.side || fused != 2 || !a.py ||
                   (a.pkind != ADD_RELU && a.pkind != ACT_RELU) || (a.pkind == ADD_RELU && !a.pr)))
@@ -595,6 +595,7 @@ int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, h
   TailArgs b = a;
   b.apply_side = fused == 2;
   if (fused == 1) {
+    if (a.gscale != 1.f) return -5;
     const int M = a.B * a.H * a.W;
     const int R = (M + FUSED_T - 1) / FUSED_T;
     // register-cached pixels per thread: up to 4 (2 for the two-BN residual tail) without spilling

@@ -157,6 +157,7 @@ struct TailArgs {
   // apply-only backward (fused = 2) of a multi-source tail: no reduce pass ran, so the apply pass stores
   // the side output itself (apply_side)
   int apply_side;
+  float gscale;                     // factor on the d(gamma), d(beta) the apply writes (SyncBN: 1 / world)
   // apply pass, optional (ppart non-null, ADD_RELU with identity shortcut): the side output dz is also a
   // gradient source of the PREVIOUS tail (the block input's own ACT_RELU / ADD_RELU tail, same pixel grid
   // and channels): accumulate that tail's partial statistics sum(dz'), sum(dz' xhat'), sum(dz' xhat2')

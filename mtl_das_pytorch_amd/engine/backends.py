@@ -195,7 +195,7 @@ class EngineBackend(Backend):
     def __init__(self, model: nn.Module, model_type: str, X: torch.Tensor, labels: torch.Tensor,
                  X_eval: torch.Tensor, labels_eval: torch.Tensor, ctx: DistContext, batch: int, lr: float,
                  weight_decay: float, loss_weights: Sequence[float] = (1.0, 1.0), use_graph: bool = True,
-                 tune: bool = False, seed: int = 0):
+                 tune: bool = False, seed: int = 0, sync_bn: bool = False):
         from .inception import InceptionProgram
         from .mtl import MTLProgram
         from .step import StepRunner
@@ -203,11 +203,15 @@ class EngineBackend(Backend):
         self.model_type = model_type
         self.ctx = ctx
         self.names, self.ncls = _report_tasks(model_type)
+        sw = ctx.world if (sync_bn and ctx.enabled) else 1
         if model_type == "multi_classifier":
-            self.prog = InceptionProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]))
+            self.prog = InceptionProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), sync_world=sw)
         else:
             w = list(loss_weights) if model_type == "MTL" else [1.0]
-            self.prog = MTLProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), loss_weights=w)
+            self.prog = MTLProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), loss_weights=w, sync_world=sw)
+        if sw > 1:  # SyncBN: BN statistics all-reduced inside the step, which then runs eagerly
+            self.prog.enable_sync_bn(lambda t: ctx.all_reduce_(t))
+            use_graph = False
         self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world)
         if hasattr(self.prog, "set_rng_stream"):
             self.prog.set_rng_stream(seed, ctx.rank)

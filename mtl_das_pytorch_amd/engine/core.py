@@ -101,6 +101,10 @@ class FlatState:
             m.running_mean = rm
             m.running_var = rv
             m.num_batches_tracked = nb
+        # SyncBN (engine.lowering enable_sync_bn): BN batch statistics span this many ranks; every BNLayer
+        # of the program registers itself here
+        self.bn_world = 1
+        self.bn_layers: List["BNLayer"] = []
         # Adam device scalars: [lr, step]
         self.lr = torch.zeros(1, device=self.device)
         self.step = torch.zeros(1, device=self.device)
@@ -260,8 +264,10 @@ class BNLayer:
         self.C = m0.num_features
         self.eps = float(m0.eps)
         self.momentum = float(m0.momentum if m0.momentum is not None else 0.1)
-        self.count = count
+        self.M = count                      # pixels per channel of this rank's batch
+        self.count = count * flat.bn_world  # elements per channel of the (Sync)BN batch statistics
         self.flat = flat
+        flat.bn_layers.append(self)
         self.pstride = flat.group_stride([m.weight for m in mods])
         rs = flat.bn_stride(mods)
         if self.G > 1 and rs != self.pstride:

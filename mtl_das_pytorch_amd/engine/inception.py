@@ -131,7 +131,8 @@ class InceptionProgram(LoweredProgram):
     # first three all-reduces overlap the remaining blocks' backward
     default_buckets = 4
 
-    def __init__(self, model: Multi_Classifier, batch: int, device, in_hw=(100, 250), p_drop: float = 0.5):
+    def __init__(self, model: Multi_Classifier, batch: int, device, in_hw=(100, 250), p_drop: float = 0.5,
+                 sync_world: int = 1):
         if model.aux_logits:
             raise NotImplementedError("aux_logits=True is not lowered (the reference trains without it)")
         if model.transform_input:
@@ -148,6 +149,7 @@ class InceptionProgram(LoweredProgram):
         self.p_drop = float(p_drop)
         model.to(self.device)
         self.flat = FlatState(model, self.device)
+        self.flat.bn_world = sync_world  # SyncBN: global BN counts (enable_sync_bn adds the collectives)
         self.arena = Arena(self.device)
         self._alloc()
         self.arena.finalize()

@@ -10,7 +10,8 @@ import torch
 from ..ops.functional import PATCH_R, WGRAD_PATCH, WGRAD_TILES
 from ..ops.hip import lib
 from .core import Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, pad_to, plain_ranges
-from .program import Launch, Phase, k_adam, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad, k_wgrad_batched
+from .program import (Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad,
+                      k_wgrad_batched)
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
 
@@ -116,8 +117,8 @@ class LoweredProgram:
             d.update({"dgamma2": gp["dgamma"], "dbeta2": gp["dbeta"], "dy2": dy2.p, "d2gs": dy2.gs, "ldd2": dy2.ld})
         if side is not None:
             d.update({"side": side.p, "sgs": side.gs, "lds": side.ld})
-        if bn.count != y.M:
-            raise ValueError("BN backward chunking assumes the BN count equals the tail's pixel count")
+        if bn.M != y.M:
+            raise ValueError("BN backward chunking assumes the BN pixel count equals the tail's pixel count")
         ph.add(f"tailbwd{kind}", k_tail_bwd, kind, G, bn.nchunk, d)
 
     def _tail_partial(self, ph: Phase, kind: int, y: Act, bn: BNLayer, g: list, r: Act = None, bn2: BNLayer = None,
@@ -143,6 +144,63 @@ class LoweredProgram:
         if bn2 is not None:
             d["bn2"] = bn2.args(True)
         return d
+
+    def enable_sync_bn(self, allreduce) -> int:
+        """SyncBN across data-parallel ranks (``--sync_bn`` with the engine).
+
+        The program must have been lowered with ``flat.bn_world = world`` (BN counts are global).  Then
+          * forward: right after the conv epilogue that accumulated a BN's fp64 replica sums (sum y,
+            sum y^2), ``allreduce`` sums them over ranks -- every tail / normalise-on-load consumer then
+            normalises with the global batch mean and variance and updates the running statistics with
+            them (identically on every rank);
+          * backward: every BN-tail backward becomes reduce (or the dgrad epilogue's fused statistics) ->
+            all-reduce of sum(dz), sum(dz xhat) -> apply, so the input gradient uses the global batch
+            sums (torch.nn.SyncBatchNorm); the apply writes d(gamma), d(beta) scaled by 1/world, so after
+            the data-parallel gradient average they equal torch's mean of the per-rank local sums.
+        Single-launch BN backwards (fused = 1) cannot be split and are replaced by reduce + apply.
+        The collectives run between kernels, so the step runs eagerly (no HIP graph).  Returns the number
+        of all-reduces inserted per training step."""
+        world = self.flat.bn_world
+        if world <= 1:
+            return 0
+        by_stats = {P(bn.stats): bn for bn in self.flat.bn_layers}
+        by_part = {P(bn.part): bn for bn in self.flat.bn_layers}
+        n = 0
+        new = []
+        for l in self.fwd_train.launches:
+            new.append(l)
+            bn = by_stats.get(l.args[3].get("stats") or 0) if l.name == "conv_fwd" else None
+            if bn is not None:
+                ar = Launch("allreduce_bn", k_allreduce, allreduce, bn.stats, stream=l.stream, record=l.record,
+                            bucket=l.bucket)
+                l.record = None
+                new.append(ar)
+                n += 1
+        self.fwd_train.launches = new
+        new = []
+        for l in self.bwd.launches:
+            if not l.name.startswith("tailbwd") or l.args[3].get("fused") == 3:
+                new.append(l)
+                continue
+            kind, G, nchunk, d = l.args
+            bn = by_part[d["part"]]
+            waits, record = l.waits, l.record
+            if d.get("fused", 0) != 2:  # statistics of this tail: a reduce-only pass first
+                red = {k: v for k, v in d.items() if k not in ("dzbuf", "dzgs", "lddz", "dy", "dgs", "ldd", "side",
+                                                                "sgs", "lds", "dgamma", "dbeta", "dgamma2", "dbeta2",
+                                                                "dy2", "d2gs", "ldd2", "pgs")}
+                red["fused"] = 3
+                new.append(Launch(f"tailpart{kind}", k_tail_bwd, kind, G, nchunk, red, stream=l.stream, waits=waits))
+                waits = ()
+            new.append(Launch("allreduce_bn", k_allreduce, allreduce, bn.part, stream=l.stream, waits=waits))
+            d = {k: v for k, v in d.items() if k not in ("dzbuf", "dzgs", "lddz")}
+            d["fused"], d["gscale"] = 2, 1.0 / world
+            new.append(Launch(l.name, k_tail_bwd, kind, G, nchunk, d, owner=l.owner, stream=l.stream, record=record,
+                              bucket=l.bucket))
+            n += 1
+        self.bwd.launches = new
+        self.sync_bn_world = world
+        return n
 
     @staticmethod
     def nol_enabled() -> bool:

@@ -39,7 +39,8 @@ class MTLProgram(LoweredProgram):
     # the backbone's weight gradients still run; the backbone bucket follows (bucket_cut_candidates)
     default_buckets = 2
 
-    def __init__(self, model: MTLNet, batch: int, device, in_hw=(100, 250), loss_weights: Optional[Sequence[float]] = None):
+    def __init__(self, model: MTLNet, batch: int, device, in_hw=(100, 250), loss_weights: Optional[Sequence[float]] = None,
+                 sync_world: int = 1):
         self.model = model
         self.B = B = batch
         self.T = T = len(model.tasks)
@@ -73,6 +74,7 @@ class MTLProgram(LoweredProgram):
                 bgroups.append([o[t][1] for t in range(T)])
         model.to(self.device)
         self.flat = FlatState(model, self.device, pgroups, bgroups)
+        self.flat.bn_world = sync_world  # SyncBN: global BN counts (enable_sync_bn adds the collectives)
         self.arena = A = Arena(self.device)
         self._alloc()
         A.finalize()

@@ -182,6 +182,15 @@ def k_adam(d, st):
     lib().adam_pack(st, d)
 
 
+def k_allreduce(fn, t, st):
+    """A collective inside a phase (SyncBN): ``fn(tensor)`` runs with ``st`` as the current stream, so it is
+    ordered after the stream's previous launches and before its next ones (RCCL / gloo stream semantics)."""
+    import torch
+    tt = t.t if hasattr(t, "bind") else t  # arena LazyView -> its bound tensor
+    with torch.cuda.stream(torch.cuda.ExternalStream(st)):
+        fn(tt)
+
+
 def k_gather(X, idx, lab, lab_w, out, lab_out, B, Cin, H, W, taps, off, st):
     lib().gather_batch(X.data_ptr(), idx.data_ptr(), lab.data_ptr(), lab_w, out.data_ptr(), lab_out.data_ptr(),
                        B, Cin, H, W, st, taps, off)

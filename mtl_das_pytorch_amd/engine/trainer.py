@@ -143,10 +143,6 @@ class Trainer:
         c = self.cfg
         if c.backend == "torch" or self.device.type != "cuda":
             return "torch"
-        if c.sync_bn:
-            if c.backend == "engine":
-                raise ValueError("--sync_bn is implemented by the torch backend (--dtype fp32)")
-            return "torch"
         return "engine"
 
     def print(self, *a, **k):
@@ -166,7 +162,7 @@ class Trainer:
         if self.backend_name == "engine":
             self.model.to(self.device)
             self.backend = EngineBackend(self.model, cfg.model, X, Y, Xv, Yv, use_graph=cfg.graph, tune=cfg.tune,
-                                         seed=cfg.seed, **kw)
+                                         seed=cfg.seed, sync_bn=cfg.sync_bn, **kw)
         else:
             if cfg.sync_bn and self.ctx.enabled:
                 self.model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(self.model)

@@ -59,7 +59,7 @@ class TrainConfig:
     tune: bool = False
     resume: Optional[str] = None          # path to a *.resume.pt sidecar, or "auto" (newest under output_savedir)
     dtype: Optional[str] = None           # bf16 -> HIP engine, fp32 -> plain PyTorch (alias of --backend)
-    sync_bn: bool = False                 # all-reduce BN batch statistics across ranks (torch backend)
+    sync_bn: bool = False                 # all-reduce BN batch statistics across ranks (engine and torch backends)
     profile_steps: int = 0                # >0: torch.profiler trace of that many train steps (rank 0)
     debug: bool = False                   # serialised kernels + blocking launches, no HIP graphs
     stream_ring: int = 4                  # --dataset_ram False: batches in flight (disk -> pinned -> HBM ring)
@@ -119,7 +119,8 @@ def build_parser(is_test: bool) -> argparse.ArgumentParser:
     g.add_argument("--dtype", choices=["bf16", "fp32"], default=None,
                    help="compute dtype: bf16 = HIP engine, fp32 = plain PyTorch (overrides --backend)")
     g.add_argument("--sync_bn", type=str2bool, default=False,
-                   help="synchronise BN batch statistics across ranks (torch backend, GPU process groups)")
+                   help="synchronise BN batch statistics across ranks (engine: in-step all-reduces of the BN "
+                        "sums, eager launches; torch: nn.SyncBatchNorm)")
     g.add_argument("--profile_steps", type=int, default=0, help="write a torch.profiler trace of N train steps")
     g.add_argument("--debug", type=str2bool, default=False,
                    help="debug mode: AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING=1, no HIP graphs")

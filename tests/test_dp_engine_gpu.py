@@ -61,3 +61,34 @@ def test_engine_dp_trainer_end_to_end(tmp_path):
     assert sum(f.endswith(".pth") for f in files) == 3
     for name in ("trainAccLine", "trainLossLine", "testAccLine", "testLossLine"):
         assert os.path.exists(os.path.join(runs[0], name + ".png"))
+
+
+@pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
+def test_engine_sync_bn(model):
+    """SyncBN on the engine (--sync_bn): 2 ranks x 16 samples reproduce ONE process training the 32 samples
+    -- BN running statistics equal on both ranks (bitwise) and to the single process, the averaged gradient
+    equal up to fp32 summation order.  Plain DP (the negative control) normalises each half separately."""
+    res = {}
+    for sync in (1, 0):
+        out = _torchrun([os.path.join(ROOT, "tests", "syncbn_engine_worker.py"), model, str(sync)], ROOT)
+        res[sync] = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+        assert len(res[sync]) == 2, out
+    print(res)
+    for r in res[1]:
+        assert r["bn_rank_rel"] == 0.0, r
+        assert r["bn_rel"] < 1e-4, r
+        assert r["loss_rel"] < 1e-4, r
+        assert r["grad_rel"] < 2e-2, r
+    for r in res[0]:
+        assert r["bn_rank_rel"] > 1e-3 and r["bn_rel"] > 100 * max(q["bn_rel"] for q in res[1]), r
+
+
+def test_engine_sync_bn_trainer(tmp_path):
+    """train.py --sync_bn True under torchrun stays on the engine backend (eager steps, in-step collectives)."""
+    _torchrun([os.path.join(ROOT, "train.py"), "--model", "single_event", "--synthetic", "4", "--batch_size", "16",
+               "--epoch_num", "1", "--val_every", "1", "--log_every", "2", "--save_threshold", "2",
+               "--sync_bn", "True", "--output_savedir", str(tmp_path)], str(tmp_path), timeout=300)
+    runs = glob.glob(str(tmp_path / "* model_type=single_event is_test=False"))
+    log = open(os.path.join(runs[0], "console output.log"), encoding="utf-8").read()
+    assert "backend: engine" in log and "world: 2" in log, log[:2000]
+    assert log.count("Validation Accuracy") == 2
