@@ -210,7 +210,7 @@ class EngineBackend(Backend):
             w = list(loss_weights) if model_type == "MTL" else [1.0]
             self.prog = MTLProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), loss_weights=w, sync_world=sw)
         if sw > 1:  # SyncBN: BN statistics all-reduced inside the step, which then runs eagerly
-            self.prog.enable_sync_bn(lambda t: ctx.all_reduce_(t))
+            self.prog.enable_sync_bn(ctx.all_reduce_ordered_)
             use_graph = False
         self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world)
         if hasattr(self.prog, "set_rng_stream"):

@@ -184,18 +184,23 @@ class LoweredProgram:
                 continue
             kind, G, nchunk, d = l.args
             bn = by_part[d["part"]]
-            waits, record = l.waits, l.record
+            name, record = l.name, l.record
+            # the original Launch object becomes the first of the new launches (it keeps its waits and its
+            # identity: bucket-cut anchors refer to it), the apply carries its event
+            l.record = None
             if d.get("fused", 0) != 2:  # statistics of this tail: a reduce-only pass first
                 red = {k: v for k, v in d.items() if k not in ("dzbuf", "dzgs", "lddz", "dy", "dgs", "ldd", "side",
                                                                 "sgs", "lds", "dgamma", "dbeta", "dgamma2", "dbeta2",
                                                                 "dy2", "d2gs", "ldd2", "pgs")}
                 red["fused"] = 3
-                new.append(Launch(f"tailpart{kind}", k_tail_bwd, kind, G, nchunk, red, stream=l.stream, waits=waits))
-                waits = ()
-            new.append(Launch("allreduce_bn", k_allreduce, allreduce, bn.part, stream=l.stream, waits=waits))
+                l.name, l.args = f"tailpart{kind}", (kind, G, nchunk, red)
+                new += [l, Launch("allreduce_bn", k_allreduce, allreduce, bn.part, stream=l.stream, bucket=l.bucket)]
+            else:  # statistics from the producing dgrad's epilogue: all-reduce them, then apply
+                l.name, l.fn, l.args = "allreduce_bn", k_allreduce, (allreduce, bn.part)
+                new.append(l)
             d = {k: v for k, v in d.items() if k not in ("dzbuf", "dzgs", "lddz")}
             d["fused"], d["gscale"] = 2, 1.0 / world
-            new.append(Launch(l.name, k_tail_bwd, kind, G, nchunk, d, owner=l.owner, stream=l.stream, record=record,
+            new.append(Launch(name, k_tail_bwd, kind, G, nchunk, d, owner=l.owner, stream=l.stream, record=record,
                               bucket=l.bucket))
             n += 1
         self.bwd.launches = new

@@ -42,9 +42,18 @@ class Launch:
         self.waits = tuple(waits)
         self.record = record
 
-    def __call__(self, st: int):
-        if self.fn is not None:  # fn None: a pseudo-launch that only carries waits / a record (fork point)
-            self.fn(*self.args, st)
+    def __call__(self, st: int, tstream=None):
+        if self.fn is None:  # a pseudo-launch that only carries waits / a record (fork point)
+            return
+        if self.fn is k_allreduce:  # a host-issued collective: it runs with the launch's stream as current
+            import torch
+            if tstream is None or tstream == torch.cuda.current_stream():
+                self.fn(*self.args, None)
+            else:
+                with torch.cuda.stream(tstream):
+                    self.fn(*self.args, None)
+            return
+        self.fn(*self.args, st)
 
 
 class Phase:
@@ -99,7 +108,7 @@ class Phase:
             s = streams[sid_of(l)]
             for tag in l.waits:
                 s.wait_event(events[self.alias.get(tag, tag)])
-            l(s.cuda_stream)
+            l(s.cuda_stream, s)
             if l.record is not None:
                 events[l.record] = s.record_event()
         for sid in used - {0}:
@@ -183,12 +192,10 @@ def k_adam(d, st):
 
 
 def k_allreduce(fn, t, st):
-    """A collective inside a phase (SyncBN): ``fn(tensor)`` runs with ``st`` as the current stream, so it is
-    ordered after the stream's previous launches and before its next ones (RCCL / gloo stream semantics)."""
-    import torch
-    tt = t.t if hasattr(t, "bind") else t  # arena LazyView -> its bound tensor
-    with torch.cuda.stream(torch.cuda.ExternalStream(st)):
-        fn(tt)
+    """A collective inside a phase (SyncBN): Launch.__call__ makes the launch's stream current, so
+    ``fn(tensor)`` (DistContext.all_reduce_ordered_) is ordered after that stream's previous launches and
+    before its next ones."""
+    fn(t.t if hasattr(t, "bind") else t)  # arena LazyView -> its bound tensor
 
 
 def k_gather(X, idx, lab, lab_w, out, lab_out, B, Cin, H, W, taps, off, st):

@@ -55,6 +55,21 @@ class DistContext:
             dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
         return t
 
+    def all_reduce_ordered_(self, t: torch.Tensor):
+        """All-reduce(SUM) of a device tensor ordered on the CURRENT stream: the kernels queued before on
+        that stream are reduced, the ones queued after see the result.  RCCL gives exactly this; gloo (the
+        one-GPU rehearsal of several ranks) goes through a host copy: ``.cpu()`` waits for the stream, the
+        CPU all-reduce runs, and the copy back is queued on the stream."""
+        if not self.enabled:
+            return t
+        if self.backend == "nccl" or t.device.type != "cuda":
+            dist.all_reduce(t)
+            return t
+        c = t.cpu()
+        dist.all_reduce(c)
+        t.copy_(c)
+        return t
+
     def broadcast_(self, t: torch.Tensor, src: int = 0):
         if self.enabled:
             dist.broadcast(t, src=src)
