@@ -22,6 +22,13 @@
 
 namespace mda {
 
+// Kernel-internal kind: ADD_RELU with a BN'ed (projection) residual.  Splitting it from the identity-shortcut
+// ADD_RELU at compile time keeps the BN2 constants, xhat2 and its accumulators out of the identity kernels'
+// registers (occupancy).  The host API keeps ADD_RELU + TailArgs::r_bn.
+constexpr int ADD_RELU2 = 6;
+template <int K>
+DEV constexpr bool is_add() { return K == ADD_RELU || K == ADD_RELU2; }
+
 
 
 // thread -> (channel group, pixel lane) mapping shared by every kernel here
@@ -38,7 +45,7 @@ struct Lanes {
 };
 
 template <int KIND>
-__global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
+DEV void tail_fwd_impl(const TailArgs& a) {
   extern __shared__ float sm[];
   float* s_sc = sm;
   float* s_sh = sm + a.C;
@@ -47,7 +54,7 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
   const int z = blockIdx.z;
   const bool upd = blockIdx.x == 0;
   bn_prepare(a.bn, z, s_sc, s_sh, nullptr, nullptr, upd);
-  if (KIND == ADD_RELU && a.r_bn) bn_prepare(a.bn2, z, s_sc2, s_sh2, nullptr, nullptr, upd);
+  if (KIND == ADD_RELU2) bn_prepare(a.bn2, z, s_sc2, s_sh2, nullptr, nullptr, upd);
   __syncthreads();
   Lanes L(a.C);
   if (!L.active) return;
@@ -85,7 +92,7 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
   }
 
   float sc2[8], sh2[8];
-  if (KIND == ADD_RELU && a.r_bn) {
+  if (KIND == ADD_RELU2) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) { sc2[j] = s_sc2[c + j]; sh2[j] = s_sh2[c + j]; }
   }
@@ -107,10 +114,10 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
       load8(rz + (int64_t)p * a.ldr + c, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = sigmoidf_(v[j]) * f[j];
-    } else if (KIND == ADD_RELU) {
+    } else if (is_add<KIND>()) {
       float f[8];
       load8(rz + (int64_t)p * a.ldr + c, f);
-      if (a.r_bn) {
+      if (KIND == ADD_RELU2) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = f[j] * sc2[j] + sh2[j];
       }
@@ -121,12 +128,25 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
   }
 }
 
+// Default register allocation (66-80 VGPRs, 6 waves per SIMD).  A budget of 8 waves per SIMD fits every kind
+// without spilling but measured +170 us on Model A's forward (docs/PERF.md, rejected).
+template <int KIND>
+__global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) { tail_fwd_impl<KIND>(a); }
+
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
 // ------------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------------
+// Per-thread views of the block's BN constants in LDS (8 channels per array).  Reading them where they are
+// used instead of caching 64 floats in registers keeps the BN-backward kernels' VGPR count -- and so their
+// occupancy, which these latency-bound passes depend on -- down.
 struct BwdCtx {
-  float sc[8], sh[8], mean[8], inv[8];
-  float sc2[8], sh2[8], mean2[8], inv2[8];
+  const float *sc, *sh, *mean, *inv;
+  const float *sc2, *sh2, *mean2, *inv2;
 };
 
 // dz for the 8 channels [c, c+8) at pre-pool pixel p; also returns xhat (and xhat2 for ADD_RELU+BN2)
@@ -193,10 +213,10 @@ DEV void compute_dz(const TailArgs& a, const BwdCtx& X, int z, int p, int c, flo
       dz[j] = g[j] * f[j] * s * (1.f - s);
       side[j] = g[j] * s;
     }
-  } else if (KIND == ADD_RELU) {
+  } else if (is_add<KIND>()) {
     float f[8];
     load8(a.r + a.rgs * z + (int64_t)p * a.ldr + c, f);
-    if (a.r_bn) {
+    if (KIND == ADD_RELU2) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         xh2[j] = (f[j] - X.mean2[j]) * X.inv2[j];
@@ -207,23 +227,6 @@ DEV void compute_dz(const TailArgs& a, const BwdCtx& X, int z, int p, int c, flo
     for (int j = 0; j < 8; ++j) {
       dz[j] = (y[j] * X.sc[j] + X.sh[j] + f[j]) > 0.f ? g[j] : 0.f;
       side[j] = dz[j];
-    }
-  }
-}
-
-template <int KIND>
-DEV void load_ctx(const TailArgs& a, BwdCtx& X, const float* s_sc, const float* s_sh, const float* s_mean,
-                  const float* s_inv, int c) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    X.sc[j] = s_sc[c + j]; X.sh[j] = s_sh[c + j]; X.mean[j] = s_mean[c + j]; X.inv[j] = s_inv[c + j];
-  }
-  if (KIND == ADD_RELU && a.r_bn) {
-    const int C = a.C;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      X.sc2[j] = s_sc[4 * C + c + j]; X.sh2[j] = s_sh[4 * C + c + j];
-      X.mean2[j] = s_mean[4 * C + c + j]; X.inv2[j] = s_inv[4 * C + c + j];
     }
   }
 }
@@ -262,7 +265,7 @@ DEV float row_stride_sum(float v) {
 // BN constants of the thread's 8 channels (BN1 and, for the residual projection, BN2)
 template <int KIND, int CGB>
 DEV void bnb_ctx(const TailArgs& a, int z, int cblk, int cgl, BwdCtx& X, float (*s_x)[5][8 * CGB]) {
-  const bool two = (KIND == ADD_RELU && a.r_bn);
+  constexpr bool two = KIND == ADD_RELU2;
   for (int t = threadIdx.x; t < (two ? 2 : 1) * 8 * CGB; t += BNB_T) {
     const int k = t / (8 * CGB), j = t - k * 8 * CGB;
     const BNArgs& bk = k ? a.bn2 : a.bn;
@@ -272,23 +275,20 @@ DEV void bnb_ctx(const TailArgs& a, int z, int cblk, int cgl, BwdCtx& X, float (
     s_x[k][4][j] = bk.gamma[bk.pstride * z + cblk + j];
   }
   __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int q = cgl * 8 + j;
-    X.sc[j] = s_x[0][0][q]; X.sh[j] = s_x[0][1][q]; X.mean[j] = s_x[0][2][q]; X.inv[j] = s_x[0][3][q];
-    X.sc2[j] = s_x[1][0][q]; X.sh2[j] = s_x[1][1][q]; X.mean2[j] = s_x[1][2][q]; X.inv2[j] = s_x[1][3][q];
-  }
+  const int q = cgl * 8;
+  X.sc = &s_x[0][0][q]; X.sh = &s_x[0][1][q]; X.mean = &s_x[0][2][q]; X.inv = &s_x[0][3][q];
+  X.sc2 = &s_x[1][0][q]; X.sh2 = &s_x[1][1][q]; X.mean2 = &s_x[1][2][q]; X.inv2 = &s_x[1][3][q];
 }
 
 template <int KIND, int CGB>
-__global__ __launch_bounds__(BNB_T) void bnb_reduce_kernel(TailArgs a) {
+DEV void bnb_reduce_impl(const TailArgs& a) {
   constexpr int PL = BNB_T / CGB, CB = 8 * CGB;
   __shared__ float s_x[2][5][CB];
   __shared__ float s_part[16][3][CB];  // 16 rows of 16 lanes per block
   const int z = blockIdx.z, chunk = blockIdx.x;
   const int cgl = threadIdx.x % CGB, pl = threadIdx.x / CGB;
   const int cblk = blockIdx.y * CB, c = cblk + cgl * 8;
-  const bool two = (KIND == ADD_RELU && a.r_bn);
+  constexpr bool two = KIND == ADD_RELU2;
   BwdCtx X;
   bnb_ctx<KIND, CGB>(a, z, cblk, cgl, X, s_x);
   const int M = a.B * a.H * a.W;
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(BNB_T) void bnb_reduce_kernel(TailArgs a) {
       sdx[j] += dz[j] * xh[j];
       if (two) sdx2[j] += dz[j] * xh2[j];
     }
-    if ((KIND == SIGMUL || (KIND == ADD_RELU && !a.r_bn)) && a.side)
+    if ((KIND == SIGMUL || KIND == ADD_RELU) && a.side)
       store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
     if (dzz) store8f(dzz + (int64_t)p * a.lddz + c, dz);
   }
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(BNB_T) void bnb_reduce_kernel(TailArgs a) {
 // source of the previous tail (TailArgs::ppart); its partial statistics are accumulated here, so that tail
 // needs no reduce pass of its own over this source.
 template <int KIND, int CGB, bool PREV>
-__global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
+DEV void bnb_apply_impl(const TailArgs& a) {
   constexpr int PL = BNB_T / CGB, CB = 8 * CGB;
   __shared__ float s_x[2][5][CB];
   __shared__ float s_red[BNB_T];
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
   const int z = blockIdx.z, chunk = blockIdx.x;
   const int cgl = threadIdx.x % CGB, pl = threadIdx.x / CGB;
   const int cblk = blockIdx.y * CB, c = cblk + cgl * 8;
-  const bool two = (KIND == ADD_RELU && a.r_bn);
+  constexpr bool two = KIND == ADD_RELU2;
   if (PREV) {
     for (int t = threadIdx.x; t < 2 * CB; t += BNB_T) {
       const int k = t / CB, j = t - k * CB;
@@ -386,13 +386,8 @@ __global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
     }
   }
   __syncthreads();
-  float A1[8], B1[8], C1[8], A2[8], B2[8], C2[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int q = cgl * 8 + j;
-    A1[j] = s_coef[0][0][q]; B1[j] = s_coef[0][1][q]; C1[j] = s_coef[0][2][q];
-    A2[j] = s_coef[1][0][q]; B2[j] = s_coef[1][1][q]; C2[j] = s_coef[1][2][q];
-  }
+  const float *A1 = &s_coef[0][0][cgl * 8], *B1 = &s_coef[0][1][cgl * 8], *C1 = &s_coef[0][2][cgl * 8];
+  const float *A2 = &s_coef[1][0][cgl * 8], *B2 = &s_coef[1][1][cgl * 8], *C2 = &s_coef[1][2][cgl * 8];
   const int M = a.B * a.H * a.W;
   const int p0 = chunk * a.chunk_px, p1 = min(M, p0 + a.chunk_px);
   const bf16_t* yz = a.y + a.ygs * z;
@@ -407,7 +402,7 @@ __global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
     } else {
       float xh[8], xh2[8], side[8];
       compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
-      if ((KIND == SIGMUL || (KIND == ADD_RELU && !a.r_bn)) && a.side && a.apply_side)
+      if ((KIND == SIGMUL || KIND == ADD_RELU) && a.side && a.apply_side)
         store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
       if (PREV) {  // side (= dz, identity shortcut) through the previous tail's activation derivative
         float pyv[8], prv[8];
@@ -460,6 +455,29 @@ __global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
   }
 }
 
+// Kernels: plain, and with the register budget of 5 waves per SIMD (<= 96 VGPRs) for the kinds that fit it
+// without spilling (every kind but the two-BN residual tail and the pooling tail; the PREV apply spills).
+// These passes are latency-bound, and occupancy is what hides the latency (measured: forward tails at 4
+// instead of 6 waves per SIMD cost Model A 150 us per step).
+template <int KIND, int CGB>
+__global__ __launch_bounds__(BNB_T) void bnb_reduce_kernel(TailArgs a) { bnb_reduce_impl<KIND, CGB>(a); }
+template <int KIND, int CGB, int W>
+__global__ __launch_bounds__(BNB_T) __attribute__((amdgpu_waves_per_eu(W))) void bnb_reduce_kernel_w(TailArgs a) {
+  bnb_reduce_impl<KIND, CGB>(a);
+}
+template <int KIND, int CGB, bool PREV>
+__global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) { bnb_apply_impl<KIND, CGB, PREV>(a); }
+template <int KIND, int CGB, int W>
+__global__ __launch_bounds__(BNB_T) __attribute__((amdgpu_waves_per_eu(W))) void bnb_apply_kernel_w(TailArgs a) {
+  bnb_apply_impl<KIND, CGB, false>(a);
+}
+// waves per SIMD each kind's passes fit without spilling (hipcc -Rpass-analysis=kernel-resource-usage, gfx950);
+// 0 = the compiler's default allocation
+template <int KIND>
+constexpr int bnb_waves() {
+  return KIND == ACT_NONE ? 8 : (KIND == ACT_RELU || KIND == ACT_SIGMOID) ? 6 : (KIND == SIGMUL || KIND == ADD_RELU) ? 5 : 0;
+}
+
 // Single-launch BN backward for small maps: block (cg, -, z) owns channels [8cg, 8cg+8) for ALL M
 // pixels, so the batch reduction is a block reduction (no global atomics, no second launch, exact and
 // deterministic).  Each of the 1024 threads keeps the dz / xhat of its R <= 4 pixels in registers, so
@@ -474,7 +492,7 @@ __global__ __launch_bounds__(FUSED_T) void tail_bwd_fused_kernel(TailArgs a) {
   __shared__ float s_coef[2][3][8];             // dy = A*dz + Bx*xhat + Cc (BN1, BN2)
   const int z = blockIdx.z;
   const int c = blockIdx.x * 8;
-  const bool two = (KIND == ADD_RELU && a.r_bn);
+  constexpr bool two = KIND == ADD_RELU2;
   const bool tick = a.tsc && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0;
 #define TICK(i) if (tick) a.tsc[i] = wall_clock64()
   TICK(0);
@@ -489,11 +507,8 @@ __global__ __launch_bounds__(FUSED_T) void tail_bwd_fused_kernel(TailArgs a) {
   __syncthreads();
   TICK(1);
   BwdCtx X;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    X.sc[j] = s_x[0][0][j]; X.sh[j] = s_x[0][1][j]; X.mean[j] = s_x[0][2][j]; X.inv[j] = s_x[0][3][j];
-    X.sc2[j] = s_x[1][0][j]; X.sh2[j] = s_x[1][1][j]; X.mean2[j] = s_x[1][2][j]; X.inv2[j] = s_x[1][3][j];
-  }
+  X.sc = s_x[0][0]; X.sh = s_x[0][1]; X.mean = s_x[0][2]; X.inv = s_x[0][3];
+  X.sc2 = s_x[1][0]; X.sh2 = s_x[1][1]; X.mean2 = s_x[1][2]; X.inv2 = s_x[1][3];
   const int M = a.B * a.H * a.W;
   float sdz[8], sdx[8], sdx2[8];
 #pragma unroll
@@ -507,7 +522,7 @@ __global__ __launch_bounds__(FUSED_T) void tail_bwd_fused_kernel(TailArgs a) {
     for (int j = 0; j < 8; ++j) { dzc[r][j] = 0.f; xhc[r][j] = 0.f; xh2c[r][j] = 0.f; }
     if (p < M) {
       compute_dz<KIND>(a, X, z, p, c, dzc[r], xhc[r], xh2c[r], side);
-      if ((KIND == SIGMUL || (KIND == ADD_RELU && !a.r_bn)) && a.side)
+      if ((KIND == SIGMUL || KIND == ADD_RELU) && a.side)
         store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
     }
 #pragma unroll
@@ -545,12 +560,8 @@ __global__ __launch_bounds__(FUSED_T) void tail_bwd_fused_kernel(TailArgs a) {
   }
   __syncthreads();
   TICK(4);
-  float A1[8], B1[8], C1[8], A2[8], B2[8], C2[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    A1[j] = s_coef[0][0][j]; B1[j] = s_coef[0][1][j]; C1[j] = s_coef[0][2][j];
-    A2[j] = s_coef[1][0][j]; B2[j] = s_coef[1][1][j]; C2[j] = s_coef[1][2][j];
-  }
+  const float *A1 = s_coef[0][0], *B1 = s_coef[0][1], *C1 = s_coef[0][2];
+  const float *A2 = s_coef[1][0], *B2 = s_coef[1][1], *C2 = s_coef[1][2];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int p = threadIdx.x + r * FUSED_T;
@@ -573,9 +584,10 @@ __global__ __launch_bounds__(FUSED_T) void tail_bwd_fused_kernel(TailArgs a) {
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st) {
   size_t lds = (size_t)4 * a.C * sizeof(float);
   dim3 grid(blocks, 1, G);
-  switch (kind) {
+  const int kk = (kind == ADD_RELU && a.r_bn) ? ADD_RELU2 : kind;
 #define K(X) case X: hipLaunchKernelGGL(tail_fwd_kernel<X>, grid, dim3(256), lds, st, a); break;
-    K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(ADD_RELU) K(POOL_RELU)
+  switch (kk) {
+    K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(POOL_RELU) K(ADD_RELU) K(ADD_RELU2)
 #undef K
     default: return -1;
   }
@@ -594,6 +606,7 @@ int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, h
     return -6;
   TailArgs b = a;
   b.apply_side = fused == 2;
+  const int kk = (kind == ADD_RELU && a.r_bn) ? ADD_RELU2 : kind;  // kernel kind
   if (fused == 1) {
     if (a.gscale != 1.f) return -5;
     const int M = a.B * a.H * a.W;
@@ -608,8 +621,8 @@ int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, h
     else if (R <= 2) KR(X, 2);              \
     else KR(X, 4);                          \
     break;
-    switch (kind) {
-      K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(ADD_RELU) K(POOL_RELU)
+    switch (kk) {
+      K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(ADD_RELU) K(ADD_RELU2) K(POOL_RELU)
       default: return -1;
     }
 #undef K
@@ -618,19 +631,39 @@ int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, h
   }
   if (!a.part || a.chunk_px <= 0 || nchunk <= 0) return -4;
   const int cgb = bnb_cgb(a.C);
+  static const int bw = env_int("MDA_BNB_WAVES", 1);  // per-kind register budgets (occupancy experiment)
   dim3 grid(nchunk, a.C / (8 * cgb), G);
 #define KC(X, CG)                                                                                    \
-  if (fused != 2) hipLaunchKernelGGL((bnb_reduce_kernel<X, CG>), grid, dim3(BNB_T), 0, st, b);       \
+  if (fused != 2) {                                                                                  \
+    bool done = false;                                                                               \
+    if constexpr (bnb_waves<X>() > 0) {                                                              \
+      if (bw) {                                                                                      \
+        hipLaunchKernelGGL((bnb_reduce_kernel_w<X, CG, bnb_waves<X>()>), grid, dim3(BNB_T), 0, st, b); \
+        done = true;                                                                                 \
+      }                                                                                              \
+    }                                                                                                \
+    if (!done) hipLaunchKernelGGL((bnb_reduce_kernel<X, CG>), grid, dim3(BNB_T), 0, st, b);           \
+  }                                                                                                  \
   if (fused == 3) break;                                                                             \
-  if (X == ADD_RELU && b.ppart) hipLaunchKernelGGL((bnb_apply_kernel<X, CG, (X == ADD_RELU)>), grid, dim3(BNB_T), 0, st, b); \
-  else hipLaunchKernelGGL((bnb_apply_kernel<X, CG, false>), grid, dim3(BNB_T), 0, st, b);
+  if (X == ADD_RELU && b.ppart) {                                                                    \
+    hipLaunchKernelGGL((bnb_apply_kernel<X, CG, (X == ADD_RELU)>), grid, dim3(BNB_T), 0, st, b);     \
+  } else {                                                                                           \
+    bool done = false;                                                                               \
+    if constexpr (bnb_waves<X>() > 0) {                                                              \
+      if (bw) {                                                                                      \
+        hipLaunchKernelGGL((bnb_apply_kernel_w<X, CG, bnb_waves<X>()>), grid, dim3(BNB_T), 0, st, b); \
+        done = true;                                                                                 \
+      }                                                                                              \
+    }                                                                                                \
+    if (!done) hipLaunchKernelGGL((bnb_apply_kernel<X, CG, false>), grid, dim3(BNB_T), 0, st, b);    \
+  }
 #define K(X)                                                   \
   case X:                                                      \
     if (cgb == 1) { KC(X, 1) } else if (cgb == 2) { KC(X, 2) } \
     else if (cgb == 4) { KC(X, 4) } else { KC(X, 8) }          \
     break;
-  switch (kind) {
-    K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(ADD_RELU) K(POOL_RELU)
+  switch (kk) {
+    K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(ADD_RELU) K(ADD_RELU2) K(POOL_RELU)
     default: return -1;
   }
 #undef K
