@@ -81,6 +81,8 @@ BNArgs parse_bn(const py::dict& d) {
   b.momentum = (float)F(d, "momentum", 0.1);
   b.training = (int)I(d, "training", 1);
   b.consts = P<float>(d, "consts");
+  b.fin = (int)I(d, "fin", 0);
+  if (b.fin && (!b.consts || !b.training)) throw std::runtime_error("bn: fin needs training and consts");
   return b;
 }
 
@@ -168,6 +170,14 @@ ConvArgs parse_conv(int mode, py::dict d) {
   }
   a.ws = P<float>(d, "ws");
   a.cnt = P<unsigned>(d, "cnt");
+  if (d.contains("fin") && !d["fin"].is_none()) {  // producer-side BN finalize (last block)
+    py::dict f = d["fin"].cast<py::dict>();
+    a.obn = parse_bn(f["bn"].cast<py::dict>());
+    a.fcnt = P<unsigned>(f, "cnt");
+    if ((mode != MODE_FWD) || !a.fcnt || !a.obn.training || a.obn.stats != a.stats || !a.obn.consts ||
+        a.obn.C != a.N)
+      throw std::runtime_error("conv: bad BN-finalize arguments");
+  }
   return a;
 }
 
@@ -330,6 +340,15 @@ void pool3(int is_max, int backward, int64_t stream, py::dict d) {
   check(launch_pool3(is_max, backward, a, S(stream)), "pool3");
 }
 
+void synth_das(int64_t stream, py::dict d) {
+  SynthArgs a{};
+  a.params = P<const float>(d, "params"); a.out = P<float>(d, "out");
+  a.C = (int)I(d, "C"); a.H = (int)I(d, "H"); a.W = (int)I(d, "W");
+  a.noise = (int)I(d, "noise", 1);
+  a.key = (uint64_t)I(d, "key"); a.sample0 = I(d, "sample0", 0);
+  check(launch_synth_das(a, (int)I(d, "n"), S(stream)), "synth_das");
+}
+
 void grad_sum(py::list g, int64_t out, int ldo, int64_t M, int C, int64_t stream) {
   check(launch_grad_sum(parse_grads(g), reinterpret_cast<float*>(out), ldo, M, C, S(stream)), "grad_sum");
 }
@@ -375,6 +394,11 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("wgrad_table", &wgrad_table);
   m.def("wgrad_batched", &wgrad_batched);
   m.def("grad_sum", &grad_sum);
+  m.def("synth_das", &synth_das);
+  m.def("philox_kat", [](int64_t ctr, uint64_t key, int64_t out, int n, int64_t stream) {
+    check(launch_philox_kat(reinterpret_cast<const uint32_t*>(static_cast<intptr_t>(ctr)), key,
+                            reinterpret_cast<uint32_t*>(static_cast<intptr_t>(out)), n, S(stream)), "philox_kat");
+  });
   m.def("tick", [](int64_t buf, int i, int64_t stream) {
     check(launch_tick(reinterpret_cast<uint64_t*>(static_cast<intptr_t>(buf)), i, S(stream)), "tick");
   });

@@ -441,6 +441,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       }
     }
   }
+  if (is_fwd<MODE>() && a.fcnt) {  // producer-side BN finalize by the last block of the group
+    __shared__ int s_fin;
+    bn_finalize(a.obn, a.fcnt, z, gridDim.x * gridDim.y, &s_fin);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------

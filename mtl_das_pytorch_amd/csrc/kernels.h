@@ -71,6 +71,9 @@ struct ConvArgs {
   // block resets it), sized by conv_lds_workspace
   float* ws;
   unsigned* cnt;
+  // FWD training, optional (fcnt null = off): the last block finalizes the output BN (common.h bn_finalize)
+  BNArgs obn;
+  unsigned* fcnt;  // [G] arrival tickets, zero-initialised, reset by the finalizing block
 };
 
 // One output-pixel phase of an LDS-staged conv launch (conv_lds.hip): output pixels (b, oy0 + i*qy,
@@ -257,6 +260,18 @@ int launch_cls_head(const ClsArgs& a, int64_t* seed_mut, hipStream_t st);
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
                         int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, hipStream_t st);
 int launch_pool3(int is_max, int backward, const PoolArgs& a, hipStream_t st);
+// synth.hip: on-device synthetic DAS samples (data/synthetic.py physical model, Philox noise)
+constexpr int SYNTH_NPARAM = 9;  // per sample: distance, event, x0, t0, jitter[4], snr_db
+struct SynthArgs {
+  const float* params;  // [n][SYNTH_NPARAM]
+  float* out;           // [n][C][H][W] fp32
+  int C, H, W;
+  int noise;            // 0: clean signal only
+  uint64_t key;         // Philox key (the draw's noise seed)
+  int64_t sample0;      // global index of sample 0 (Philox counter)
+};
+int launch_synth_das(const SynthArgs& a, int n, hipStream_t st);
+int launch_philox_kat(const uint32_t* ctr, uint64_t key, uint32_t* out, int n, hipStream_t st);
 int launch_tick(uint64_t* buf, int i, hipStream_t st);
 int launch_grad_sum(const GradSrcs& g, float* out, int ldo, int64_t M, int C, hipStream_t st);
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st);

@@ -5,7 +5,7 @@ run on synthetic data of the paper's shape: ``C x 100 x 250`` (C = 1 by default,
 configurable), 16 radial-distance classes (0..15 m, 1 m bins) and 2 event types (striking=0,
 excavating=1).
 
-Physical toy model (per sample, vectorised in torch so it runs on the GPU as well as the CPU):
+Physical toy model (per sample; torch ops on the CPU, one HIP kernel -- csrc/synth.hip -- on the GPU):
   * a source at radial distance ``d`` metres from the fibre and along-fibre position ``x0`` emits a
     wavelet that reaches fibre point ``x`` at ``t0 + sqrt(d^2 + (x-x0)^2) / v`` (hyperbolic moveout);
   * amplitude decays as ``1 / (1 + d/4)``, the spatial footprint widens with ``d``;
@@ -35,8 +35,14 @@ N_DIST, N_EVENT = 16, 2
 
 def generate(n: int, seed: int = 0, device="cpu", in_channels: int = 1, height: int = H, width: int = W,
              distance: Optional[torch.Tensor] = None, event: Optional[torch.Tensor] = None,
-             snr_db: Tuple[float, float] = (6.0, 20.0), dtype=torch.float32):
-    """Return ``(x [n,C,H,W], distance [n], event [n])``; labels drawn uniformly unless given."""
+             snr_db: Tuple[float, float] = (6.0, 20.0), dtype=torch.float32, backend: Optional[str] = None,
+             noise: bool = True):
+    """Return ``(x [n,C,H,W], distance [n], event [n])``; labels drawn uniformly unless given.
+
+    ``backend``: "hip" evaluates the model in one HIP kernel (``csrc/synth.hip``, Philox noise; the default on
+    a GPU), "torch" with torch ops (the default on the CPU).  Both draw the per-sample scalars from the same
+    CPU generator, so their clean signals agree to fp32 rounding; the noise streams differ.  ``noise=False``
+    returns the clean signal (x 100)."""
     g = torch.Generator(device="cpu").manual_seed(seed)
     if distance is None:
         distance = torch.randint(0, N_DIST, (n,), generator=g)
@@ -52,6 +58,13 @@ def generate(n: int, seed: int = 0, device="cpu", in_channels: int = 1, height: 
     noise_seed = int(torch.randint(0, 2 ** 31 - 1, (1,), generator=g))
 
     dev = torch.device(device)
+    if backend is None:
+        backend = "hip" if dev.type == "cuda" else "torch"
+    if backend == "hip":
+        return _generate_hip(n, dev, distance, event, x0, t0, jitter, snr, noise_seed, in_channels, height, width,
+                             noise, dtype)
+    if backend != "torch":
+        raise ValueError(f"unknown backend {backend!r}")
     d = distance.to(dev, torch.float32)
     ev = event.to(dev, torch.float32)
     x0, t0, jitter, snr = x0.to(dev), t0.to(dev), jitter.to(dev), snr.to(dev)
@@ -75,7 +88,7 @@ def generate(n: int, seed: int = 0, device="cpu", in_channels: int = 1, height: 
     e = ev.view(n, 1, 1)
     clean = amp * footprint * ((1 - e) * strike + e * dig)               # [n, H, W]
     p_sig = clean.pow(2).mean(dim=(1, 2), keepdim=True).clamp_min(1e-12)
-    sigma = torch.sqrt(p_sig / (10.0 ** (snr.view(n, 1, 1) / 10.0)))
+    sigma = torch.sqrt(p_sig / (10.0 ** (snr.view(n, 1, 1) / 10.0))) * float(noise)
     gn = torch.Generator(device=dev).manual_seed(noise_seed)
     chans = []
     for c in range(in_channels):
@@ -83,6 +96,20 @@ def generate(n: int, seed: int = 0, device="cpu", in_channels: int = 1, height: 
         sig = clean if c == 0 else torch.roll(clean, shifts=c, dims=2)   # extra channels: shifted copies
         chans.append(sig + sigma * noise)
     x = torch.stack(chans, dim=1) * 100.0                               # field units ~ O(1..10)
+    return x.to(dtype), distance.to(dev), event.to(dev)
+
+
+def _generate_hip(n, dev, distance, event, x0, t0, jitter, snr, noise_seed, in_channels, height, width, noise,
+                  dtype):
+    """One ``synth_das`` launch: block s evaluates sample s (csrc/synth.hip)."""
+    from ..ops.hip import lib
+    params = torch.cat([distance.float().view(n, 1), event.float().view(n, 1), x0.view(n, 1), t0.view(n, 1),
+                        jitter.view(n, 4), snr.view(n, 1)], 1).contiguous().to(dev)
+    x = torch.empty(n, in_channels, height, width, device=dev, dtype=torch.float32)
+    with torch.cuda.device(dev):
+        lib().synth_das(torch.cuda.current_stream(dev).cuda_stream,
+                        {"params": params.data_ptr(), "out": x.data_ptr(), "n": n, "C": in_channels, "H": height,
+                         "W": width, "noise": int(noise), "key": noise_seed, "sample0": 0})
     return x.to(dtype), distance.to(dev), event.to(dev)
 
 

@@ -123,6 +123,20 @@ class Pool:
         self.src.grads.append(self.dx)
 
 
+def _mixed6_hw(in_hw):
+    """Spatial size of Mixed_6a..6e's output for an input of ``in_hw`` (valid 3x3/s2 stem conv, two valid
+    3x3 convs... as in modelC_multiClassifier.py:63-86)."""
+    def s2(x):
+        return (x - 3) // 2 + 1
+    out = []
+    for x in in_hw:
+        x = s2(x) - 2       # Conv2d_1a (s2), Conv2d_2a; 2b keeps the size (pad 1)
+        x = s2(x) - 2       # maxpool1, Conv2d_3b (1x1), Conv2d_4a
+        x = s2(s2(x))       # maxpool2, Mixed_6a (s2)
+        out.append(x)
+    return tuple(out)
+
+
 class InceptionProgram(LoweredProgram):
     """Static train/eval programs of a :class:`Multi_Classifier` for a fixed per-GPU batch size."""
 
@@ -134,7 +148,15 @@ class InceptionProgram(LoweredProgram):
     def __init__(self, model: Multi_Classifier, batch: int, device, in_hw=(100, 250), p_drop: float = 0.5,
                  sync_world: int = 1):
         if model.aux_logits:
-            raise NotImplementedError("aux_logits=True is not lowered (the reference trains without it)")
+            h6 = _mixed6_hw(in_hw)
+            if min(h6) < 5:
+                # InceptionAux opens with avg_pool(5, stride 3) on Mixed_6e's output, 4 x 13 for the DAS input
+                # (100 x 250): the reference model (modelC_multiClassifier.py:78-80,134-141) raises in
+                # F.avg_pool2d at such a shape, so there is no trainable configuration to lower
+                raise ValueError(f"aux_logits=True: InceptionAux needs >= 5 x 5 at Mixed_6e, input {tuple(in_hw)} gives "
+                                 f"{h6[0]} x {h6[1]} (the reference raises in avg_pool2d too); use aux_logits=False")
+            raise NotImplementedError("aux_logits=True is lowered only by the torch backend (the reference trains "
+                                      "without it)")
         if model.transform_input:
             raise NotImplementedError("transform_input is not lowered")
         if model.num_classes > 64:

@@ -22,7 +22,9 @@ def _setup(model_cls, B=8, seed=0, **kw):
     model = model_cls(**kw)
     ref = copy.deepcopy(model).cuda()
     prog = MTLProgram(model, B, "cuda")
-    X, d, e = generate(2 * B, seed=seed + 1, device="cuda")
+    # torch-op generator: the whole-network bounds below were calibrated on this input (at init the
+    # network amplifies rounding differences input-dependently; the HIP generator's noise is another draw)
+    X, d, e = generate(2 * B, seed=seed + 1, device="cuda", backend="torch")
     labels = torch.stack([d, e], 1)
     return model, ref, prog, X, labels
 

@@ -1,5 +1,6 @@
 """The MI355X lowering is pure bookkeeping until launch time: build it on the CPU and check the program
 structure, the grouped (per-task) parameter layout and the descriptor tables."""
+import pytest
 import torch
 
 from mtl_das_pytorch_amd.engine.mtl import MTLProgram
@@ -256,3 +257,18 @@ def test_merge_wgrad_cfgs_caps_batches_per_stream():
         assert l.owner.wgrad_valid(l.args[0]) and l.args[2]["splits"] == l.owner.splits
     p.batch_wgrads()
     _check_event_order(p.bwd)
+
+
+def test_inception_aux_logits_shape_error():
+    """aux_logits at the DAS input: the reference's own InceptionAux cannot run (avg_pool 5/3 on 4 x 13); the
+    engine says so instead of lowering a configuration that does not exist."""
+    import torch
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram, _mixed6_hw
+    from mtl_das_pytorch_amd.models.multi_classifier import Multi_Classifier
+    assert _mixed6_hw((100, 250)) == (4, 13)
+    assert _mixed6_hw((299, 299)) == (17, 17)  # torchvision's comment sizes
+    m = Multi_Classifier(aux_logits=True).train()
+    with pytest.raises(RuntimeError, match="too small"):
+        m(torch.randn(2, 1, 100, 250))
+    with pytest.raises(ValueError, match="4 x 13"):
+        InceptionProgram(m, 2, "cpu")
