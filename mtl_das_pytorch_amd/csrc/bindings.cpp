@@ -81,8 +81,6 @@ BNArgs parse_bn(const py::dict& d) {
   b.momentum = (float)F(d, "momentum", 0.1);
   b.training = (int)I(d, "training", 1);
   b.consts = P<float>(d, "consts");
-  b.fin = (int)I(d, "fin", 0);
-  if (b.fin && (!b.consts || !b.training)) throw std::runtime_error("bn: fin needs training and consts");
   return b;
 }
 
@@ -116,7 +114,9 @@ void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
 py::tuple conv_workspace(int mode, int cfg, int G, py::dict d) {
   ConvArgs a = parse_conv(mode, d);
   int64_t ws = 0, nt = 0;
-  const int rc = cfg >= CONV_LDS_CFG0 ? conv_lds_workspace(mode, a, G, cfg, ws, nt) : 0;
+  int rc = 0;
+  if (cfg >= CONV_DEEP_CFG0) rc = (cfg < CONV_DEEP_CFG0 + CONV_DEEP_NCFG && !(mode != MODE_FWD && a.aol)) ? 0 : -1;
+  else if (cfg >= CONV_LDS_CFG0) rc = conv_lds_workspace(mode, a, G, cfg, ws, nt);
   return py::make_tuple(rc, ws, nt);
 }
 
@@ -170,14 +170,6 @@ ConvArgs parse_conv(int mode, py::dict d) {
   }
   a.ws = P<float>(d, "ws");
   a.cnt = P<unsigned>(d, "cnt");
-  if (d.contains("fin") && !d["fin"].is_none()) {  // producer-side BN finalize (last block)
-    py::dict f = d["fin"].cast<py::dict>();
-    a.obn = parse_bn(f["bn"].cast<py::dict>());
-    a.fcnt = P<unsigned>(f, "cnt");
-    if ((mode != MODE_FWD) || !a.fcnt || !a.obn.training || a.obn.stats != a.stats || !a.obn.consts ||
-        a.obn.C != a.N)
-      throw std::runtime_error("conv: bad BN-finalize arguments");
-  }
   return a;
 }
 
@@ -381,6 +373,8 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("conv_workspace", &conv_workspace);
   m.attr("CONV_LDS_CFG0") = CONV_LDS_CFG0;
   m.attr("CONV_LDS_NCFG") = CONV_LDS_NCFG;
+  m.attr("CONV_DEEP_CFG0") = CONV_DEEP_CFG0;
+  m.attr("CONV_DEEP_NCFG") = CONV_DEEP_NCFG;
   m.def("wgrad", &wgrad);
   m.def("wgrad_finalize", &wgrad_finalize);
   m.def("tail_fwd", &tail_fwd);

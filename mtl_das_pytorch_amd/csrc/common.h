@@ -137,9 +137,6 @@ struct BNArgs {
   float* consts;         // optional [G][4][C] (+ z * 4C): scale, shift, mean, invstd of the current batch,
                          // written by the forward tail's block 0 (training) and read by every backward
                          // kernel of this BN -- 4 floats per channel instead of 2 x NREP fp64 replicas
-  int fin;               // training: the producing conv's last block already reduced the replicas into
-                         // consts and updated the running statistics (bn_finalize) -- consumers read the
-                         // 4 constants instead of 2 x NREP fp64 replicas per channel
 };
 
 // BN constants of channel c of group z: out = y * scale + shift == gamma * (y - mean) * invstd + beta.
@@ -148,11 +145,6 @@ struct BNArgs {
 DEV void bn_channel(const BNArgs& a, int z, int c, bool update_running, float& scale, float& shift, float& mean,
                     float& inv) {
   float var;
-  if (a.training && a.fin) {
-    const float* k = a.consts + (int64_t)z * 4 * a.C;
-    scale = k[c]; shift = k[a.C + c]; mean = k[2 * a.C + c]; inv = k[3 * a.C + c];
-    return;
-  }
   if (a.training) {
     const double* st = a.stats + (int64_t)z * NREP * 2 * a.C;
     double s = 0.0, ss = 0.0;
@@ -203,38 +195,7 @@ DEV void bn_prepare(const BNArgs& a, int z, float* s_scale, float* s_shift, floa
     if (s_invstd) s_invstd[c] = inv;
     if (kz) { kz[c] = sc; kz[a.C + c] = sh; kz[2 * a.C + c] = mu; kz[3 * a.C + c] = inv; }
   }
-  if (update_running && a.training && !a.fin && threadIdx.x == 0 && a.nbt) a.nbt[z] += 1;
-}
-
-// Producer-side BN finalize (conv epilogues, ConvArgs::fcnt): every block of group z, after its replica
-// atomics, takes an arrival ticket (agent-scope release / acquire, as the split-K reduction of conv_lds.hip);
-// the last of `total` blocks reduces the NREP replicas of all C channels once, publishes the batch constants
-// and updates the running statistics -- the work every consumer block used to repeat.  Call from all
-// threads of the block; s_flag is one int of LDS.
-DEV void bn_finalize(const BNArgs& b, unsigned* cnt, int z, unsigned total, int* s_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const unsigned t = __hip_atomic_fetch_add(cnt + z, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_flag[0] = t == total - 1;
-  }
-  __syncthreads();
-  if (!s_flag[0]) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __hip_atomic_store(cnt + z, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reusable next launch
-  }
-  __syncthreads();
-  BNArgs r = b;
-  r.fin = 0;
-  float* kz = b.consts + (int64_t)z * 4 * b.C;
-  for (int c = threadIdx.x; c < b.C; c += blockDim.x) {
-    float sc, sh, mu, inv;
-    bn_channel(r, z, c, true, sc, sh, mu, inv);
-    kz[c] = sc; kz[b.C + c] = sh; kz[2 * b.C + c] = mu; kz[3 * b.C + c] = inv;
-  }
-  if (threadIdx.x == 0 && b.nbt) b.nbt[z] += 1;
+  if (update_running && a.training && threadIdx.x == 0 && a.nbt) a.nbt[z] += 1;
 }
 
 }  // namespace mda

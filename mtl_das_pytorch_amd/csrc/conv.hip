@@ -78,11 +78,21 @@ DEV void aol_apply(bf16x8* bfr, const float4 (*gq)[2], const uint4* yq, uint32_t
 // Normalise-on-load: the 8 channels [c, c+8) of an im2col fragment are pre-BN conv outputs y; the operand
 // is act(y * scale + shift) (act = ReLU or identity), rounded to bf16 exactly as the BN tail that used to
 // materialise it.  Fragments of zero padding (bit f of okm clear) stay zero.
+// The stage's 8 scale and 8 shift constants (k[0..7], k[8..15]) are read from LDS when the stage's loads are
+// issued (nol_fetch), not here: a read at consumption time put an LDS round trip into every K step's chain.
+DEV void nol_fetch(float* k, int c, const float* s_nol, int Cs) {
+  const float4* p0 = reinterpret_cast<const float4*>(s_nol + c);
+  const float4* p1 = reinterpret_cast<const float4*>(s_nol + Cs + c);
+  const float4 a0 = p0[0], a1 = p0[1], b0 = p1[0], b1 = p1[1];
+  k[0] = a0.x; k[1] = a0.y; k[2] = a0.z; k[3] = a0.w; k[4] = a1.x; k[5] = a1.y; k[6] = a1.z; k[7] = a1.w;
+  k[8] = b0.x; k[9] = b0.y; k[10] = b0.z; k[11] = b0.w; k[12] = b1.x; k[13] = b1.y; k[14] = b1.z; k[15] = b1.w;
+}
+
 template <int FM>
-DEV void nol_apply(bf16x8* bfr, uint32_t okm, int c, const float* s_nol, int Cs, bool relu) {
+DEV void nol_apply(bf16x8* bfr, uint32_t okm, const float* k, bool relu) {
   float sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { sc[j] = s_nol[c + j]; sh[j] = s_nol[Cs + c + j]; }
+  for (int j = 0; j < 8; ++j) { sc[j] = k[j]; sh[j] = k[8 + j]; }
 #pragma unroll
   for (int f = 0; f < FM; ++f) {
     if (!((okm >> f) & 1)) continue;
@@ -136,14 +146,19 @@ DEV void conv_load_stage(const ConvArgs& a, const int* s_tab, int ks, int kgl, i
         yq[f] = *reinterpret_cast<const uint4*>(a.ao.y + a.ao.ygs * z + pix * a.ao.ldy + c);
       }
     } else {
-      bfr[f] = ok ? *reinterpret_cast<const bf16x8*>(sb + ((int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw) * sld + c) : zero8;
+      // unconditional load from a valid address, zeroed after: no exec-masked branch around the load, so the
+      // waitcnt pass can count the loads of every pipeline stage exactly instead of draining with vmcnt(0)
+      const bf16_t* q = ok ? sb + ((int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw) * sld + c : sb;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(q);
+      bfr[f] = ok ? v : zero8;
     }
     okm |= (uint32_t)ok << f;
   }
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
     const int n = n_base + i * 16 + l16;
-    afr[i] = n < a.Npad ? *reinterpret_cast<const bf16x8*>(wz + (int64_t)n * a.Kpad + ks * 32 + kgl * 8) : zero8;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(wz + (int64_t)(n < a.Npad ? n : 0) * a.Kpad + ks * 32 + kgl * 8);
+    afr[i] = n < a.Npad ? v : zero8;
   }
 }
 
@@ -151,7 +166,9 @@ DEV void conv_load_stage(const ConvArgs& a, const int* s_tab, int ks, int kgl, i
 // its share of K with a two-stage register pipeline (loads of step k+1 in flight during the MFMAs of
 // step k); KSPLIT > 1 partial accumulators are summed through LDS, so small-M / long-K layers (the 5x11
 // and 9x21 stages, K up to 1152) get up to 4x shorter dependency chains.
-template <int MODE, int WN, int WM, int WAVES_N, int WAVES_M, int KSPLIT>
+// PD = register pipeline depth: fragment loads of PD - 1 K-steps are in flight while one step's MFMAs run.
+// The small-M layers (grids below one wave per SIMD) are bound by this load latency, not by occupancy.
+template <int MODE, int WN, int WM, int WAVES_N, int WAVES_M, int KSPLIT, int PD>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   static_assert(WAVES_N * WAVES_M * KSPLIT == 4, "4 waves per block");
   constexpr int FN = WN / 16, FM = WM / 16;
@@ -224,7 +241,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const bool aol_relu = a.ao.kind == ACT_RELU;
   __syncthreads();
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wave index through readfirstlane: the compiler then knows every K-loop bound and guard below is
+  // wave-uniform and branches on it.  An MFMA ignores EXEC, so a guard lowered to an exec mask would still
+  // accumulate the stale fragments of a step past kend (seen with the depth-4 pipeline's remainder steps).
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wn = wid % WAVES_N, wm = (wid / WAVES_N) % WAVES_M, wk = wid / (WAVES_N * WAVES_M);
   const int n_base = blockIdx.y * BN_T + wn * WN;
   const int m_base = blockIdx.x * BM_T + wm * WM;
@@ -281,26 +301,43 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       }
   };
   if (PREFETCH_Y) load_y();
-  bf16x8 a0[FN], b0[FM], a1[FN], b1[FM];
-  uint32_t ok0 = 0, ok1 = 0;
-  int c0 = 0, c1 = 0;
-  float4 g0[FM][2], g1[FM][2];  // AOL raw stage data (eliminated in the other modes)
-  uint4 y0[FM], y1[FM];
-#define LOAD_STAGE(KS, AF, BF, OK, CC, GQ, YQ) \
-  conv_load_stage<MODE, FN, FM>(a, s_tab, KS, kgl, l16, n_base, pb, py, px, pv, base0, base1, ld0, ld1, wz, AF, BF, OK, CC, GQ, YQ, z)
+  bf16x8 af[PD][FN], bq[PD][FM];
+  uint32_t okq[PD];
+  int ccq[PD];
+  constexpr int PG = AOL ? PD : 1;  // AOL raw stage data (eliminated in the other modes)
+  float nk[NOL ? PD : 1][16];       // NOL: the stage's BN scale / shift
+  float4 gq[PG][FM][2];
+  uint4 yq[PG][FM];
+#define LOAD_STAGE(KS, J) do { \
+  conv_load_stage<MODE, FN, FM>(a, s_tab, KS, kgl, l16, n_base, pb, py, px, pv, base0, base1, ld0, ld1, wz, af[J], bq[J], \
+                                okq[J], ccq[J], gq[AOL ? (J) : 0], yq[AOL ? (J) : 0], z);                   \
+  if (NOL) nol_fetch(nk[NOL ? (J) : 0], ccq[J], s_nol, a.Cs); } while (0)
   // NOL / AOL: the operand transform runs when the stage is consumed, so the loads stay in flight meanwhile
-#define MMA_STAGE(AF, BF, OK, CC, GQ, YQ)                                                                 \
-  if (NOL) nol_apply<FM>(BF, OK, CC, s_nol, a.Cs, nol_relu);                                              \
-  if (AOL) aol_apply<FM>(BF, GQ, YQ, OK, CC, s_aol, a.Cs, aol_relu);                                      \
+#define MMA_STAGE(J)                                                                                      \
+  if (NOL) nol_apply<FM>(bq[J], okq[J], nk[NOL ? (J) : 0], nol_relu);                                     \
+  if (AOL) aol_apply<FM>(bq[J], gq[AOL ? (J) : 0], yq[AOL ? (J) : 0], okq[J], ccq[J], s_aol, a.Cs, aol_relu); \
   _Pragma("unroll") for (int i = 0; i < FN; ++i)                                                          \
   _Pragma("unroll") for (int f = 0; f < FM; ++f)                                                          \
-    acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AF[i], BF[f], acc[i][f], 0, 0, 0);
-  if (kbeg < kend) LOAD_STAGE(kbeg, a0, b0, ok0, c0, g0, y0);
-  for (int ks = kbeg; ks < kend; ks += 2) {
-    if (ks + 1 < kend) LOAD_STAGE(ks + 1, a1, b1, ok1, c1, g1, y1);
-    MMA_STAGE(a0, b0, ok0, c0, g0, y0)
-    if (ks + 2 < kend) LOAD_STAGE(ks + 2, a0, b0, ok0, c0, g0, y0);
-    if (ks + 1 < kend) { MMA_STAGE(a1, b1, ok1, c1, g1, y1) }
+    acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[J][i], bq[J][f], acc[i][f], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < PD - 1; ++j)
+    if (kbeg + j < kend) LOAD_STAGE(kbeg + j, j);
+  int ks = kbeg;
+  // steady state: every load of the PD steps is in range, so the body has no branches and the waitcnt pass
+  // keeps PD - 1 stages of loads in flight (a guarded body makes it drain with vmcnt(0) at each join)
+  for (; ks + 2 * PD - 2 < kend; ks += PD) {
+#pragma unroll
+    for (int j = 0; j < PD; ++j) {
+      LOAD_STAGE(ks + j + PD - 1, (j + PD - 1) % PD);
+      MMA_STAGE(j)
+    }
+  }
+  for (; ks < kend; ks += PD) {  // the last 1..2 PD-blocks of steps
+#pragma unroll
+    for (int j = 0; j < PD; ++j) {
+      if (ks + j + PD - 1 < kend) LOAD_STAGE(ks + j + PD - 1, (j + PD - 1) % PD);
+      if (ks + j < kend) { MMA_STAGE(j) }
+    }
   }
 #undef LOAD_STAGE
 #undef MMA_STAGE
@@ -440,10 +477,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         atomicAdd(dst + gb + ((int64_t)rep * (want_bnb ? 3 : 2) + which) * nlim + n, (double)v);
       }
     }
-  }
-  if (is_fwd<MODE>() && a.fcnt) {  // producer-side BN finalize by the last block of the group
-    __shared__ int s_fin;
-    bn_finalize(a.obn, a.fcnt, z, gridDim.x * gridDim.y, &s_fin);
   }
 }
 
@@ -898,8 +931,16 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
 template <int MODE>
 static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
   const int M = a.B * a.Ho * a.Wo;
+  const bool deep = cfg >= CONV_DEEP_CFG0;  // pipeline depth 4 (the same tile as cfg - CONV_DEEP_CFG0)
+  if (deep) {
+    if (has_aol<MODE>()) return -1;  // apply-on-load stages hold fp32 g + bf16 y: too many registers
+    cfg -= CONV_DEEP_CFG0;
+  }
   const int nkg4 = ((a.Kpad / 8) + 3) & ~3;
 #define LAUNCH_CFG(WN, WM, WAN, WAM, KS)                                                                \
+  if (!deep) LAUNCH_PD(WN, WM, WAN, WAM, KS, 2)                                                         \
+  else if constexpr (!has_aol<MODE>()) LAUNCH_PD(WN, WM, WAN, WAM, KS, 4)
+#define LAUNCH_PD(WN, WM, WAN, WAM, KS, PD)                                                             \
   {                                                                                                     \
     constexpr int TILE = (WN / 16) * (WM / 16) * 4 * 64;                                                \
     size_t red = (size_t)(KS - 1) * WAN * WAM * TILE;                                                   \
@@ -907,32 +948,32 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
     size_t lds = (size_t)nkg4 * 4 + (red > st2 ? red : st2) * 4 +                                        \
                  (a.nol ? 2 * a.Cs * 4 : (a.bpart ? 8 * WN * WAN * 4 : 0) + (a.aol ? 5 * a.Cs * 4 : 0));    \
     dim3 grid((M + WM * WAM - 1) / (WM * WAM), (a.N + WN * WAN - 1) / (WN * WAN), G);                    \
-    hipLaunchKernelGGL((conv_igemm_kernel<MODE, WN, WM, WAN, WAM, KS>), grid, dim3(256), lds, st, a);   \
-    break;                                                                                              \
+    hipLaunchKernelGGL((conv_igemm_kernel<MODE, WN, WM, WAN, WAM, KS, PD>), grid, dim3(256), lds, st, a); \
   }
   switch (cfg) {
-    case 0: LAUNCH_CFG(16, 64, 1, 4, 1)
-    case 1: LAUNCH_CFG(32, 32, 1, 4, 1)
-    case 2: LAUNCH_CFG(32, 32, 2, 2, 1)
-    case 3: LAUNCH_CFG(64, 32, 2, 2, 1)
-    case 4: LAUNCH_CFG(32, 16, 2, 2, 1)
-    case 5: LAUNCH_CFG(16, 32, 1, 2, 2)
-    case 6: LAUNCH_CFG(32, 16, 1, 2, 2)
-    case 7: LAUNCH_CFG(32, 16, 2, 1, 2)
-    case 8: LAUNCH_CFG(32, 16, 1, 1, 4)
-    case 9: LAUNCH_CFG(64, 16, 1, 1, 4)
-    case 10: LAUNCH_CFG(16, 16, 1, 1, 4)
-    case 11: LAUNCH_CFG(64, 32, 1, 1, 4)
-    case 12: LAUNCH_CFG(16, 32, 1, 4, 1)
-    case 13: LAUNCH_CFG(16, 16, 1, 4, 1)
+    case 0: LAUNCH_CFG(16, 64, 1, 4, 1) break;
+    case 1: LAUNCH_CFG(32, 32, 1, 4, 1) break;
+    case 2: LAUNCH_CFG(32, 32, 2, 2, 1) break;
+    case 3: LAUNCH_CFG(64, 32, 2, 2, 1) break;
+    case 4: LAUNCH_CFG(32, 16, 2, 2, 1) break;
+    case 5: LAUNCH_CFG(16, 32, 1, 2, 2) break;
+    case 6: LAUNCH_CFG(32, 16, 1, 2, 2) break;
+    case 7: LAUNCH_CFG(32, 16, 2, 1, 2) break;
+    case 8: LAUNCH_CFG(32, 16, 1, 1, 4) break;
+    case 9: LAUNCH_CFG(64, 16, 1, 1, 4) break;
+    case 10: LAUNCH_CFG(16, 16, 1, 1, 4) break;
+    case 11: LAUNCH_CFG(64, 32, 1, 1, 4) break;
+    case 12: LAUNCH_CFG(16, 32, 1, 4, 1) break;
+    case 13: LAUNCH_CFG(16, 16, 1, 4, 1) break;
     default: return -1;
   }
 #undef LAUNCH_CFG
+#undef LAUNCH_PD
   return (int)hipGetLastError();
 }
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
-  if (cfg >= CONV_LDS_CFG0) {  // LDS-staged kernels (conv_lds.hip)
+  if (cfg >= CONV_LDS_CFG0 && cfg < CONV_DEEP_CFG0) {  // LDS-staged kernels (conv_lds.hip)
     const int m = mode == MODE_FWD ? (a.nol ? MODE_FWD_NOL : MODE_FWD) : (a.bpart ? MODE_DGRAD_BNS : MODE_DGRAD);
     return launch_conv_lds(m, a, G, cfg, st);
   }

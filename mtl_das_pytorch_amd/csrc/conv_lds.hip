@@ -401,8 +401,6 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
       }
     }
   }
-  // producer-side BN finalize: the last of the group's output tiles (the split-K reducers) to arrive
-  if (FWD && a.fcnt) bn_finalize(a.obn, a.fcnt, z, gridDim.x * gridDim.y / pl.splits, s_flag);
 }
 
 #undef PSEL

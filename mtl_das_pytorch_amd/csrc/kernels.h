@@ -71,9 +71,6 @@ struct ConvArgs {
   // block resets it), sized by conv_lds_workspace
   float* ws;
   unsigned* cnt;
-  // FWD training, optional (fcnt null = off): the last block finalizes the output BN (common.h bn_finalize)
-  BNArgs obn;
-  unsigned* fcnt;  // [G] arrival tickets, zero-initialised, reset by the finalizing block
 };
 
 // One output-pixel phase of an LDS-staged conv launch (conv_lds.hip): output pixels (b, oy0 + i*qy,
@@ -242,6 +239,8 @@ struct AdamArgs {
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 // LDS-staged implicit GEMM (conv_lds.hip): cfg = CONV_LDS_CFG0 + 8 * tile + 4 * (KC == 128) + log2(splits)
 constexpr int CONV_LDS_CFG0 = 16, CONV_LDS_NCFG = 64;
+// register-pipelined conv_igemm tiles 0-13 at pipeline depth 4 (conv.hip): cfg = CONV_DEEP_CFG0 + tile
+constexpr int CONV_DEEP_CFG0 = 128, CONV_DEEP_NCFG = 14;
 int launch_conv_lds(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 // fp32 workspace floats and ticket count a cfg needs (0 when it does not split K); < 0: cfg invalid for a
 int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_floats, int64_t& ntickets);

@@ -59,7 +59,7 @@ def generate(n: int, seed: int = 0, device="cpu", in_channels: int = 1, height: 
 
     dev = torch.device(device)
     if backend is None:
-        backend = "hip" if dev.type == "cuda" else "torch"
+        backend = os.environ.get("MDA_SYNTH_BACKEND") or ("hip" if dev.type == "cuda" else "torch")
     if backend == "hip":
         return _generate_hip(n, dev, distance, event, x0, t0, jitter, snr, noise_seed, in_channels, height, width,
                              noise, dtype)

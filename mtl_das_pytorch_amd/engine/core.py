@@ -279,12 +279,6 @@ class BNLayer:
         self.part = arena.zeroed((self.G, NREP, 3, self.C), torch.float64)
         # batch constants (scale, shift, mean, invstd) published by the forward tail for the backward
         self.consts = arena.empty((self.G, 4, self.C), torch.float32)
-        # producer-side finalize (csrc/common.h bn_finalize): the producing conv's last block reduces the
-        # replicas once and publishes the constants; consumers read 4 floats per channel.  Off under SyncBN
-        # (the replicas are all-reduced after the conv) and with MDA_BN_FIN=0.
-        import os
-        self.fin = flat.bn_world == 1 and os.environ.get("MDA_BN_FIN", "1") == "1"
-        self.fin_cnt = torch.zeros(self.G, dtype=torch.int32, device=flat.device) if self.fin else None
         self.arena = arena
         self.dzbuf = None
 
@@ -295,7 +289,7 @@ class BNLayer:
                 "run_mean": P(f.bn_mean, f.bn_offsets[id(m0)]), "run_var": P(f.bn_var, f.bn_offsets[id(m0)]),
                 "nbt": P(f.bn_nbt, f.bn_index[id(m0)]), "pstride": self.pstride, "C": self.C, "count": self.count,
                 "eps": self.eps, "momentum": self.momentum, "training": 1 if training else 0,
-                "consts": P(self.consts), "fin": 1 if (training and self.fin) else 0}
+                "consts": P(self.consts)}
 
     def grad_ptrs(self) -> dict:
         f = self.flat
@@ -464,8 +458,6 @@ class ConvLayer:
              "B": self.B, "Hs": self.Hi, "Ws": self.Wi, "Ho": self.Ho, "Wo": self.Wo, "N": self.Co, "Npad": self.Npad,
              "Cs": self.Cs, "KH": self.KH, "KW": self.KW, "sh": self.sh, "sw": self.sw, "ph": self.ph, "pw": self.pw,
              "Kpad": self.Kpad}
-        if bn is not None and training and bn.fin:
-            d["fin"] = {"bn": dict(bn.args(True), fin=0), "cnt": P(bn.fin_cnt)}
         return (0, self.fwd_cfg(self.Co, self.M_out), self.G, d)
 
     def dgrad_args(self, dy: Act, dx_out: Act) -> tuple:

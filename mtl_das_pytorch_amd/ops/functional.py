@@ -72,6 +72,7 @@ def _fwd_cfg(N, M):
 
 
 CONV_LDS_CFG0, CONV_LDS_NCFG = 16, 64  # csrc/kernels.h: LDS-staged conv configs (conv_lds.hip)
+CONV_DEEP_CFG0, CONV_DEEP_NCFG = 128, 14  # conv_igemm tiles 0-13 at register-pipeline depth 4 (conv.hip)
 LDS_TILES = [(64, 64), (128, 64), (64, 128), (128, 128), (32, 64), (64, 32), (32, 32), (128, 16)]
 
 

@@ -31,6 +31,14 @@ def _load():
                 _b.build(verbose=False)
         if pkg_dir not in sys.path:
             sys.path.insert(0, pkg_dir)
+        alt = os.environ.get("MDA_EXT_PATH")  # A/B measurements: another build of the same extension
+        if alt:
+            from importlib import util as _ilu
+            spec = _ilu.spec_from_file_location("mtl_das_pytorch_amd._mda_hip", alt)
+            _LIB = _ilu.module_from_spec(spec)
+            spec.loader.exec_module(_LIB)
+            sys.modules["mtl_das_pytorch_amd._mda_hip"] = _LIB
+            return
         _LIB = importlib.import_module("mtl_das_pytorch_amd._mda_hip")
     except Exception as e:  # pragma: no cover - exercised on broken installs
         _ERR = e

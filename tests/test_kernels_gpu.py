@@ -139,7 +139,8 @@ def test_conv_wgrad_patch(fn, case, cfg, nol):
 
 
 # conv.hip default tile, and conv_lds.hip LDS-staged configs (tile, K chunk, K split) -- see test_conv_lds_gpu.py
-LDS_SAMPLE = [None, 16 + 8 * 0 + 0 + 0, 16 + 8 * 1 + 4 + 2, 16 + 8 * 7 + 0 + 3]
+# heuristic, three LDS-staged configs, and two depth-4 register-pipelined tiles (conv.hip, cfg 128 + tile)
+LDS_SAMPLE = [None, 16 + 8 * 0 + 0 + 0, 16 + 8 * 1 + 4 + 2, 16 + 8 * 7 + 0 + 3, 128 + 8, 128 + 11]
 
 
 @pytest.mark.parametrize("cfg", LDS_SAMPLE)

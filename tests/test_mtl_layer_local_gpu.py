@@ -56,7 +56,11 @@ def engine_step():
     from mtl_das_pytorch_amd.engine.mtl import MTLProgram
     from mtl_das_pytorch_amd.engine.tune import autotune_program
     from mtl_das_pytorch_amd.models import MTL_Net
-    torch.backends.cudnn.allow_tf32 = False  # the fp32 references must be fp32 (MIOpen / hipBLASLt)
+    # the single-op fp32 references run on PyTorch's native im2col + GEMM convolution, not MIOpen: one run
+    # of this module hit an illegal address inside the reference conv backward (MIOpen solver choice)
+    flags = (torch.backends.cudnn.enabled, torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32)
+    torch.backends.cudnn.enabled = False
+    torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.manual_seed(0)
     B = 32
@@ -73,7 +77,8 @@ def engine_step():
     prog.bwd.run()
     torch.cuda.synchronize()
     prog.flat.sync_module_grads()
-    return model, prog, X, labels
+    yield model, prog, X, labels
+    torch.backends.cudnn.enabled, torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32 = flags
 
 
 class Checker:

@@ -2,8 +2,8 @@
 
     python tools/conv_probe.py B H W Ci Co KH KW s p [--dgrad]
 
-Prints, per config: plain, +fused BN sums (forward) / +fused BN-backward sums (dgrad), and +normalise-on-load
-(forward), so fixed costs (BN-constant preparation, fp64 replica atomics) can be told apart from the
+Prints, per config: plain, +fused BN sums (forward) / +fused BN-backward sums (dgrad), +normalise-on-load
+(forward; training statistics from the replicas) and +normalise-on-load with eval statistics (no replica reduction), so fixed costs (BN-constant preparation, fp64 replica atomics) can be told apart from the
 main loop.
 """
 import argparse
@@ -48,7 +48,8 @@ def main():
     for c in CONV_CFGS:
         row = [c]
         variants = ([{}, {"bn_stats": (yb, bn, part, 1)}] if a.dgrad else
-                    [{}, {"stats": stats}, {"stats": stats, "nol": (bn, 1)}])
+                    [{}, {"stats": stats}, {"stats": stats, "nol": (bn, 1)},
+                     {"stats": stats, "nol": (dict(bn, training=0), 1)}])
         ok = True
         for kw in variants:
             try:
@@ -65,7 +66,7 @@ def main():
     fl = 2 * a.B * Ho * Wo * a.Co * a.Ci * a.KH * a.KW
     print(f"M={a.B * Ho * Wo} N={a.Co if not a.dgrad else a.Ci} K={a.Ci * a.KH * a.KW if not a.dgrad else a.Co * a.KH * a.KW}"
           f" {fl / 1e9:.3f} GFLOP")
-    hdr = ["cfg", "plain", "+bnb"] if a.dgrad else ["cfg", "plain", "+stats", "+nol"]
+    hdr = ["cfg", "plain", "+bnb"] if a.dgrad else ["cfg", "plain", "+stats", "+nol", "+nol_ev"]
     print("  ".join(f"{h:>8s}" for h in hdr))
     for r in sorted(res, key=lambda r: r[1])[:a.top]:
         print("  ".join([f"{r[0]:8d}"] + [f"{v:8.2f}" for v in r[1:]]))

@@ -36,7 +36,7 @@ def main():
         m = build_model(name)
         prog = InceptionProgram(m, args.batch, "cuda") if name == "multi_classifier" else MTLProgram(m, args.batch, "cuda")
         n0 = len(cache)
-        autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose=False, measure=True)
+        autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose=True, measure=True)
         print(f"{name}: {len(cache) - n0} new entries in {time.time() - t0:.1f} s", flush=True)
         del prog, m
         torch.cuda.empty_cache()
