@@ -81,6 +81,8 @@ BNArgs parse_bn(const py::dict& d) {
   b.momentum = (float)F(d, "momentum", 0.1);
   b.training = (int)I(d, "training", 1);
   b.consts = P<float>(d, "consts");
+  b.nrep = (int)I(d, "nrep", NREP);
+  if (b.nrep < 1 || b.nrep > NREP || (b.nrep & (b.nrep - 1))) throw std::runtime_error("bn: nrep must be a power of two <= NREP");
   return b;
 }
 
@@ -131,6 +133,8 @@ ConvArgs parse_conv(int mode, py::dict d) {
   a.ogs = I(d, "ogs");
   a.ldo = (int)I(d, "ldo");
   a.stats = P<double>(d, "stats");
+  a.stats_nrep = (int)I(d, "stats_nrep", NREP);
+  if (a.stats_nrep < 1 || a.stats_nrep > NREP) throw std::runtime_error("conv: bad stats_nrep");
   a.B = (int)I(d, "B"); a.Hs = (int)I(d, "Hs"); a.Ws = (int)I(d, "Ws"); a.Ho = (int)I(d, "Ho"); a.Wo = (int)I(d, "Wo");
   a.N = (int)I(d, "N"); a.Npad = (int)I(d, "Npad"); a.Cs = (int)I(d, "Cs");
   a.KH = (int)I(d, "KH"); a.KW = (int)I(d, "KW"); a.sh = (int)I(d, "sh"); a.sw = (int)I(d, "sw");

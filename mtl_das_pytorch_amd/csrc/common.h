@@ -137,7 +137,16 @@ struct BNArgs {
   float* consts;         // optional [G][4][C] (+ z * 4C): scale, shift, mean, invstd of the current batch,
                          // written by the forward tail's block 0 (training) and read by every backward
                          // kernel of this BN -- 4 floats per channel instead of 2 x NREP fp64 replicas
+  int nrep;              // replicas in use (power of two <= NREP; the producer wrote blockIdx.x % nrep):
+                         // small-M layers have few producer blocks, and every consumer block reads all of
+                         // them (Model C's 1x6 layers: 32 replicas x 448 channels = 229 KB per block)
 };
+
+template <int R>
+DEV void bn_rep_sum(const double* st, int C, int c, double& s, double& ss) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) { s += st[r * 2 * C + c]; ss += st[r * 2 * C + C + c]; }
+}
 
 // BN constants of channel c of group z: out = y * scale + shift == gamma * (y - mean) * invstd + beta.
 // Training: batch statistics from the NREP replicas of the conv-epilogue sums (and, when requested,
@@ -148,8 +157,14 @@ DEV void bn_channel(const BNArgs& a, int z, int c, bool update_running, float& s
   if (a.training) {
     const double* st = a.stats + (int64_t)z * NREP * 2 * a.C;
     double s = 0.0, ss = 0.0;
-#pragma unroll
-    for (int r = 0; r < NREP; ++r) { s += st[r * 2 * a.C + c]; ss += st[r * 2 * a.C + a.C + c]; }
+    switch (a.nrep) {  // a compile-time trip count keeps all loads of the reduction in flight
+      case 1: bn_rep_sum<1>(st, a.C, c, s, ss); break;
+      case 2: bn_rep_sum<2>(st, a.C, c, s, ss); break;
+      case 4: bn_rep_sum<4>(st, a.C, c, s, ss); break;
+      case 8: bn_rep_sum<8>(st, a.C, c, s, ss); break;
+      case 16: bn_rep_sum<16>(st, a.C, c, s, ss); break;
+      default: bn_rep_sum<NREP>(st, a.C, c, s, ss); break;
+    }
     const double inv_n = 1.0 / (double)a.count;
     const double md = s * inv_n;
     mean = (float)md;

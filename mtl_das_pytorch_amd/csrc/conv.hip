@@ -459,7 +459,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   }
   if (want_red) {
     __syncthreads();
-    const int rep = blockIdx.x % NREP;
+    const int rep = blockIdx.x % (want_bnb ? NREP : a.stats_nrep);
     // forward: [G][NREP][2][N] (sum y, sum y^2); fused BN backward: rows 0/1 (2 with a BN2 residual) of
     // the tail's [G][NREP][3][bN]
     const int nrow = want_bnb ? (a.br_bn ? 3 : 2) : 2;

@@ -33,7 +33,8 @@ struct ConvArgs {
   void* out;  // FWD: bf16, DGRAD: fp32; [M][ldo] (+ z * ogs)
   int64_t ogs;
   int ldo;
-  double* stats;  // FWD: [G][NREP][2][N] fp64 (may be null)
+  double* stats;  // FWD: [G][NREP][2][N] fp64 (may be null); replica blockIdx.x % stats_nrep
+  int stats_nrep;
   int B, Hs, Ws, Ho, Wo;
   int N, Npad, Cs;
   int KH, KW, sh, sw, ph, pw;

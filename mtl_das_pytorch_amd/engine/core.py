@@ -279,6 +279,12 @@ class BNLayer:
         self.part = arena.zeroed((self.G, NREP, 3, self.C), torch.float64)
         # batch constants (scale, shift, mean, invstd) published by the forward tail for the backward
         self.consts = arena.empty((self.G, 4, self.C), torch.float32)
+        # forward replicas in use: about one per 256 pixels (the producing conv then has at most ~16 blocks
+        # per replica address), so small maps are not read back as 32 mostly-empty replicas by every
+        # consumer block (MDA_BN_NREP overrides)
+        import os
+        fixed = int(os.environ.get("MDA_BN_NREP", "0"))
+        self.nrep = fixed or min(NREP, 1 << max(0, math.ceil(math.log2(max(1, count) / 256))))
         self.arena = arena
         self.dzbuf = None
 
@@ -289,7 +295,7 @@ class BNLayer:
                 "run_mean": P(f.bn_mean, f.bn_offsets[id(m0)]), "run_var": P(f.bn_var, f.bn_offsets[id(m0)]),
                 "nbt": P(f.bn_nbt, f.bn_index[id(m0)]), "pstride": self.pstride, "C": self.C, "count": self.count,
                 "eps": self.eps, "momentum": self.momentum, "training": 1 if training else 0,
-                "consts": P(self.consts)}
+                "consts": P(self.consts), "nrep": self.nrep}
 
     def grad_ptrs(self) -> dict:
         f = self.flat
@@ -455,6 +461,7 @@ class ConvLayer:
              "bias": P(f.params, f.off(self.mods[0].bias)) if self.has_bias else 0, "bgs": self.bstride,
              "out": out.p, "ogs": out.gs, "ldo": out.ld,
              "stats": P(bn.stats) if (bn is not None and training) else 0,
+             "stats_nrep": bn.nrep if bn is not None else NREP,
              "B": self.B, "Hs": self.Hi, "Ws": self.Wi, "Ho": self.Ho, "Wo": self.Wo, "N": self.Co, "Npad": self.Npad,
              "Cs": self.Cs, "KH": self.KH, "KW": self.KW, "sh": self.sh, "sw": self.sw, "ph": self.ph, "pw": self.pw,
              "Kpad": self.Kpad}
