@@ -82,6 +82,8 @@ BNArgs parse_bn(const py::dict& d) {
   b.training = (int)I(d, "training", 1);
   b.consts = P<float>(d, "consts");
   b.nrep = (int)I(d, "nrep", NREP);
+  b.pnrep = (int)I(d, "pnrep", NREP);
+  if (b.pnrep < 1 || b.pnrep > NREP) throw std::runtime_error("bn: bad pnrep");
   if (b.nrep < 1 || b.nrep > NREP || (b.nrep & (b.nrep - 1))) throw std::runtime_error("bn: nrep must be a power of two <= NREP");
   return b;
 }

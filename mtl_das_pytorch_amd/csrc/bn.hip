@@ -324,7 +324,7 @@ DEV void bnb_reduce_impl(const TailArgs& a) {
     float v = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) v += s_part[r][k][q];
-    atomicAdd(a.part + (((int64_t)z * NREP + chunk % NREP) * 3 + k) * a.C + cblk + q, (double)v);
+    atomicAdd(a.part + (((int64_t)z * NREP + chunk % a.bn.pnrep) * 3 + k) * a.C + cblk + q, (double)v);
   }
 }
 
@@ -362,7 +362,7 @@ DEV void bnb_apply_impl(const TailArgs& a) {
       const int item = t % NI, q = t / NI;
       const int k = item / CB, j = item - k * CB;
       double v = 0.0;
-      for (int r = q; r < NREP; r += Q) v += base[((int64_t)r * 3 + k) * a.C + j];
+      for (int r = q; r < a.bn.pnrep; r += Q) v += base[((int64_t)r * 3 + k) * a.C + j];
       s_red[q * NI + item] = (float)v;
     }
   }
@@ -450,7 +450,7 @@ DEV void bnb_apply_impl(const TailArgs& a) {
       float v = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) v += s_pp[r][k][q];
-      atomicAdd(a.ppart + ((int64_t)(chunk % NREP) * 3 + k) * a.C + cblk + q, (double)v);
+      atomicAdd(a.ppart + ((int64_t)(chunk % a.pbn.pnrep) * 3 + k) * a.C + cblk + q, (double)v);
     }
   }
 }

@@ -137,6 +137,7 @@ struct BNArgs {
   float* consts;         // optional [G][4][C] (+ z * 4C): scale, shift, mean, invstd of the current batch,
                          // written by the forward tail's block 0 (training) and read by every backward
                          // kernel of this BN -- 4 floats per channel instead of 2 x NREP fp64 replicas
+  int pnrep;             // backward: replicas in use of the [G][NREP][3][C] partial sums (bnb, dgrad epilogue)
   int nrep;              // replicas in use (power of two <= NREP; the producer wrote blockIdx.x % nrep):
                          // small-M layers have few producer blocks, and every consumer block reads all of
                          // them (Model C's 1x6 layers: 32 replicas x 448 channels = 229 KB per block)

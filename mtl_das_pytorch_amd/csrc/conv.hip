@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       const double* pp = o.part + (int64_t)z * NREP * 3 * C;
       double sd = 0.0, sx = 0.0;
 #pragma unroll
-      for (int r = 0; r < NREP; ++r) { sd += pp[(r * 3) * C + c]; sx += pp[(r * 3 + 1) * C + c]; }
+      for (int r = 0; r < o.bn.pnrep; ++r) { sd += pp[(r * 3) * C + c]; sx += pp[(r * 3 + 1) * C + c]; }
       float sc, sh, mu, inv;
       bn_channel_bwd(o.bn, z, c, sc, sh, mu, inv);
       const float gam = o.bn.gamma[o.bn.pstride * z + c];
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   }
   if (want_red) {
     __syncthreads();
-    const int rep = blockIdx.x % (want_bnb ? NREP : a.stats_nrep);
+    const int rep = blockIdx.x % (want_bnb ? a.bbn.pnrep : a.stats_nrep);
     // forward: [G][NREP][2][N] (sum y, sum y^2); fused BN backward: rows 0/1 (2 with a BN2 residual) of
     // the tail's [G][NREP][3][bN]
     const int nrow = want_bnb ? (a.br_bn ? 3 : 2) : 2;

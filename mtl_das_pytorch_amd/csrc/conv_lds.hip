@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
   }
   if (want_red) {
     __syncthreads();
-    const int rep = blockIdx.x % (BNS ? NREP : a.stats_nrep);
+    const int rep = blockIdx.x % (BNS ? a.bbn.pnrep : a.stats_nrep);
     double* dst = BNS ? a.bpart : a.stats;
     const int rows = BNS ? 3 : 2, nrow = BNS && a.br_bn ? 3 : 2, nlim = BNS ? bN : a.N;
     const int64_t gb = BNS ? (a.bpgs < 0 ? (int64_t)z * NREP * 3 * bN : (int64_t)z * a.bpgs)

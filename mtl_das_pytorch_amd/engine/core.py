@@ -285,6 +285,10 @@ class BNLayer:
         import os
         fixed = int(os.environ.get("MDA_BN_NREP", "0"))
         self.nrep = fixed or min(NREP, 1 << max(0, math.ceil(math.log2(max(1, count) / 256))))
+        # backward partial sums (bnb reduce chunks, dgrad epilogues): the same count, and every chunk of
+        # the reduce pass in a replica of its own when there are few (MDA_BN_PNREP overrides)
+        pfixed = int(os.environ.get("MDA_BN_PNREP", "0"))
+        self.pnrep = pfixed or max(self.nrep, min(NREP, 1 << max(0, math.ceil(math.log2(max(1, self.nchunk))))))
         self.arena = arena
         self.dzbuf = None
 
@@ -295,7 +299,7 @@ class BNLayer:
                 "run_mean": P(f.bn_mean, f.bn_offsets[id(m0)]), "run_var": P(f.bn_var, f.bn_offsets[id(m0)]),
                 "nbt": P(f.bn_nbt, f.bn_index[id(m0)]), "pstride": self.pstride, "C": self.C, "count": self.count,
                 "eps": self.eps, "momentum": self.momentum, "training": 1 if training else 0,
-                "consts": P(self.consts), "nrep": self.nrep}
+                "consts": P(self.consts), "nrep": self.nrep, "pnrep": self.pnrep}
 
     def grad_ptrs(self) -> dict:
         f = self.flat
