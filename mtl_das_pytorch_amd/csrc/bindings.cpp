@@ -83,7 +83,7 @@ BNArgs parse_bn(const py::dict& d) {
   b.consts = P<float>(d, "consts");
   b.nrep = (int)I(d, "nrep", NREP);
   b.pnrep = (int)I(d, "pnrep", NREP);
-  if (b.pnrep < 1 || b.pnrep > NREP) throw std::runtime_error("bn: bad pnrep");
+  if (b.pnrep < 1 || b.pnrep > NREP || (b.pnrep & (b.pnrep - 1))) throw std::runtime_error("bn: pnrep must be a power of two <= NREP");
   if (b.nrep < 1 || b.nrep > NREP || (b.nrep & (b.nrep - 1))) throw std::runtime_error("bn: nrep must be a power of two <= NREP");
   return b;
 }

@@ -31,6 +31,18 @@ DEV constexpr bool is_add() { return K == ADD_RELU || K == ADD_RELU2; }
 
 
 
+// sum of replicas q, q + Q, ... < R of a [R][stride] fp64 array (fixed trip count, predicated)
+template <int R, int Q>
+DEV double rep_sum_q(const double* b, int64_t stride, int q) {
+  double v = 0.0;
+#pragma unroll
+  for (int i = 0; i < (R + Q - 1) / Q; ++i) {
+    const int r = q + i * Q;
+    if (r < R) v += b[(int64_t)r * stride];
+  }
+  return v;
+}
+
 // thread -> (channel group, pixel lane) mapping shared by every kernel here
 struct Lanes {
   int CG, PL, cg, pl;
@@ -361,8 +373,16 @@ DEV void bnb_apply_impl(const TailArgs& a) {
     for (int t = threadIdx.x; t < NI * Q; t += BNB_T) {
       const int item = t % NI, q = t / NI;
       const int k = item / CB, j = item - k * CB;
-      double v = 0.0;
-      for (int r = q; r < a.bn.pnrep; r += Q) v += base[((int64_t)r * 3 + k) * a.C + j];
+      const double* b = base + (int64_t)k * a.C + j;
+      double v;
+      switch (a.bn.pnrep) {  // compile-time trip counts: every replica load in flight at once
+        case 1: v = rep_sum_q<1, Q>(b, 3 * a.C, q); break;
+        case 2: v = rep_sum_q<2, Q>(b, 3 * a.C, q); break;
+        case 4: v = rep_sum_q<4, Q>(b, 3 * a.C, q); break;
+        case 8: v = rep_sum_q<8, Q>(b, 3 * a.C, q); break;
+        case 16: v = rep_sum_q<16, Q>(b, 3 * a.C, q); break;
+        default: v = rep_sum_q<NREP, Q>(b, 3 * a.C, q); break;
+      }
       s_red[q * NI + item] = (float)v;
     }
   }

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     for (int c = threadIdx.x; c < C; c += 256) {
       const double* pp = o.part + (int64_t)z * NREP * 3 * C;
       double sd = 0.0, sx = 0.0;
-#pragma unroll
+#pragma unroll 8
       for (int r = 0; r < o.bn.pnrep; ++r) { sd += pp[(r * 3) * C + c]; sx += pp[(r * 3 + 1) * C + c]; }
       float sc, sh, mu, inv;
       bn_channel_bwd(o.bn, z, c, sc, sh, mu, inv);
