@@ -120,7 +120,7 @@ py::tuple conv_workspace(int mode, int cfg, int G, py::dict d) {
   int64_t ws = 0, nt = 0;
   int rc = 0;
   if (cfg >= CONV_DEEP_CFG0) rc = (cfg < CONV_DEEP_CFG0 + CONV_DEEP_NCFG && !(mode != MODE_FWD && a.aol)) ? 0 : -1;
-  else if (cfg >= CONV_LDS_CFG0) rc = conv_lds_workspace(mode, a, G, cfg, ws, nt);
+  else if (cfg >= CONV_LDS_CFG0) rc = a.nr ? -1 : conv_lds_workspace(mode, a, G, cfg, ws, nt);
   return py::make_tuple(rc, ws, nt);
 }
 
@@ -165,8 +165,15 @@ ConvArgs parse_conv(int mode, py::dict d) {
     a.nbn = parse_bn(n["bn"].cast<py::dict>());
     a.nol = 1;
     a.nol_kind = (int)I(n, "kind");
-    if (mode != MODE_FWD || a.src.C1 != 0 || a.nbn.C != a.Cs || (a.nol_kind != ACT_NONE && a.nol_kind != ACT_RELU) ||
-        (a.nbn.training && !a.nbn.stats))
+    if (a.nol_kind == ADD_RELU) {  // residual-on-load
+      py::dict r = n["r"].cast<py::dict>();
+      a.nr = P<const bf16_t>(r, "p"); a.nrgs = I(r, "gs"); a.ldnr = (int)I(r, "ld");
+      if (n.contains("bn2") && !n["bn2"].is_none()) { a.nbn2 = parse_bn(n["bn2"].cast<py::dict>()); a.nr_bn = 1; }
+      if (!a.nr || a.ldnr % 8 || (a.nr_bn && a.nbn2.C != a.Cs))
+        throw std::runtime_error("conv: bad residual-on-load arguments");
+    }
+    if (mode != MODE_FWD || a.src.C1 != 0 || a.nbn.C != a.Cs ||
+        (a.nol_kind != ACT_NONE && a.nol_kind != ACT_RELU && a.nol_kind != ADD_RELU) || (a.nbn.training && !a.nbn.stats))
       throw std::runtime_error("conv: bad normalise-on-load arguments");
   }
   if (d.contains("aol") && !d["aol"].is_none()) {  // dgrad: dy operand = BN-tail backward applied on load

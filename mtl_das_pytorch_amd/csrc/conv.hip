@@ -39,7 +39,7 @@ DEV int encode_kg(int i, int Ktot, int Cs8, int KW, int C0) {
 }
 
 template <int MODE>
-constexpr bool is_fwd() { return MODE == MODE_FWD || MODE == MODE_FWD_NOL; }
+constexpr bool is_fwd() { return MODE == MODE_FWD || MODE == MODE_FWD_NOL || MODE == MODE_FWD_ROL; }
 template <int MODE>
 constexpr bool has_aol() { return MODE == MODE_DGRAD_AOL || MODE == MODE_DGRAD_AOL_BNS; }
 template <int MODE>
@@ -107,13 +107,34 @@ DEV void nol_apply(bf16x8* bfr, uint32_t okm, const float* k, bool relu) {
   }
 }
 
+// Residual-on-load: operand = relu(y * scale + shift + r'), r' = r or r * scale2 + shift2 -- the exact
+// expression (and rounding) of the ADD_RELU tail that materialises the residual block's output.
+// s_nol = [4][Cs]: scale, shift, scale2, shift2.
+template <int FM>
+DEV void rol_apply(bf16x8* bfr, const bf16x8* rq, uint32_t okm, int c, const float* s_nol, int Cs, bool r_bn) {
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    if (!((okm >> f) & 1)) continue;
+    bf16x8 v = bfr[f];
+    const bf16x8 r = rq[f];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = __uint_as_float(((uint32_t)(uint16_t)v[j]) << 16) * s_nol[c + j] + s_nol[Cs + c + j];
+      float rr = __uint_as_float(((uint32_t)(uint16_t)r[j]) << 16);
+      if (r_bn) rr = rr * s_nol[2 * Cs + c + j] + s_nol[3 * Cs + c + j];
+      v[j] = (short)f2bf(fmaxf(x + rr, 0.f));
+    }
+    bfr[f] = v;
+  }
+}
+
 // One wave's fragment loads for k-step `ks`: FM im2col fragments (B operand) + FN weight fragments (A).
 // okm / cch: which im2col fragments hold real (not padding) data and their first channel (for NOL).
 template <int MODE, int FN, int FM>
 DEV void conv_load_stage(const ConvArgs& a, const int* s_tab, int ks, int kgl, int l16, int n_base,
                          const int* pb, const int* py, const int* px, const bool* pv, const bf16_t* base0,
                          const bf16_t* base1, int ld0, int ld1, const bf16_t* wz, bf16x8* afr, bf16x8* bfr,
-                         uint32_t& okm, int& cch, float4 (*gq)[2], uint4* yq, int z) {
+                         uint32_t& okm, int& cch, float4 (*gq)[2], uint4* yq, bf16x8* rq, int z) {
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   const int e = s_tab[ks * 4 + kgl];
   const bool valid = (e >> 29) & 1;
@@ -151,6 +172,10 @@ DEV void conv_load_stage(const ConvArgs& a, const int* s_tab, int ks, int kgl, i
       const bf16_t* q = ok ? sb + ((int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw) * sld + c : sb;
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(q);
       bfr[f] = ok ? v : zero8;
+      if (MODE == MODE_FWD_ROL) {  // the residual r at the same pixel and channels
+        const int64_t pix = ok ? (int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw : 0;
+        rq[f] = *reinterpret_cast<const bf16x8*>(a.nr + a.nrgs * z + pix * a.ldnr + c);
+      }
     }
     okm |= (uint32_t)ok << f;
   }
@@ -206,7 +231,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // LDS, and block (0, 0) of each group performs that BN's running-statistics update and publishes its
   // batch constants for the backward (the work of the forward tail this mode replaces)
   constexpr bool NOL = MODE == MODE_FWD_NOL;
-  if (NOL) bn_prepare(a.nbn, z, s_nol, s_nol + a.Cs, nullptr, nullptr, blockIdx.x == 0 && blockIdx.y == 0);
+  constexpr bool ROL = MODE == MODE_FWD_ROL;
+  // (ROL: the block's tail still runs -- on another stream -- and owns the running-statistics update)
+  if (NOL || ROL) bn_prepare(a.nbn, z, s_nol, s_nol + a.Cs, nullptr, nullptr, NOL && blockIdx.x == 0 && blockIdx.y == 0);
+  if (ROL && a.nr_bn) bn_prepare(a.nbn2, z, s_nol + 2 * a.Cs, s_nol + 3 * a.Cs, nullptr, nullptr, false);
   const bool nol_relu = a.nol_kind == ACT_RELU;
   // MODE_DGRAD_AOL(_BNS): the dy operand is the BN-tail backward applied on load.  Per dy channel: the
   // fused statistics (rows 0/1 of ao.part) and the BN constants give dy = A*dz + B*y + C; block (0, 0)
@@ -306,15 +334,17 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   int ccq[PD];
   constexpr int PG = AOL ? PD : 1;  // AOL raw stage data (eliminated in the other modes)
   float nk[NOL ? PD : 1][16];       // NOL: the stage's BN scale / shift
+  bf16x8 rqs[ROL ? PD : 1][FM];     // ROL: the stage's residual fragments
   float4 gq[PG][FM][2];
   uint4 yq[PG][FM];
 #define LOAD_STAGE(KS, J) do { \
   conv_load_stage<MODE, FN, FM>(a, s_tab, KS, kgl, l16, n_base, pb, py, px, pv, base0, base1, ld0, ld1, wz, af[J], bq[J], \
-                                okq[J], ccq[J], gq[AOL ? (J) : 0], yq[AOL ? (J) : 0], z);                   \
+                                okq[J], ccq[J], gq[AOL ? (J) : 0], yq[AOL ? (J) : 0], rqs[ROL ? (J) : 0], z); \
   if (NOL) nol_fetch(nk[NOL ? (J) : 0], ccq[J], s_nol, a.Cs); } while (0)
   // NOL / AOL: the operand transform runs when the stage is consumed, so the loads stay in flight meanwhile
 #define MMA_STAGE(J)                                                                                      \
   if (NOL) nol_apply<FM>(bq[J], okq[J], nk[NOL ? (J) : 0], nol_relu);                                     \
+  if (ROL) rol_apply<FM>(bq[J], rqs[ROL ? (J) : 0], okq[J], ccq[J], s_nol, a.Cs, a.nr_bn);                  \
   if (AOL) aol_apply<FM>(bq[J], gq[AOL ? (J) : 0], yq[AOL ? (J) : 0], okq[J], ccq[J], s_aol, a.Cs, aol_relu); \
   _Pragma("unroll") for (int i = 0; i < FN; ++i)                                                          \
   _Pragma("unroll") for (int f = 0; f < FM; ++f)                                                          \
@@ -946,7 +976,7 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
     size_t red = (size_t)(KS - 1) * WAN * WAM * TILE;                                                   \
     size_t st2 = (size_t)WAM * WN * WAN * 3;                                                            \
     size_t lds = (size_t)nkg4 * 4 + (red > st2 ? red : st2) * 4 +                                        \
-                 (a.nol ? 2 * a.Cs * 4 : (a.bpart ? 8 * WN * WAN * 4 : 0) + (a.aol ? 5 * a.Cs * 4 : 0));    \
+                 (a.nol ? (a.nr ? 4 : 2) * a.Cs * 4 : (a.bpart ? 8 * WN * WAN * 4 : 0) + (a.aol ? 5 * a.Cs * 4 : 0)); \
     dim3 grid((M + WM * WAM - 1) / (WM * WAM), (a.N + WN * WAN - 1) / (WN * WAN), G);                    \
     hipLaunchKernelGGL((conv_igemm_kernel<MODE, WN, WM, WAN, WAM, KS, PD>), grid, dim3(256), lds, st, a); \
   }
@@ -974,10 +1004,14 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
   if (cfg >= CONV_LDS_CFG0 && cfg < CONV_DEEP_CFG0) {  // LDS-staged kernels (conv_lds.hip)
+    if (a.nr) return -1;  // residual-on-load: register-pipelined kernels only
     const int m = mode == MODE_FWD ? (a.nol ? MODE_FWD_NOL : MODE_FWD) : (a.bpart ? MODE_DGRAD_BNS : MODE_DGRAD);
     return launch_conv_lds(m, a, G, cfg, st);
   }
-  if (mode == MODE_FWD) return a.nol ? launch_conv_cfg<MODE_FWD_NOL>(a, G, cfg, st) : launch_conv_cfg<MODE_FWD>(a, G, cfg, st);
+  if (mode == MODE_FWD) {
+    if (a.nol && a.nr) return launch_conv_cfg<MODE_FWD_ROL>(a, G, cfg, st);
+    return a.nol ? launch_conv_cfg<MODE_FWD_NOL>(a, G, cfg, st) : launch_conv_cfg<MODE_FWD>(a, G, cfg, st);
+  }
   if (a.aol)
     return a.bpart ? launch_conv_cfg<MODE_DGRAD_AOL_BNS>(a, G, cfg, st) : launch_conv_cfg<MODE_DGRAD_AOL>(a, G, cfg, st);
   return a.bpart ? launch_conv_cfg<MODE_DGRAD_BNS>(a, G, cfg, st) : launch_conv_cfg<MODE_DGRAD>(a, G, cfg, st);

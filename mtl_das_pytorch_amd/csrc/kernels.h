@@ -8,7 +8,9 @@ namespace mda {
 
 // 2: dgrad + fused BN-backward statistics; 3: forward with normalise-on-load of its input;
 // 5: dgrad with apply-on-load of its dy operand; 6: both 2 and 5
-enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD_BNS = 2, MODE_FWD_NOL = 3, MODE_DGRAD_AOL = 5, MODE_DGRAD_AOL_BNS = 6 };
+// 7: forward with residual-on-load (normalise-on-load of a residual block's output: relu(BN(y) + r'))
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD_BNS = 2, MODE_FWD_NOL = 3, MODE_DGRAD_AOL = 5, MODE_DGRAD_AOL_BNS = 6,
+       MODE_FWD_ROL = 7 };
 
 // Apply-on-load of a BN-tail backward (ACT_NONE / ACT_RELU): the conv operand dy = A*dz + B*y + C with
 // dz = g * act'(y * scale + shift) is computed from the tail's fp32 upstream gradient g and its pre-BN y
@@ -64,6 +66,12 @@ struct ConvArgs {
   // group updates that BN's running statistics and publishes its constants (BNArgs::consts).
   BNArgs nbn;
   int nol, nol_kind;
+  // ... residual-on-load (nol_kind ADD_RELU, MODE_FWD_ROL): the input is a residual block's output
+  // relu(BN(y) + r'), r' = r (identity shortcut) or BN2(r) (projection, nr_bn = 1), computed on load from
+  // the block's pre-BN y (src) and r -- the block's ADD_RELU tail then runs off the critical stream
+  const bf16_t* nr; int64_t nrgs; int ldnr;
+  BNArgs nbn2;
+  int nr_bn;
   // DGRAD only, optional (aol = 0 off): the dy operand is applied on load (AolArgs)
   AolArgs ao;
   int aol;

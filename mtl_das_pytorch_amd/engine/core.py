@@ -284,7 +284,8 @@ class BNLayer:
         # consumer block (MDA_BN_NREP overrides)
         import os
         fixed = int(os.environ.get("MDA_BN_NREP", "0"))
-        self.nrep = fixed or min(NREP, 1 << max(0, math.ceil(math.log2(max(1, count) / 256))))
+        px = int(os.environ.get("MDA_BN_PX_PER_REP", "256"))
+        self.nrep = fixed or min(NREP, 1 << max(0, math.ceil(math.log2(max(1, count) / px))))
         # backward partial sums (bnb reduce chunks, dgrad epilogues): the same count, and every chunk of
         # the reduce pass in a replica of its own when there are few (MDA_BN_PNREP overrides)
         pfixed = int(os.environ.get("MDA_BN_PNREP", "0"))

@@ -217,8 +217,12 @@ class LoweredProgram:
 
     def _conv_fwd(self, ph: Phase, c: ConvLayer, src: dict, out: Act, bn: BNLayer, training: bool, nol=None):
         mode, cfg, G, d = c.fwd_args(src, out, bn, training)
-        if nol is not None:  # (BNLayer of the input, activation kind)
+        if nol is not None:  # (BNLayer of the input, activation kind[, residual Act, residual BNLayer or None])
             d["nol"] = {"bn": nol[0].args(training), "kind": nol[1]}
+            if len(nol) > 2:  # residual-on-load: relu(BN(y) + r') of a residual block's output
+                r = nol[2]
+                d["nol"].update(r={"p": r.p, "gs": r.gs, "ld": r.ld},
+                                bn2=nol[3].args(training) if nol[3] is not None else None)
         ph.add("conv_fwd", k_conv, mode, cfg, G, d, owner=c)
 
     def _conv_bwd(self, ph: Phase, c: ConvLayer, src: dict, dy: Act, dx: Optional[Act], nol=None):

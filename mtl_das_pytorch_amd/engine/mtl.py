@@ -183,20 +183,37 @@ class MTLProgram(LoweredProgram):
         self._conv_fwd(ph, self.conv1, src_dict(self.xin), self.y0, self.bn1, training)
         self._tail(ph, ACT_RELU, 1, self.y0, self.bn1, self.f0, training)
         ph.cur_stream = 0
+        rol = self.nol and self.rol_enabled()
         for ri, L in enumerate(self.rbs):
             s = src_dict(L["in"])
-            self._conv_fwd(ph, L["ca"], s, L["ya"], L["bna"], training)
+            nol_in = None
+            if rol and ri > 0:
+                # residual-on-load: this block's convs compute their input F_ri = relu(BN(yb) + r') from the
+                # previous block's yb and residual, so the previous block's ADD_RELU tail runs on stream 2,
+                # off the backbone chain; an identity residual r' = F_{ri-1} comes from stream 2 too
+                P_ = self.rbs[ri - 1]
+                s = src_dict(P_["yb"])
+                nol_in = (P_["bnb"], ADD_RELU, P_["ys"] if P_["proj"] else P_["in"], P_["bns"] if P_["proj"] else None)
+                if not P_["proj"] and ri >= 2:
+                    ph.pending_waits.append(f"F{ri - 1}")
+            self._conv_fwd(ph, L["ca"], s, L["ya"], L["bna"], training, nol=nol_in)
             if self.nol:  # conv b normalises ya on load: no BN+ReLU tail, ha never materialised
                 self._conv_fwd(ph, L["cb"], src_dict(L["ya"]), L["yb"], L["bnb"], training, nol=(L["bna"], ACT_RELU))
             else:
                 self._tail(ph, ACT_RELU, 1, L["ya"], L["bna"], L["ha"], training)
                 self._conv_fwd(ph, L["cb"], src_dict(L["ha"]), L["yb"], L["bnb"], training)
             if L["proj"]:
-                self._conv_fwd(ph, L["cs"], s, L["ys"], L["bns"], training)
+                self._conv_fwd(ph, L["cs"], s, L["ys"], L["bns"], training, nol=nol_in)
+            if rol:
+                ph.mark(f"yb{ri + 1}")
+                ph.cur_stream = 2
+                ph.pending_waits.append(f"yb{ri + 1}")
+            if L["proj"]:
                 self._tail(ph, ADD_RELU, 1, L["yb"], L["bnb"], L["out"], training, r=L["ys"], bn2=L["bns"])
             else:
                 self._tail(ph, ADD_RELU, 1, L["yb"], L["bnb"], L["out"], training, r=L["in"])
             ph.mark(f"F{ri + 1}")
+            ph.cur_stream = 0
         # task branches (both tasks per launch) on side stream 1, overlapping the backbone
         ph.cur_stream = 1
         for lvl, L in enumerate(self.levels):
@@ -228,6 +245,18 @@ class MTLProgram(LoweredProgram):
             hd["lab_off"] = 0
         ph.add("mtl_head", k_head, hd)
         return ph
+
+    @staticmethod
+    def rol_enabled() -> bool:
+        """Residual-on-load in the forward (MDA_ROL=1, opt-in): the first convs of residual block k + 1
+        read block k's pre-BN yb and residual and apply relu(BN(yb) + r') on load (csrc/conv.hip
+        MODE_FWD_ROL, bitwise the tail's output: tests/test_engine_gpu.py::test_residual_on_load_bitwise),
+        so the ADD_RELU tails that materialise F_k for the task branches, the next tail's residual and the
+        backward run on stream 2.  Measured slower on MI355X (docs/PERF.md): forward 304 -> 600 us with the
+        side stream, 388 -> 437 us on one stream -- the ROL convs run 20-25 us instead of 12-15 (two BN
+        constant sets read from LDS in every K step's chain, a second operand load)."""
+        import os
+        return os.environ.get("MDA_ROL", "0") == "1"
 
     @staticmethod
     def msbns_enabled() -> bool:

@@ -35,8 +35,11 @@ _CACHE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_cf
 def conv_signature(mode: int, G: int, d: dict) -> str:
     keys = ("B", "Hs", "Ws", "Ho", "Wo", "N", "Cs", "KH", "KW", "sh", "sw", "ph", "pw")
     src = d["src"]
-    return f"conv{mode}|G{G}|" + ",".join(str(d[k]) for k in keys) + f"|seg{int(src.get('C1', 0) > 0)}" + \
-           f"|st{int(bool(d.get('stats')))}"
+    sig = f"conv{mode}|G{G}|" + ",".join(str(d[k]) for k in keys) + f"|seg{int(src.get('C1', 0) > 0)}" + \
+          f"|st{int(bool(d.get('stats')))}"
+    if (d.get("nol") or {}).get("r"):  # residual-on-load runs on the register-pipelined kernels only
+        sig += "|rol"
+    return sig
 
 
 def load_cache(path: str = _CACHE_PATH) -> Dict[str, int]:

@@ -145,7 +145,10 @@ def prepare_conv2d(x, w, bias=None, stride=1, padding=0, stats=None, x2=None, cf
          "Npad": wf.shape[0], "Cs": Cs, "KH": KH, "KW": KW, "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": wf.shape[1]}
     if nol is not None:  # (bn dict of x's BN, kind): x is a pre-BN y, the operand is act(BN(x)) on load
         d["nol"] = {"bn": nol[0], "kind": nol[1]}
-    return ConvCall(0, _fwd_cfg(Co, B * Ho * Wo) if cfg is None else cfg, d, y, (x, x2, wf, bias, stats))
+        if len(nol) > 2:  # residual-on-load (kind 4): (bn, 4, r [B,H,W,C] bf16, bn2 dict or None)
+            r = nol[2]
+            d["nol"].update(r={"p": ptr(r), "gs": 0, "ld": r.shape[-1]}, bn2=nol[3])
+    return ConvCall(0, _fwd_cfg(Co, B * Ho * Wo) if cfg is None else cfg, d, y, (x, x2, wf, bias, stats, nol))
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, stride=1, padding=0,

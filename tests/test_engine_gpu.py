@@ -278,3 +278,38 @@ def test_multi_source_bn_stats_match_reduce(monkeypatch, B):
     assert srel[7] < 1e-9 and srel[6] < 1e-5, srel  # RB8 (task sources only), RB7 (first multi-producer)
     assert max(srel) < 1e-2, srel
     assert rel(g1, g0) < 1e-2
+
+
+def test_residual_on_load_bitwise(monkeypatch):
+    """MDA_ROL=1 (opt-in: the next block's convs compute relu(BN(yb) + r') on load, the ADD_RELU tails run on a
+    side stream) gives bitwise the same training step as materialising every residual block output first: same
+    forward logits and metrics, same gradients, same BN running statistics (graph replay, two steps)."""
+    from mtl_das_pytorch_amd.data.synthetic import generate
+    from mtl_das_pytorch_amd.engine.mtl import MTLProgram
+    from mtl_das_pytorch_amd.engine.step import StepRunner
+    from mtl_das_pytorch_amd.models import MTL_Net
+    X, d, e = generate(64, seed=21, device="cuda")
+    labels = torch.stack([d, e], 1)
+    out = {}
+    for rol in ("0", "1"):
+        monkeypatch.setenv("MDA_ROL", rol)
+        torch.manual_seed(0)
+        prog = MTLProgram(MTL_Net(), 32, "cuda")
+        prog.set_optimizer(weight_decay=1e-5)  # heuristic conv configs: the same tiles with and without ROL
+        n_rol = sum(1 for l in prog.fwd_train.launches if l.name == "conv_fwd" and (l.args[3].get("nol") or {}).get("r"))
+        run = StepRunner(prog, X, labels)
+        run.set_lr(1e-3)
+        for i in range(2):
+            run.train_step(torch.arange(32 * i, 32 * (i + 1), device="cuda"))
+        torch.cuda.synchronize()
+        f = prog.flat
+        out[rol] = (n_rol, prog.logp.clone(), prog.metrics.clone(), f.grads.clone(), f.params.clone(),
+                    f.bn_mean.clone(), f.bn_var.clone())
+    assert out["0"][0] == 0 and out["1"][0] == 10  # RB2..RB8 conv a + the 3 projection shortcuts
+    names = ("logp", "metrics", "grads", "params", "bn_mean", "bn_var")
+    diff = {n: (a - b).abs().max().item() for n, a, b in zip(names, out["0"][1:], out["1"][1:])
+            if n != "metrics" and not torch.equal(a, b)}
+    assert not diff, diff
+    # the head's loss sums are fp32 atomics (order-dependent in the last bit); counts are exact
+    m0, m1 = out["0"][2], out["1"][2]
+    assert torch.equal(m0[:, 1:3], m1[:, 1:3]) and torch.allclose(m0, m1, rtol=1e-5, atol=0)
