@@ -514,12 +514,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
+template <int HI = 4>
 DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
-  // Block of rows r..r+7 (two 4-row transposed reads), 16 columns col0..col0+15.
+  // Rows r..r+3 and r+HI..r+HI+3 (two 4-row transposed reads), 16 columns col0..col0+15.
   // Lane 4q+p of each 16-lane group supplies &row[q][col0 + 4p]; lane i receives column col0+i.
   const int i = lane & 15, q = i >> 2, p = i & 3;
   const bf16_t* a0 = lds_row0 + q * ld_elems + col0 + 4 * p;
-  const bf16_t* a1 = a0 + 4 * ld_elems;
+  const bf16_t* a1 = a0 + HI * ld_elems;
   v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
   v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a1));
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -532,8 +533,11 @@ DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
 // by the same conv's dgrad), so the tail never materialises dy.
 template <int TN, int TK, int MCH, bool AOL>
 DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const int z) {
-  constexpr int PAD = 8;  // rows stay 16-byte aligned (ds_write_b128 staging, 8-byte tr-read addresses)
-  constexpr int LDY = TN + PAD, LDX = TK + PAD;
+  // Row pitch 16 x odd elements (TN + 16 for even multiples of 16): with the row permutation below the 32
+  // lanes of one ds_read_b64_tr_b16 read rows 0-7 of a 16-row block, whose 8-bank windows then tile the 64
+  // banks exactly (the previous pitch TN + 8 with rows 0-3 and 8-11 per instruction left 2-way conflicts:
+  // SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.38)
+  constexpr int LDY = (TN / 16) % 2 ? TN : TN + 16, LDX = (TK / 16) % 2 ? TK : TK + 16;
   __shared__ __attribute__((aligned(16))) bf16_t s_dy[MCH * LDY];
   __shared__ __attribute__((aligned(16))) bf16_t s_x[MCH * LDX];
   __shared__ int s_tab[TK / 8];
@@ -686,14 +690,16 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
     if (mc + MCH < mend) load_chunk(mc + MCH);  // in flight during this chunk's MFMAs
 #pragma unroll
     for (int kk = 0; kk < MCH / 32; ++kk) {
-      const int prow = kk * 32 + 8 * (lane >> 4);
+      // the MFMA's k index (pixel) of lane group g = lane >> 4 is any fixed permutation of the chunk's
+      // pixels, the same for both operands: group g takes rows 16(g/2) + 4(g%2) + {0..3, 8..11}
+      const int prow = kk * 32 + 16 * (lane >> 5) + 4 * ((lane >> 4) & 1);
 #pragma unroll
       for (int j = 0; j < FPW; ++j) {
         const int fr = wid + 4 * j;
         if (fr < NFR) {
           const int fi = fr / FK, fk = fr - fi * FK;
-          bf16x8 av = tr_read8(&s_dy[prow * LDY], LDY, fi * 16, lane);
-          bf16x8 bv = tr_read8(&s_x[prow * LDX], LDX, fk * 16, lane);
+          bf16x8 av = tr_read8<8>(&s_dy[prow * LDY], LDY, fi * 16, lane);
+          bf16x8 bv = tr_read8<8>(&s_x[prow * LDX], LDX, fk * 16, lane);
           acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[j], 0, 0, 0);
         }
       }
