@@ -159,3 +159,8 @@ def main():
 
 if __name__ == "__main__":
     main()
+    # the result line is out: leave without the interpreter's teardown, whose destruction order of HIP
+    # graphs / streams / the runtime crashed one tool run at exit (SIGSEGV after its last line)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)
