@@ -368,6 +368,7 @@ void adam_pack(int64_t stream, py::dict d) {
   a.wd = (float)F(d, "wd", 0.0); a.grad_scale = (float)F(d, "grad_scale", 1.0);
   a.update = (int)I(d, "update", 1);
   a.ticket = P<unsigned>(d, "ticket");
+  a.fused = (int)I(d, "fused", 0);
   check(launch_adam_pack(a, P<const OptSeg>(d, "segs"), (int)I(d, "nsegs"), I(d, "nblocks"), S(stream)), "adam_pack");
 }
 

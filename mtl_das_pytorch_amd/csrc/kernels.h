@@ -242,7 +242,9 @@ struct AdamArgs {
   int update;  // 0: pack only
   // fused update (non-null): ONE launch over an OptSeg table of kind 0 (plain Adam ranges) and kind 2
   // (conv weight tiles: Adam + both bf16 images); the last block to finish advances the step counter
-  unsigned* ticket;
+  unsigned* ticket;  // fused kernel: the last block advances the step counter (null: leave it, see fused)
+  int fused;         // run the fused Adam + pack kernel over `segs` even without a ticket (a partial
+                     // update inside the backward; the step's last optimizer launch advances the counter)
 };
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);

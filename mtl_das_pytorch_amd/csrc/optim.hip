@@ -207,6 +207,7 @@ __global__ __launch_bounds__(256) void adam_pack_fused_kernel(AdamArgs a, const 
     }
   }
   // step counter: the last block (all others have read step[0]) advances it and re-arms the ticket
+  if (!a.ticket) return;
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned t = atomicAdd(a.ticket, 1u);
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(256) void adam_pack_fused_kernel(AdamArgs a, const 
 __global__ void step_inc_kernel(float* step) { step[0] += 1.f; }
 
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st) {
-  if (a.update && a.ticket) {
+  if (a.update && (a.ticket || a.fused)) {
     if (nblocks <= 0) return -2;
     hipLaunchKernelGGL(adam_pack_fused_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, a, d_segs, ns);
     return (int)hipGetLastError();

@@ -470,6 +470,70 @@ class LoweredProgram:
         self.buckets = buckets
         return buckets
 
+    # ---- early optimizer (single GPU) -------------------------------------------------------------
+    def early_opt_enabled(self) -> bool:
+        """Adam + re-pack of the side streams' parameters inside the backward (MDA_EARLY_OPT=1, opt-in).
+        Measured on MI355X: Model C's optimizer tail 174 -> 14 us, but the backward 2,634 -> 2,826 us (the
+        side-stream updates contend with the main stream's stem backward), full step 4,297 vs 4,279 us;
+        Model A 32.7k vs 32.5k.  Only without data parallelism: the gradients must be complete before any update, so a program whose
+        optimizer averages over ranks (grad_scale != 1), is cut into gradient buckets or runs SyncBN keeps
+        the single optimizer launch after the backward."""
+        import os
+        return (os.environ.get("MDA_EARLY_OPT", "0") == "1" and self._opt_hparams.get("grad_scale", 1.0) == 1.0
+                and self.flat.bn_world == 1 and not any(l.name == "cut" for l in self.bwd.launches))
+
+    def _grad_writer_streams(self, bwd_launches) -> Dict[int, set]:
+        """Flat offset of each directly written gradient (BN affine parameters, fc) -> the streams that write
+        it (-1: written in the forward phase, e.g. the classifier head's fc gradient)."""
+        gbase, n = P(self.flat.grads), self.flat.numel
+        out: Dict[int, set] = {}
+        for l in bwd_launches:
+            if l.fn is not None:
+                for off in _grad_offsets(l, gbase, n):
+                    out.setdefault(off, set()).add(l.stream)
+        for l in self.fwd_train.launches:
+            if l.fn is not None:
+                for off in _grad_offsets(l, gbase, n):
+                    out.setdefault(off, set()).add(-1)
+        return out
+
+    def _early_segments(self, st: int, convs, writers) -> tuple:
+        """Fused Adam + pack segments of the parameters stream ``st`` alone produces: the weights of the convs
+        whose weight gradients it batches (finalized just before on the same stream), and every parameter
+        whose gradient only ``st`` writes (the BN layers of those convs).  Conv biases stay late."""
+        f = self.flat
+        segs = [sg for c in convs for sg in c.fused_segments()]
+        ranges = [(sg["off"], sg["n"]) for sg in segs]
+        conv_params = {id(m.weight) for c in self.convs for m in c.mods}
+        conv_params |= {id(m.bias) for c in self.convs for m in c.mods if m.bias is not None}
+        for p in self.model.parameters():
+            if id(p) in conv_params:
+                continue
+            o = f.off(p)
+            if writers.get(o) == {st}:
+                segs.append({"kind": 0, "off": o, "n": p.numel()})
+                ranges.append((o, p.numel()))
+        segs.sort(key=lambda sg: sg["off"])
+        return segs, ranges
+
+    def _set_late_optimizer(self, early_ranges):
+        """The optimizer phase after the backward: fused Adam + pack over every parameter not updated early
+        (the main stream's convs, conv biases, the head, BN layers written on the main stream), advancing
+        the step counter at its end."""
+        f = self.flat
+        covered = set(early_ranges)
+        late = [sg for c in self.convs for sg in c.fused_segments() if (sg["off"], sg["n"]) not in covered]
+        conv_w = [(sg["off"], sg["n"]) for c in self.convs for sg in c.fused_segments()]
+        late += plain_ranges(f.numel, conv_w + [r for r in early_ranges if r not in set(conv_w)])
+        late.sort(key=lambda sg: sg["off"])
+        self.late_segs = late
+        self.optseg_late, ns, nb = build_optseg_table(late, self.device)
+        self.adam_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._opt_upd = dict(self._opt_base, segs=P(self.optseg_late), nsegs=ns, nblocks=nb, ticket=P(self.adam_ticket))
+        upd = Phase("adam")
+        upd.add("adam_pack", k_adam, dict(self._opt_upd, update=1, **self._opt_hparams))
+        self.opt["adam"] = upd
+
     def merge_wgrad_cfgs(self, max_batches: Optional[int] = None) -> int:
         """Cap the number of distinct weight-gradient tile configs per stream (= batched launches, which run
         back to back at the end of the stream's backward): repeatedly move the cheapest config group whose
@@ -549,8 +613,16 @@ class LoweredProgram:
         staged = self._stage_wgrads(wg, ls, anchor_of)
         # MDA_FIN_SPLIT=1 (opt-in; measured neutral: A 31.53-31.58k vs 31.57-31.62k, C 6.89k vs 6.86k): one
         # finalize per stream, right after that stream's batches
-        split_fin = (os.environ.get("MDA_FIN_SPLIT", "0") == "1" and staged is None and not self._fan_out_wgrads()
-                     and any(l.stream == 0 for l in wg) and all(l.owner is not None for l in wg))
+        split_ok = (staged is None and not self._fan_out_wgrads() and any(l.stream == 0 for l in wg)
+                    and all(l.owner is not None for l in wg))
+        # early optimizer: each side stream finalizes its convs and runs Adam + the bf16 re-pack on every
+        # parameter only it produces gradients for, overlapping the main stream's remaining backward
+        early = split_ok and self.early_opt_enabled() and not any(l.args[2].get("aol") for l in wg)
+        split_fin = split_ok and (early or os.environ.get("MDA_FIN_SPLIT", "0") == "1")
+        writers = self._grad_writer_streams(ls) if early else None
+        self.early_adam = []
+        self.early_segs = {}
+        early_ranges = []
         self.wgfin_tables = []
         self.wgrad_tables = []
         inserts, tags = [], []
@@ -581,6 +653,17 @@ class LoweredProgram:
                     t, nd, nb = build_wgfin_table([l.owner.finalize_desc() for l in wg if l.stream == st], self.device)
                     self.wgfin_tables.append(t)
                     batched.append(Launch("wgrad_finalize", k_wgfin, t, nd, nb, stream=st))
+                    if early:
+                        segs, ranges = self._early_segments(st, [l.owner for l in wg if l.stream == st], writers)
+                        self.early_segs[st] = segs
+                        if segs:
+                            table, ns, nb = build_optseg_table(segs, self.device)
+                            self.wgfin_tables.append(table)
+                            d = dict(self._opt_base, segs=P(table), nsegs=ns, nblocks=nb, fused=1, ticket=0,
+                                     update=1, **self._opt_hparams)
+                            batched.append(Launch("adam_early", k_adam, d, stream=st))
+                            self.early_adam.append(batched[-1])
+                            early_ranges += ranges
                 batched[-1].record = f"wgrads_s{st}"
                 tags.append(batched[-1].record)
             inserts.append((pos, batched))
@@ -596,6 +679,8 @@ class LoweredProgram:
             self.wgfin_tables.append(t)
             fin_l.args = (t, nd, nb)
             fin_l.waits = ()
+        if self.early_adam:
+            self._set_late_optimizer(early_ranges)
         self.bwd.launches = keep + ls[fin:]
         self.wgrads_batched = True
 
@@ -744,17 +829,23 @@ class LoweredProgram:
             self.optseg_fused, nsf, nbf = build_optseg_table(fsegs, self.device)
             self.adam_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
             self._opt_upd = dict(base, segs=P(self.optseg_fused), nsegs=nsf, nblocks=nbf, ticket=P(self.adam_ticket))
+        self._opt_hparams = dict(b1=0.9, b2=0.999, eps=1e-8, wd=0.0, grad_scale=grad_scale)
         upd = Phase("adam")
-        upd.add("adam_pack", k_adam, dict(self._opt_upd, update=1, b1=0.9, b2=0.999, eps=1e-8, wd=0.0,
-                                          grad_scale=grad_scale))
+        upd.add("adam_pack", k_adam, dict(self._opt_upd, update=1, **self._opt_hparams))
         pack = Phase("pack")
         pack.add("pack", k_adam, dict(base, update=0))
         return {"adam": upd, "pack": pack}
 
     def set_optimizer(self, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, grad_scale: float = 1.0):
-        d = dict(self._opt_upd, update=1, b1=betas[0], b2=betas[1], eps=eps, wd=weight_decay, grad_scale=grad_scale)
+        early = getattr(self, "early_adam", [])
+        if early and grad_scale != 1.0:
+            raise RuntimeError("the early optimizer (single GPU) is already placed in the backward: set the data-"
+                               "parallel grad_scale before autotune_program / batch_wgrads")
+        self._opt_hparams = dict(b1=betas[0], b2=betas[1], eps=eps, wd=weight_decay, grad_scale=grad_scale)
+        for l in early:
+            l.args[0].update(self._opt_hparams)
         upd = Phase("adam")
-        upd.add("adam_pack", k_adam, d)
+        upd.add("adam_pack", k_adam, dict(self._opt_upd, update=1, **self._opt_hparams))
         self.opt["adam"] = upd
 
     # -------------------------------------------------------------------------------------------

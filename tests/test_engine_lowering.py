@@ -90,6 +90,7 @@ def test_wgrad_batching_structure():
     for split in ("1", "0"):
         import os
         os.environ["MDA_FIN_SPLIT"] = split
+        os.environ["MDA_EARLY_OPT"] = "0"
         try:
             p = MTLProgram(MTL_Net(), 32, "cpu")
             n_wg = sum(1 for l in p.bwd.launches if l.name == "conv_wgrad")
@@ -97,6 +98,7 @@ def test_wgrad_batching_structure():
             p.batch_wgrads()
         finally:
             del os.environ["MDA_FIN_SPLIT"]
+            del os.environ["MDA_EARLY_OPT"]
         b = [l for l in p.bwd.launches if l.name == "wgrad_batched"]
         assert sum(l.args[2] for l in b) == n_wg
         fin = p.bwd.launches[-1]
@@ -272,3 +274,49 @@ def test_inception_aux_logits_shape_error():
         m(torch.randn(2, 1, 100, 250))
     with pytest.raises(ValueError, match="4 x 13"):
         InceptionProgram(m, 2, "cpu")
+
+
+@pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
+def test_early_optimizer_partition(model):
+    """Early optimizer (single GPU, MDA_EARLY_OPT=1): every side stream finalizes its convs and then runs Adam + re-pack on the
+    parameters only it produces gradients for; the optimizer phase after the backward covers the rest.
+    Together the segments cover the flat buffer exactly once, conv weights as pack tiles, and an early
+    parameter's gradient is written by no other stream and not in the forward."""
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.engine.lowering import _grad_offsets
+    from mtl_das_pytorch_amd.engine.core import P
+    from mtl_das_pytorch_amd.models import build_model
+    import os
+    torch.manual_seed(0)
+    m = build_model(model)
+    p = InceptionProgram(m, 8, "cpu") if model == "multi_classifier" else MTLProgram(m, 8, "cpu")
+    os.environ["MDA_EARLY_OPT"] = "1"
+    try:
+        p.batch_wgrads()
+    finally:
+        del os.environ["MDA_EARLY_OPT"]
+    ls = p.bwd.launches
+    early = [l for l in ls if l.name == "adam_early"]
+    assert early and all(l.stream != 0 for l in early)
+    for l in early:  # right after its stream's finalize, carrying the stream's end event
+        i = ls.index(l)
+        assert ls[i - 1].name == "wgrad_finalize" and ls[i - 1].stream == l.stream
+        assert l.record == f"wgrads_s{l.stream}" and l.args[0]["fused"] == 1 and l.args[0]["ticket"] == 0
+    n = p.flat.numel
+    cover = torch.zeros(n, dtype=torch.int32)
+    segs = [sg for st in p.early_segs.values() for sg in st] + p.late_segs
+    for sg in segs:
+        cover[sg["off"]:sg["off"] + sg["n"]] += 1
+    assert torch.all(cover == 1)
+    conv_w = {p.flat.off(mm.weight) for c in p.convs for mm in c.mods}
+    assert {sg["off"] for sg in segs if sg["kind"] == 2} == conv_w
+    gbase = P(p.flat.grads)
+    for st, ss in p.early_segs.items():
+        for sg in ss:
+            if sg["kind"] != 0:
+                continue
+            for l in ls + p.fwd_train.launches:
+                if l.fn is not None and sg["off"] in _grad_offsets(l, gbase, n):
+                    assert l in ls and l.stream == st, (l.name, l.stream, st)
+    late = p.opt["adam"].launches
+    assert len(late) == 1 and late[0].args[0]["ticket"] != 0  # the late launch advances the step counter
