@@ -29,6 +29,9 @@ METRIC = "samples/sec (whole node) MTL train bs=32 at 1/2/4/8 MI355X; event-cls 
 # MI355X measured 4,037 samples/s (profiles/r1_eager_reference_probe.log) and is reported alongside.
 BASELINE_VALUE = 176.1
 EAGER_MI355X_PER_GPU = 4037.0
+# reference-style eager fp32 PyTorch on one MI355X per model (docs/PERF.md headline table,
+# profiles/r1_eager_reference_probe.log, profiles/r1_modelB_C_engine_vs_eager.log)
+EAGER_BY_MODEL = {"MTL": EAGER_MI355X_PER_GPU, "single_event": 5292.0, "multi_classifier": 1876.0}
 MODEL_NAMES = {"MTL": "modelA_MTL", "single_distance": "modelB_singleTask_distance",
                "single_event": "modelB_singleTask_event", "multi_classifier": "modelC_multiClassifier"}
 
@@ -145,12 +148,13 @@ def main():
         "heldout_acc_after_timed_steps": _accs(mh, joint) if mh is not None else None,
         "heldout_samples": (args.heldout // args.batch) * args.batch * world,
         "train_steps_before_heldout": args.warmup + args.steps,
-        "vs_eager_pytorch_mi355x": round(value / (EAGER_MI355X_PER_GPU * world), 3) if args.model == "MTL" else None,
+        "vs_eager_pytorch_mi355x": (round(value / (EAGER_BY_MODEL[args.model] * world), 3)
+                                    if args.model in EAGER_BY_MODEL else None),
         "hip_graph": not args.no_graph,
         "grad_buckets_mb": [round((hi - lo) * 4 / 2 ** 20, 2) for lo, hi in buckets],
         "baseline_note": "vs_baseline divides by BASELINE.md's 176.1 samples/s (reference on CPU, the only "
                          "throughput number it has); vs_eager_pytorch_mi355x divides by the reference-style "
-                         "eager fp32 PyTorch step measured on MI355X (4037 samples/s/GPU)",
+                         "eager fp32 PyTorch step of the same model measured on MI355X (A: 4037 samples/s/GPU)",
     }
     if ctx.is_main:
         print(json.dumps(out), flush=True)
@@ -160,7 +164,9 @@ def main():
 if __name__ == "__main__":
     main()
     # the result line is out: leave without the interpreter's teardown, whose destruction order of HIP
-    # graphs / streams / the runtime crashed one tool run at exit (SIGSEGV after its last line)
+    # graphs / streams / the runtime crashed one tool run at exit (SIGSEGV after its last line).
+    # Under a profiler (rocprofv3 flushes its buffers from exit handlers) the normal exit is kept.
     sys.stdout.flush()
     sys.stderr.flush()
-    os._exit(0)
+    if os.environ.get("MDA_CLEAN_EXIT") != "1" and not any(k.startswith("ROCPROF") for k in os.environ):
+        os._exit(0)

@@ -382,6 +382,7 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.doc() = "gfx950 HIP kernels of mtl_das_pytorch_amd";
   m.attr("NREP") = NREP;
   m.attr("SIZEOF_WGFIN") = (int)sizeof(WgFinDesc);
+  m.attr("FIN_EPT") = FIN_EPT;
   m.attr("SIZEOF_OPTSEG") = (int)sizeof(OptSeg);
   m.def("conv", &conv);
   m.def("conv_workspace", &conv_workspace);

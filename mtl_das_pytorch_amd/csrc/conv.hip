@@ -909,55 +909,84 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const Wgr
 
 // Sums the split-M partial slabs of many convolutions into the flat fp32 gradient buffer (deterministic,
 // one launch per backward), reference weight layout [Cout][Cin][KH][KW].
+// Threads walk the OUTPUT in its own order: a block owns FIN_EPT x (256 / lanes) consecutive NCHW weights,
+// so every store is a full-line contiguous write.  (Walking the slab's k-fastest order instead scattered
+// the stores with a KH*KW*4-byte stride: each gradient line was then assembled from partial writes of
+// up to KH*KW blocks on different XCDs, and the launch ran at ~1.5 TB/s.)  The slab reads are
+// tap-strided runs of consecutive input channels; a block covers ~FIN_EPT*256/taps channels of every
+// tap, so the lines it reads are mostly its own.
 // Each weight is reduced by D.lanes threads (a power of two <= 16, chosen per conv from its split count):
-// lane q sums splits q, q + lanes, ... and the lane partials are added in lane order through LDS --
-// deterministic, and a conv with many splits no longer sets the launch's length with one long serial
-// chain of loads.  The lane is the slow thread index of a block (block = 256/lanes weights x lanes), so
-// neighbouring threads still read neighbouring slab columns.  Descriptors own whole blocks, so `lanes`
-// is uniform within a block.
+// lane q sums splits q, q + lanes, ... (two chains) and the lane partials are added in lane order through
+// LDS -- deterministic.  Descriptors own whole blocks, so `lanes` is uniform within a block.
 __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale) {
-  __shared__ float s_part[256];
+  __shared__ float s_part[FIN_EPT][256];
   int lo = 0, hi = nd - 1;  // last descriptor with block0 <= blockIdx.x
   while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (descs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
   const WgFinDesc& D = descs[lo];
   const int L = D.lanes, EPB = 256 / L;
-  // threads walk the slab in its own (k-fastest) order so the split reads are coalesced; the single
-  // write per weight is scattered into the NCHW layout.
-  const int Kt = D.KH * D.KW * D.Cs;
+  const int taps = D.KH * D.KW, row = D.Ci * taps, per = D.Co * row;
   const int q = threadIdx.x / EPB, ie = threadIdx.x - q * EPB;
-  const int64_t e = ((int64_t)blockIdx.x - D.block0) * EPB + ie;
-  const int64_t per = (int64_t)D.Co * Kt;
-  const int g = (int)(e / per);
-  int64_t r = e - g * per;
-  const int co = (int)(r / Kt);
-  const int k = (int)(r - (int64_t)co * Kt);
-  const int ci = k % D.Cs, tap = k / D.Cs;
-  const bool ok = e < D.elems && ci < D.Ci;
-  const int kh = tap / D.KW, kw = tap - kh * D.KW;
-  const float* s = D.slab + (((int64_t)g * D.splits) * D.Npad + co) * D.Kpad + k;
+  const int base = (int)((int64_t)blockIdx.x - D.block0) * (EPB * FIN_EPT) + ie;
+  const int elems = (int)D.elems, splits = D.splits;
   const int64_t sstride = (int64_t)D.Npad * D.Kpad;
-  // 8 independent partial sums keep 8 loads in flight per thread
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (ok) {
-    int sp = q;
-    for (; sp + 7 * L < D.splits; sp += 8 * L) {
+  const float* src[FIN_EPT];
+  float* dst[FIN_EPT];
+  bool ok[FIN_EPT];
+  // (g, co, ci, tap) of the first weight by division, then advanced by EPB in mixed radix (one division
+  // at most per step: the index math would otherwise rival the memory time of this streaming kernel)
+  int g = base / per, r = base - g * per;
+  int co = r / row, ci = (r - co * row) / taps, tap = r - co * row - ci * taps;
+  const int s_ci = EPB / taps, s_tap = EPB - s_ci * taps;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += s[(int64_t)(sp + j * L) * sstride];
+  for (int j = 0; j < FIN_EPT; ++j) {
+    const int e = base + j * EPB;
+    ok[j] = e < elems;
+    src[j] = D.slab + ((int64_t)g * splits * D.Npad + co) * D.Kpad + tap * D.Cs + ci;
+    dst[j] = D.grad + g * D.ggs + ((co * D.Ci + ci) * taps + tap);  // NCHW offset within group g
+    tap += s_tap;
+    ci += s_ci;
+    if (tap >= taps) { tap -= taps; ++ci; }
+    if (ci >= D.Ci) {
+      if (s_ci < D.Ci) { ci -= D.Ci; ++co; }
+      else { const int c = ci / D.Ci; co += c; ci -= c * D.Ci; }
     }
-    for (; sp < D.splits; sp += L) acc[0] += s[(int64_t)sp * sstride];
+    while (co >= D.Co) { co -= D.Co; ++g; }
   }
-  const float v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  float* dst = D.grad + g * D.ggs + (((int64_t)co * D.Ci + ci) * D.KH + kh) * D.KW + kw;
+  float a0[FIN_EPT], a1[FIN_EPT];
+#pragma unroll
+  for (int j = 0; j < FIN_EPT; ++j) { a0[j] = 0.f; a1[j] = 0.f; }
+  int sp = q;
+  for (; sp + L < splits; sp += 2 * L) {
+#pragma unroll
+    for (int j = 0; j < FIN_EPT; ++j) {
+      if (ok[j]) {
+        a0[j] += src[j][(int64_t)sp * sstride];
+        a1[j] += src[j][(int64_t)(sp + L) * sstride];
+      }
+    }
+  }
+  if (sp < splits) {
+#pragma unroll
+    for (int j = 0; j < FIN_EPT; ++j)
+      if (ok[j]) a0[j] += src[j][(int64_t)sp * sstride];
+  }
   if (L == 1) {
-    if (ok) *dst = v * scale;
+#pragma unroll
+    for (int j = 0; j < FIN_EPT; ++j)
+      if (ok[j]) *dst[j] = (a0[j] + a1[j]) * scale;
     return;
   }
-  s_part[threadIdx.x] = v;
+#pragma unroll
+  for (int j = 0; j < FIN_EPT; ++j) s_part[j][threadIdx.x] = a0[j] + a1[j];
   __syncthreads();
-  if (ok && q == 0) {
-    float sum = 0.f;
-    for (int j = 0; j < L; ++j) sum += s_part[j * EPB + ie];
-    *dst = sum * scale;
+  if (q == 0) {
+#pragma unroll
+    for (int j = 0; j < FIN_EPT; ++j) {
+      if (!ok[j]) continue;
+      float sum = 0.f;
+      for (int l = 0; l < L; ++l) sum += s_part[j][l * EPB + ie];
+      *dst[j] = sum * scale;
+    }
   }
 }
 

@@ -144,6 +144,8 @@ struct WgFinDesc {
   int64_t elems;      // G * Co * Ci * KH * KW
   int64_t block0;     // first block index of this descriptor
 };
+// weights per thread (per lane) of wgrad_finalize: a block owns FIN_EPT * 256 / lanes consecutive weights
+constexpr int FIN_EPT = 4;
 
 enum TailKind { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, SIGMUL = 3, ADD_RELU = 4, POOL_RELU = 5 };
 

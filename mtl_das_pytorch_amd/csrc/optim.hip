@@ -123,24 +123,19 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, 
   const int64_t total8 = S.n / 8;  // S.n = rows * K (multiple of 8)
   if (e8 >= total8) return;
   const int64_t e = e8 * 8;
-  const int row = (int)(e / K);
-  const int k0 = (int)(e - (int64_t)row * K);
-  const float* W = P + S.off;
+  const int row = (int)e / K;  // S.n < 2^31
+  const int k0 = (int)e - row * K;
   const int taps = S.KH * S.KW;
+  // row = co, k = tap*Cs + ci; Cs and k0 are multiples of 8, so the chunk's 8 elements share one tap
+  const int tap = k0 / S.Cs, ci0 = k0 - tap * S.Cs;
+  const bool live = row < S.Co && tap < taps;
+  const float* W = P + S.off + ((int64_t)row * S.Ci + ci0) * taps + tap;
+  float v[8];
+#pragma unroll
+  for (int h = 0; h < 8; ++h) v[h] = (live && ci0 + h < S.Ci) ? W[h * taps] : 0.f;
   uint32_t w4[4];
 #pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    float v[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int k = k0 + j + h;
-      float x = 0.f;  // row = co, k = tap*Cs + ci
-      const int ci = k % S.Cs, tap = k / S.Cs;
-      if (row < S.Co && tap < taps && ci < S.Ci) x = W[((int64_t)row * S.Ci + ci) * taps + tap];
-      v[h] = x;
-    }
-    w4[j / 2] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-  }
+  for (int j = 0; j < 4; ++j) w4[j] = (uint32_t)f2bf(v[2 * j]) | ((uint32_t)f2bf(v[2 * j + 1]) << 16);
   bf16_t* dst = S.wf + e;
   *reinterpret_cast<uint4*>(dst) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
 }

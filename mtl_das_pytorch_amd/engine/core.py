@@ -457,7 +457,7 @@ class ConvLayer:
         return {"slab": P(self.slab), "grad": P(self.flat.grads, self.flat.off(m0.weight)), "ggs": self.wstride,
                 "G": self.G, "splits": self.splits, "Npad": self.Npad, "Kpad": self.Kpad_w, "Co": self.Co,
                 "Ci": self.Ci, "Cs": self.Cs, "KH": self.KH, "KW": self.KW,
-                "elems": self.G * self.Co * self.KH * self.KW * self.Cs}
+                "elems": self.G * self.Co * self.KH * self.KW * self.Ci}
 
     # ---- launches --------------------------------------------------------------------------------
     def fwd_args(self, src: dict, out: Act, bn: Optional[BNLayer], training: bool) -> tuple:
@@ -516,7 +516,7 @@ def build_wgfin_table(descs: List[dict], device) -> tuple:
         lanes = finalize_lanes(d["splits"])
         arr[i]["lanes"] = lanes
         arr[i]["block0"] = b0
-        b0 += math.ceil(d["elems"] * lanes / 256)
+        b0 += math.ceil(d["elems"] * lanes / (256 * lib().FIN_EPT))
     t = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
     return t, len(descs), b0
 

@@ -205,7 +205,7 @@ def test_stem_tap_packing_geometry():
     assert p.stem_pack == (7, 2)
     assert (c1.Ci, c1.KH, c1.KW, c1.Cs, c1.ph, c1.pw, c1.Ho, c1.Wo, c1.Kpad) == (7, 1, 7, 8, 0, 2, 33, 83, 64)
     d = c1.finalize_desc()
-    assert d["elems"] == 16 * 7 * 8 and (d["Ci"], d["KH"], d["KW"]) == (7, 1, 7)
+    assert d["elems"] == 16 * 7 * 7 and (d["Ci"], d["KH"], d["KW"]) == (7, 1, 7)
     c = InceptionProgram(Multi_Classifier(), 4, "cpu")
     s = c.ops[0].conv
     assert c.stem_pack == (3, 0) and (s.Ho, s.Wo, s.Kpad) == (49, 124, 32)

@@ -1,5 +1,6 @@
 # Kernel-trace the Model A bench under several variants (env assignments), one rocprofv3 run each, and
 # summarise per kernel.   bash tools/kt_variants.sh OUT "NAME1:VAR=a,VAR2=b" "NAME2:..." ...   (MODEL env: bench model)
+export MDA_CLEAN_EXIT=1  # bench.py: normal interpreter exit, so rocprofv3 flushes its trace
 set -e
 out=gpurun_out/$1; shift; mkdir -p $out
 for spec in "$@"; do

@@ -8,6 +8,7 @@
 #    limits: TCC 4 -- FETCH_SIZE uses 3, WRITE_SIZE 2 -- SQ 8, GRBM 2)  -> gpurun_out/pmc_<tag>_<group>/
 # 3. tools/pmc_table.py over the passes                           -> gpurun_out/pmc_<tag>.txt
 # Every rocprofv3 run has its own hard time limit (a counter request beyond the hardware's capacity hangs).
+export MDA_CLEAN_EXIT=1  # bench.py: normal interpreter exit, so rocprofv3 flushes its trace
 PROF_ARGS=${PROF_ARGS:-"--steps 12 --warmup 2 --no-tune --heldout 0"}
 prof_model() {
   local model=$1 tag=$2
