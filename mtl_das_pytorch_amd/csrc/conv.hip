@@ -908,38 +908,69 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const Wgr
 }
 
 // Sums the split-M partial slabs of many convolutions into the flat fp32 gradient buffer (deterministic,
-// one launch per backward), reference weight layout [Cout][Cin][KH][KW].
-// Threads walk the OUTPUT in its own order: a block owns FIN_EPT x (256 / lanes) consecutive NCHW weights,
-// so every store is a full-line contiguous write.  (Walking the slab's k-fastest order instead scattered
-// the stores with a KH*KW*4-byte stride: each gradient line was then assembled from partial writes of
-// up to KH*KW blocks on different XCDs, and the launch ran at ~1.5 TB/s.)  The slab reads are
-// tap-strided runs of consecutive input channels; a block covers ~FIN_EPT*256/taps channels of every
-// tap, so the lines it reads are mostly its own.
-// Each weight is reduced by D.lanes threads (a power of two <= 16, chosen per conv from its split count):
-// lane q sums splits q, q + lanes, ... (two chains) and the lane partials are added in lane order through
-// LDS -- deterministic.  Descriptors own whole blocks, so `lanes` is uniform within a block.
+// one launch per backward), reference weight layout [Cout][Cin][KH][KW].  Two thread mappings, chosen per
+// descriptor by its split count (D.order, set by the host; D.lanes = threads per weight, a power of two <= 16):
+// * order 1 (few splits, one lane; most of the bytes: Model C's wide layers): threads walk the OUTPUT in its
+//   own order, a block owning FIN_EPT x 256 consecutive NCHW weights, so every store is a full-line
+//   contiguous write.  (Walking the slab's k-fastest order scattered the stores with a KH*KW*4-byte
+//   stride: each gradient line was assembled from partial writes of up to KH*KW blocks on different
+//   XCDs, and the launch ran at ~1.5 TB/s.)  The slab reads are tap-strided runs of consecutive input
+//   channels; a block covers ~FIN_EPT*256/taps channels of every tap, so the lines it reads are its own.
+// * order 0 (many splits of a small weight: reads dominate): threads walk the slab's k-fastest order so
+//   the split reads are coalesced; lane q sums splits q, q + lanes, ... with 8 loads in flight and the
+//   lane partials are added in lane order through LDS -- deterministic.
+// Descriptors own whole blocks, so the mapping is uniform within a block.
 __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale) {
-  __shared__ float s_part[FIN_EPT][256];
+  __shared__ float s_part[256];
   int lo = 0, hi = nd - 1;  // last descriptor with block0 <= blockIdx.x
   while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (descs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
   const WgFinDesc& D = descs[lo];
   const int L = D.lanes, EPB = 256 / L;
-  const int taps = D.KH * D.KW, row = D.Ci * taps, per = D.Co * row;
-  const int q = threadIdx.x / EPB, ie = threadIdx.x - q * EPB;
-  const int base = (int)((int64_t)blockIdx.x - D.block0) * (EPB * FIN_EPT) + ie;
+  const int taps = D.KH * D.KW;
   const int elems = (int)D.elems, splits = D.splits;
   const int64_t sstride = (int64_t)D.Npad * D.Kpad;
+  if (D.order == 0) {  // slab order: elems = G * Co * taps * Cs
+    const int Kt = taps * D.Cs, perS = D.Co * Kt;
+    const int q = threadIdx.x / EPB, ie = threadIdx.x - q * EPB;
+    const int e = (int)((int64_t)blockIdx.x - D.block0) * EPB + ie;
+    const int g = e / perS, r = e - g * perS, co = r / Kt, k = r - co * Kt;
+    const int tap = k / D.Cs, ci = k - tap * D.Cs;
+    const bool ok = e < elems && ci < D.Ci;
+    const float* s = D.slab + ((int64_t)g * splits * D.Npad + co) * D.Kpad + k;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ok) {
+      int sp = q;
+      for (; sp + 7 * L < splits; sp += 8 * L) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += s[(int64_t)(sp + j * L) * sstride];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (sp + j * L < splits) acc[j] += s[(int64_t)(sp + j * L) * sstride];
+    }
+    s_part[threadIdx.x] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    __syncthreads();
+    if (ok && q == 0) {
+      float sum = 0.f;
+      for (int l = 0; l < L; ++l) sum += s_part[l * EPB + ie];
+      D.grad[g * D.ggs + (co * D.Ci + ci) * taps + tap] = sum * scale;
+    }
+    return;
+  }
+  // output order: elems = G * Co * Ci * taps, one lane per weight, FIN_EPT weights per thread
+  const int row = D.Ci * taps, per = D.Co * row;
+  const int base = (int)((int64_t)blockIdx.x - D.block0) * (256 * FIN_EPT) + threadIdx.x;
   const float* src[FIN_EPT];
   float* dst[FIN_EPT];
   bool ok[FIN_EPT];
-  // (g, co, ci, tap) of the first weight by division, then advanced by EPB in mixed radix (one division
+  // (g, co, ci, tap) of the first weight by division, then advanced by 256 in mixed radix (one division
   // at most per step: the index math would otherwise rival the memory time of this streaming kernel)
   int g = base / per, r = base - g * per;
   int co = r / row, ci = (r - co * row) / taps, tap = r - co * row - ci * taps;
-  const int s_ci = EPB / taps, s_tap = EPB - s_ci * taps;
+  const int s_ci = 256 / taps, s_tap = 256 - s_ci * taps;
 #pragma unroll
   for (int j = 0; j < FIN_EPT; ++j) {
-    const int e = base + j * EPB;
+    const int e = base + j * 256;
     ok[j] = e < elems;
     src[j] = D.slab + ((int64_t)g * splits * D.Npad + co) * D.Kpad + tap * D.Cs + ci;
     dst[j] = D.grad + g * D.ggs + ((co * D.Ci + ci) * taps + tap);  // NCHW offset within group g
@@ -952,16 +983,17 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
     }
     while (co >= D.Co) { co -= D.Co; ++g; }
   }
+  // (<= 8 splits) two independent chains per weight: up to 8 loads in flight per thread
   float a0[FIN_EPT], a1[FIN_EPT];
 #pragma unroll
   for (int j = 0; j < FIN_EPT; ++j) { a0[j] = 0.f; a1[j] = 0.f; }
-  int sp = q;
-  for (; sp + L < splits; sp += 2 * L) {
+  int sp = 0;
+  for (; sp + 1 < splits; sp += 2) {
 #pragma unroll
     for (int j = 0; j < FIN_EPT; ++j) {
       if (ok[j]) {
         a0[j] += src[j][(int64_t)sp * sstride];
-        a1[j] += src[j][(int64_t)(sp + L) * sstride];
+        a1[j] += src[j][(int64_t)(sp + 1) * sstride];
       }
     }
   }
@@ -970,24 +1002,9 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
     for (int j = 0; j < FIN_EPT; ++j)
       if (ok[j]) a0[j] += src[j][(int64_t)sp * sstride];
   }
-  if (L == 1) {
 #pragma unroll
-    for (int j = 0; j < FIN_EPT; ++j)
-      if (ok[j]) *dst[j] = (a0[j] + a1[j]) * scale;
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < FIN_EPT; ++j) s_part[j][threadIdx.x] = a0[j] + a1[j];
-  __syncthreads();
-  if (q == 0) {
-#pragma unroll
-    for (int j = 0; j < FIN_EPT; ++j) {
-      if (!ok[j]) continue;
-      float sum = 0.f;
-      for (int l = 0; l < L; ++l) sum += s_part[j][l * EPB + ie];
-      *dst[j] = sum * scale;
-    }
-  }
+  for (int j = 0; j < FIN_EPT; ++j)
+    if (ok[j]) *dst[j] = (a0[j] + a1[j]) * scale;
 }
 
 // ------------------------------------------------------------------------------------------------

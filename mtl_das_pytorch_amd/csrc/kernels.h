@@ -141,10 +141,13 @@ struct WgFinDesc {
   int64_t ggs;        // element stride between groups in the flat grad buffer
   int G, splits, Npad, Kpad, Co, Ci, Cs, KH, KW;
   int lanes;          // threads per weight (power of two <= 16): the splits are summed in lanes x parallel
-  int64_t elems;      // G * Co * Ci * KH * KW
+  int order;          // 1: output (NCHW) order, lanes == 1, FIN_EPT weights per thread; 0: slab order
+  int _pad;
+  int64_t elems;      // G * Co * Ci * KH * KW (order 1); G * Co * KH * KW * Cs (order 0)
   int64_t block0;     // first block index of this descriptor
 };
-// weights per thread (per lane) of wgrad_finalize: a block owns FIN_EPT * 256 / lanes consecutive weights
+// weights per thread of wgrad_finalize's output-order mapping (order 1): a block owns FIN_EPT * 256
+// consecutive NCHW weights
 constexpr int FIN_EPT = 4;
 
 enum TailKind { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, SIGMUL = 3, ADD_RELU = 4, POOL_RELU = 5 };

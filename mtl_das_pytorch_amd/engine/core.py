@@ -502,11 +502,17 @@ def finalize_lanes(splits: int) -> int:
     return lanes
 
 
+# convs with at most this many wgrad splits are finalized in output order (contiguous gradient stores);
+# more splits: slab order with several lanes per weight (coalesced split reads)
+FIN_OUT_MAX_SPLITS = int(__import__("os").environ.get("MDA_FIN_OUT_MAX", "2"))
+
+
 def build_wgfin_table(descs: List[dict], device) -> tuple:
     """Pack WgFinDesc structs (layout must match csrc/kernels.h)."""
     dt = np.dtype([("slab", "<u8"), ("grad", "<u8"), ("ggs", "<i8"), ("G", "<i4"), ("splits", "<i4"),
                    ("Npad", "<i4"), ("Kpad", "<i4"), ("Co", "<i4"), ("Ci", "<i4"), ("Cs", "<i4"), ("KH", "<i4"),
-                   ("KW", "<i4"), ("lanes", "<i4"), ("elems", "<i8"), ("block0", "<i8")])
+                   ("KW", "<i4"), ("lanes", "<i4"), ("order", "<i4"), ("_pad", "<i4"), ("elems", "<i8"),
+                   ("block0", "<i8")])
     assert dt.itemsize == lib().SIZEOF_WGFIN, (dt.itemsize, lib().SIZEOF_WGFIN)
     arr = np.zeros(len(descs), dtype=dt)
     b0 = 0
@@ -514,9 +520,14 @@ def build_wgfin_table(descs: List[dict], device) -> tuple:
         for k, v in d.items():
             arr[i][k] = v
         lanes = finalize_lanes(d["splits"])
-        arr[i]["lanes"] = lanes
         arr[i]["block0"] = b0
-        b0 += math.ceil(d["elems"] * lanes / (256 * lib().FIN_EPT))
+        if d["splits"] <= FIN_OUT_MAX_SPLITS:  # output order, one lane, FIN_EPT weights per thread
+            arr[i]["lanes"], arr[i]["order"] = 1, 1
+            b0 += math.ceil(d["elems"] / (256 * lib().FIN_EPT))
+        else:  # slab-order mapping (csrc/conv.hip wgrad_finalize_kernel): padded channels included
+            arr[i]["lanes"] = lanes
+            arr[i]["elems"] = d["G"] * d["Co"] * d["KH"] * d["KW"] * d["Cs"]
+            b0 += math.ceil(int(arr[i]["elems"]) * lanes / 256)
     t = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
     return t, len(descs), b0
 

@@ -35,7 +35,7 @@ def test_mtl_program_structure(monkeypatch):
     assert p.flat.off(g1) - p.flat.off(g0) == L["c0"].wstride
     # shared backbone input read with group stride 0, per-task prev level with stride > 0
     assert L["Fa"].gs == 0 and L["prevB"].gs > 0
-    assert p.wgfin_table.numel() == len(p.convs) * 80
+    assert p.wgfin_table.numel() == len(p.convs) * 88
     assert p.optseg_table.numel() == 2 * sum(c.G for c in p.convs) * 80
 
 
@@ -78,7 +78,7 @@ def test_inception_program_structure():
         if getattr(o, "dx", None) is not None or isinstance(o, CBR):
             assert 1 <= len(o.out.grad_sources()) <= 6
     # every parameter has a gradient producer: conv weights (finalize), BN (tails), fc (head)
-    assert p.wgfin_table.numel() == 94 * 80
+    assert p.wgfin_table.numel() == 94 * 88
     assert len(p.model.state_dict()) == 566
 
 
