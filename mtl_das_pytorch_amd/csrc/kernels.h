@@ -238,6 +238,12 @@ struct OptSeg {
 // keep in sync with engine/core.py build_optseg_table.
 constexpr int PACK_ROWS = 72;
 __host__ __device__ inline int pack_dgrad_cit(int taps) { return std::min(32, PACK_ROWS / taps); }
+// Forward image pack (optim.hip pack_fwd_rows): a block stages up to PACK_FWD_FLOATS contiguous master
+// floats = whole co rows (at least one) in LDS; rows of more than PACK_FWD_FLOATS floats are not supported.
+constexpr int PACK_FWD_FLOATS = 4096;
+__host__ __device__ inline int pack_fwd_rows(int Ci, int taps, int Co) {
+  return std::max(1, std::min(Co, PACK_FWD_FLOATS / (Ci * taps)));
+}
 
 struct AdamArgs {
   float* p; const float* g; float* m; float* v;

@@ -101,43 +101,51 @@ DEV void pack_dgrad_tile(const float* __restrict__ W, const OptSeg& S, int tile,
   }
 }
 
+// Forward image [Co][(kh,kw,ci)] of rb consecutive co rows (one contiguous span of the [Co][Ci][taps]
+// masters) through LDS: the span is read coalesced, each 16-byte store packs 8 channels of one tap (Cs and
+// Kpad_f are multiples of 8) read from LDS with a stride of taps floats (odd for every conv of the models:
+// conflict-free).  The direct per-chunk mapping read the masters with a stride of taps floats per lane and
+// was address-unit bound.  Padding rows (co >= Co) are never written (zero-initialised images).
+DEV void pack_fwd_rows_block(const float* __restrict__ W, const OptSeg& S, int blk, float* s_w) {
+  const int taps = S.KH * S.KW, row = S.Ci * taps;
+  const int rb = pack_fwd_rows(S.Ci, taps, S.Co);
+  const int co0 = blk * rb, nr = min(rb, S.Co - co0);
+  const float* src = W + (int64_t)co0 * row;
+  for (int e = threadIdx.x; e < nr * row; e += 256) s_w[e] = src[e];
+  __syncthreads();
+  const int K8 = S.Kpad_f >> 3;
+  for (int item = threadIdx.x; item < nr * K8; item += 256) {
+    const int r = item / K8, k0 = (item - r * K8) * 8;
+    const int tap = k0 / S.Cs, ci0 = k0 - tap * S.Cs;
+    const float* w = s_w + r * row + ci0 * taps + tap;
+    uint32_t w4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x0 = (tap < taps && ci0 + 2 * j < S.Ci) ? w[(2 * j) * taps] : 0.f;
+      const float x1 = (tap < taps && ci0 + 2 * j + 1 < S.Ci) ? w[(2 * j + 1) * taps] : 0.f;
+      w4[j] = (uint32_t)f2bf(x0) | ((uint32_t)f2bf(x1) << 16);
+    }
+    *reinterpret_cast<uint4*>(S.wf + (int64_t)(co0 + r) * S.Kpad_f + k0) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+  }
+}
+
 // Writes the packed bf16 MFMA images of every conv weight.  Segment `kind` selects the image:
-// 1 = forward [Co][(kh,kw,ci)] (rows Npad, cols Kpad_f): one thread per 8 packed elements (16-B stores,
-// coalesced), padding (re)written as zeros; 2 = data-gradient [Ci][(kh,kw,co)]: one block per LDS-
-// transposed tile (pack_dgrad_tile).
+// 1 = forward [Co][(kh,kw,ci)] (rows Npad, cols Kpad_f): one block per pack_fwd_rows co rows
+// (pack_fwd_rows_block); 2 = data-gradient [Ci][(kh,kw,co)]: one block per LDS-transposed tile
+// (pack_dgrad_tile).
 // `step` (non-null after an Adam update): the step counter is advanced here -- the pack runs after the
 // Adam kernel that read it, so the separate one-thread launch is not needed.
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, const OptSeg* __restrict__ segs, int ns,
                                                    float* step) {
   __shared__ float s_t[PACK_ROWS][65];
+  static_assert(PACK_ROWS * 65 >= PACK_FWD_FLOATS, "pack_fwd_rows_block stages its rows in s_t");
   if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1.f;
   int lo = 0, hi = ns - 1;
   while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (segs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
   const OptSeg& S = segs[lo];
-  if (S.kind == 2) {
-    pack_dgrad_tile(P + S.off, S, (int)((int64_t)blockIdx.x - S.block0), s_t);
-    return;
-  }
-  const int64_t e8 = ((int64_t)blockIdx.x - S.block0) * 256 + threadIdx.x;  // index of an 8-element chunk
-  const int K = S.Kpad_f;
-  const int64_t total8 = S.n / 8;  // S.n = rows * K (multiple of 8)
-  if (e8 >= total8) return;
-  const int64_t e = e8 * 8;
-  const int row = (int)e / K;  // S.n < 2^31
-  const int k0 = (int)e - row * K;
-  const int taps = S.KH * S.KW;
-  // row = co, k = tap*Cs + ci; Cs and k0 are multiples of 8, so the chunk's 8 elements share one tap
-  const int tap = k0 / S.Cs, ci0 = k0 - tap * S.Cs;
-  const bool live = row < S.Co && tap < taps;
-  const float* W = P + S.off + ((int64_t)row * S.Ci + ci0) * taps + tap;
-  float v[8];
-#pragma unroll
-  for (int h = 0; h < 8; ++h) v[h] = (live && ci0 + h < S.Ci) ? W[h * taps] : 0.f;
-  uint32_t w4[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) w4[j] = (uint32_t)f2bf(v[2 * j]) | ((uint32_t)f2bf(v[2 * j + 1]) << 16);
-  bf16_t* dst = S.wf + e;
-  *reinterpret_cast<uint4*>(dst) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+  const int blk = (int)((int64_t)blockIdx.x - S.block0);
+  if (S.kind == 2) pack_dgrad_tile(P + S.off, S, blk, s_t);
+  else pack_fwd_rows_block(P + S.off, S, blk, &s_t[0][0]);
 }
 
 // Fused optimizer step: every block of kind 0 updates 1024 consecutive elements of a plain range (BN

@@ -533,6 +533,7 @@ def build_wgfin_table(descs: List[dict], device) -> tuple:
 
 
 PACK_ROWS = 72  # csrc/kernels.h
+PACK_FWD_FLOATS = 4096  # csrc/kernels.h
 
 
 def plain_ranges(numel: int, covered: List[tuple]) -> List[dict]:
@@ -566,7 +567,11 @@ def build_optseg_table(segs: List[dict], device) -> tuple:
                 raise ValueError(f"pack: {taps} taps exceed the {PACK_ROWS} LDS rows of a tile")
             cit = min(32, PACK_ROWS // taps)
             b0 += math.ceil(s["Co"] / 64) * math.ceil(s["Ci"] / cit)
-        else:
-            b0 += math.ceil(s["n"] / 2048)  # 256 threads x 8 packed elements
+        else:  # whole co rows staged in LDS (csrc/optim.hip pack_fwd_rows_block)
+            row = s["Ci"] * s["KH"] * s["KW"]
+            if row > PACK_FWD_FLOATS:
+                raise ValueError(f"pack: a {row}-float weight row exceeds the {PACK_FWD_FLOATS}-float LDS stage")
+            rb = max(1, min(s["Co"], PACK_FWD_FLOATS // row))
+            b0 += math.ceil(s["Co"] / rb)
     t = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
     return t, len(segs), b0
