@@ -920,10 +920,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const Wgr
 //   the split reads are coalesced; lane q sums splits q, q + lanes, ... with 8 loads in flight and the
 //   lane partials are added in lane order through LDS -- deterministic.
 // Descriptors own whole blocks, so the mapping is uniform within a block.
-__global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale) {
+__global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale, int remap) {
   __shared__ float s_part[256];
-  int lo = 0, hi = nd - 1;  // last descriptor with block0 <= blockIdx.x
-  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (descs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
+  const int bx = xcd_block((int)blockIdx.x, (int)gridDim.x, remap);
+  int lo = 0, hi = nd - 1;  // last descriptor with block0 <= bx
+  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (descs[mid].block0 <= (int64_t)bx) lo = mid; else hi = mid - 1; }
   const WgFinDesc& D = descs[lo];
   const int L = D.lanes, EPB = 256 / L;
   const int taps = D.KH * D.KW;
@@ -932,7 +933,7 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
   if (D.order == 0) {  // slab order: elems = G * Co * taps * Cs
     const int Kt = taps * D.Cs, perS = D.Co * Kt;
     const int q = threadIdx.x / EPB, ie = threadIdx.x - q * EPB;
-    const int e = (int)((int64_t)blockIdx.x - D.block0) * EPB + ie;
+    const int e = (int)((int64_t)bx - D.block0) * EPB + ie;
     const int g = e / perS, r = e - g * perS, co = r / Kt, k = r - co * Kt;
     const int tap = k / D.Cs, ci = k - tap * D.Cs;
     const bool ok = e < elems && ci < D.Ci;
@@ -959,7 +960,7 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
   }
   // output order: elems = G * Co * Ci * taps, one lane per weight, FIN_EPT weights per thread
   const int row = D.Ci * taps, per = D.Co * row;
-  const int base = (int)((int64_t)blockIdx.x - D.block0) * (256 * FIN_EPT) + threadIdx.x;
+  const int base = (int)((int64_t)bx - D.block0) * (256 * FIN_EPT) + threadIdx.x;
   const float* src[FIN_EPT];
   float* dst[FIN_EPT];
   bool ok[FIN_EPT];
@@ -1175,7 +1176,8 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
 
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st) {
   if (nblocks <= 0) return 0;
-  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, d_descs, nd, scale);
+  static const int remap = env_flag("MDA_XCD_REMAP", 0);
+  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, d_descs, nd, scale, remap);
   return (int)hipGetLastError();
 }
 

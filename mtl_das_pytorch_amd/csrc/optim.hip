@@ -136,14 +136,15 @@ DEV void pack_fwd_rows_block(const float* __restrict__ W, const OptSeg& S, int b
 // `step` (non-null after an Adam update): the step counter is advanced here -- the pack runs after the
 // Adam kernel that read it, so the separate one-thread launch is not needed.
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, const OptSeg* __restrict__ segs, int ns,
-                                                   float* step) {
+                                                   float* step, int remap) {
   __shared__ float s_t[PACK_ROWS][65];
+  const int bx = xcd_block((int)blockIdx.x, (int)gridDim.x, remap);
   static_assert(PACK_ROWS * 65 >= PACK_FWD_FLOATS, "pack_fwd_rows_block stages its rows in s_t");
   if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1.f;
   int lo = 0, hi = ns - 1;
-  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (segs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
+  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (segs[mid].block0 <= (int64_t)bx) lo = mid; else hi = mid - 1; }
   const OptSeg& S = segs[lo];
-  const int blk = (int)((int64_t)blockIdx.x - S.block0);
+  const int blk = (int)((int64_t)bx - S.block0);
   if (S.kind == 2) pack_dgrad_tile(P + S.off, S, blk, s_t);
   else pack_fwd_rows_block(P + S.off, S, blk, &s_t[0][0]);
 }
@@ -237,7 +238,9 @@ int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nb
     if (rc) return rc;
   }
   float* step = a.update ? const_cast<float*>(a.step) : nullptr;
-  if (nblocks > 0) hipLaunchKernelGGL(pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, (const float*)a.p, d_segs, ns, step);
+  static const int remap = env_flag("MDA_XCD_REMAP", 0);
+  if (nblocks > 0)
+    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, (const float*)a.p, d_segs, ns, step, remap);
   int rc = (int)hipGetLastError();
   if (rc || !a.update || nblocks > 0) return rc;
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);

@@ -758,7 +758,10 @@ class LoweredProgram:
         backbone's backward instead of queueing at the step's tail.  Only when stream 2 is otherwise
         unused (Model A/B).  Returns (stream, anchor launch) or None."""
         import os
-        frac = float(os.environ.get("MDA_WGRAD_STAGE", "0"))
+        mode = os.environ.get("MDA_WGRAD_STAGE", self.default_wgrad_stage)
+        if mode == "join":
+            return self._stage_wgrads_join(wg, ls)
+        frac = float(mode)
         wg0 = [l for l in wg if l.stream == 0]
         n1 = int(len(wg0) * frac)
         if not 0 < n1 < len(wg0) or any(l.stream == self.STAGE_STREAM for l in ls):
@@ -773,6 +776,34 @@ class LoweredProgram:
         for l in wg0[:n1]:
             l.stream = self.STAGE_STREAM
         return self.STAGE_STREAM, anchor
+
+    default_wgrad_stage = "0"  # engine/inception.py: "join"
+
+    def _stage_wgrads_join(self, wg: List[Launch], ls: List[Launch]):
+        """MDA_WGRAD_STAGE=join (Model C's default): once side stream 2 has issued its last backward launch
+        (the Inception blocks are done and only the single-stream stem is left on the main stream), the main
+        stream's weight gradients of every layer before that point are batched on stream 2, waiting on the
+        next main-stream launch -- they overlap the stem's backward chain instead of queueing at the step's
+        tail behind it.  Returns (stream, anchor launch) or None."""
+        S = self.STAGE_STREAM
+        fin = next(i for i, l in enumerate(ls) if l.name == "wgrad_finalize")
+        last2 = max((i for i in range(fin) if ls[i].stream == S and ls[i].name != "conv_wgrad"), default=None)
+        if last2 is None:
+            return None
+        ai = next((i for i in range(last2 + 1, fin) if ls[i].stream == 0 and ls[i].name != "conv_wgrad"), None)
+        if ai is None:
+            return None
+        staged = [l for l in wg if l.stream == 0 and ls.index(l) < ai]
+        if not staged:
+            return None
+        anchor = ls[ai]
+        if anchor.record is None:
+            anchor.record = "wgstage"
+        else:
+            self.bwd.alias["wgstage"] = anchor.record
+        for l in staged:
+            l.stream = S
+        return S, anchor
 
     @staticmethod
     def _fan_out_wgrads() -> bool:

@@ -116,6 +116,36 @@ def test_wgrad_batching_structure():
         _check_event_order(p.bwd)
 
 
+def test_wgrad_join_stage_structure(monkeypatch):
+    """Model C (MDA_WGRAD_STAGE=join): the main stream's weight gradients of the Inception blocks move to
+    stream 2, batched right after the first main-stream launch that follows stream 2's last backward launch
+    (waiting on its event); the stem's weight gradients stay at the main stream's tail; every conv is in
+    exactly one batch and the finalize waits for every stream's last batch."""
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.models import Multi_Classifier
+    monkeypatch.setenv("MDA_WGRAD_STAGE", "join")
+    monkeypatch.setenv("MDA_EARLY_OPT", "0")
+    p = InceptionProgram(Multi_Classifier(), 4, "cpu")
+    ls = p.bwd.launches
+    n_wg = sum(1 for l in ls if l.name == "conv_wgrad")
+    last2 = max(i for i, l in enumerate(ls) if l.stream == 2 and l.name != "conv_wgrad")
+    ai = next(i for i in range(last2 + 1, len(ls)) if ls[i].stream == 0 and ls[i].name != "conv_wgrad")
+    anchor, last2_l = ls[ai], ls[last2]
+    moved = {id(l.owner) for l in ls[:ai] if l.name == "conv_wgrad" and l.stream == 0}
+    tail = {id(l.owner) for l in ls[ai:] if l.name == "conv_wgrad" and l.stream == 0}
+    assert moved and tail
+    p.batch_wgrads()
+    ls = p.bwd.launches
+    b = [l for l in ls if l.name == "wgrad_batched"]
+    assert sum(l.args[2] for l in b) == n_wg
+    s2 = [l for l in b if l.stream == 2]
+    assert s2[0].waits == ("wgstage",) and ls.index(s2[0]) == ls.index(anchor) + 1
+    assert all(ls.index(l) > ls.index(last2_l) for l in s2)
+    fin = ls[-1]
+    assert fin.name == "wgrad_finalize" and set(fin.waits) == {f"wgrads_s{s}" for s in {l.stream for l in b}}
+    _check_event_order(p.bwd)
+
+
 def test_wgrad_fanout_structure(monkeypatch):
     """Opt-in (MDA_WGRAD_FANOUT=1): the main stream's batches are fanned out over the side streams from
     one fork point."""
