@@ -215,6 +215,18 @@ class LoweredProgram:
         import os
         return os.environ.get("MDA_NOL", "1") == "1"
 
+    NOL_MAX_PX = 1 << 30  # per-model default of MDA_NOL_MAX_PX
+
+    def nol_max_px(self) -> int:
+        """Normalise-on-load only for consumer convs with at most this many output pixels (B*Ho*Wo):
+        on the large stem maps the on-load transform (repeated KH*KW times per element by the im2col)
+        costs more than the BN+ReLU tail it removes (MDA_NOL_MAX_PX overrides the model's default)."""
+        import os
+        return int(os.environ.get("MDA_NOL_MAX_PX", str(self.NOL_MAX_PX)))
+
+    def nol_for(self, conv: ConvLayer) -> bool:
+        return self.nol and conv.M_out <= self.nol_max_px()
+
     def _conv_fwd(self, ph: Phase, c: ConvLayer, src: dict, out: Act, bn: BNLayer, training: bool, nol=None):
         mode, cfg, G, d = c.fwd_args(src, out, bn, training)
         if nol is not None:  # (BNLayer of the input, activation kind[, residual Act, residual BNLayer or None])

@@ -197,7 +197,7 @@ class MTLProgram(LoweredProgram):
                 if not P_["proj"] and ri >= 2:
                     ph.pending_waits.append(f"F{ri - 1}")
             self._conv_fwd(ph, L["ca"], s, L["ya"], L["bna"], training, nol=nol_in)
-            if self.nol:  # conv b normalises ya on load: no BN+ReLU tail, ha never materialised
+            if self.nol_for(L["cb"]):  # conv b normalises ya on load: no BN+ReLU tail, ha never materialised
                 self._conv_fwd(ph, L["cb"], src_dict(L["ya"]), L["yb"], L["bnb"], training, nol=(L["bna"], ACT_RELU))
             else:
                 self._tail(ph, ACT_RELU, 1, L["ya"], L["bna"], L["ha"], training)
@@ -222,7 +222,7 @@ class MTLProgram(LoweredProgram):
             ph.pending_waits.append(f"F{2 * lvl + 1}")
             s = src_dict(L["Fa"], L["prevB"]) if L["prevB"] is not None else src_dict(L["Fa"])
             self._conv_fwd(ph, L["c0"], s, L["ym1"], L["bn0"], training)
-            if self.nol:
+            if self.nol_for(L["c3"]):
                 self._conv_fwd(ph, L["c3"], src_dict(L["ym1"]), L["ym2"], L["bn3"], training, nol=(L["bn0"], ACT_RELU))
             else:
                 self._tail(ph, ACT_RELU, T, L["ym1"], L["bn0"], L["hm"], training)
@@ -321,7 +321,7 @@ class MTLProgram(LoweredProgram):
             self._tail_bwd(ph, SIGMUL, T, L["ym2"], L["bn3"], [(L["dA"].p, L["dA"].gs, L["dA"].ld)], L["dym2"],
                            r=L["Fb"], side=L["dF"])
             ph.mark(f"dF{li}")  # F_{2l+2}'s gradient from this level is complete here
-            if self.nol:
+            if self.nol_for(L["c3"]):
                 self._conv_bwd(ph, L["c3"], src_dict(L["ym1"]), L["dym2"], L["dhm"], nol=(L["bn0"], ACT_RELU))
             else:
                 self._conv_bwd(ph, L["c3"], src_dict(L["hm"]), L["dym2"], L["dhm"])
@@ -375,7 +375,7 @@ class MTLProgram(LoweredProgram):
                 self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["in"], side=R["side"],
                                apply_only=msbns)
             R["tail_bwd"] = ph.launches[-1]
-            if self.nol:
+            if self.nol_for(R["cb"]):
                 self._conv_bwd(ph, R["cb"], src_dict(R["ya"]), R["dyb"], R["dha"], nol=(R["bna"], ACT_RELU))
             else:
                 self._conv_bwd(ph, R["cb"], src_dict(R["ha"]), R["dyb"], R["dha"])
