@@ -19,7 +19,7 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 tot = collections.defaultdict(float)
 cnt = collections.Counter()
 for r in rows:
-    n = r["Kernel_Name"].split("(")[0][:70]
+    n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:70]
     tot[n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     cnt[n] += 1
 # steady state: the last 10 complete steps (windows between consecutive gather launches)
@@ -29,7 +29,7 @@ if len(gi) >= 12:
     wt = collections.defaultdict(float)
     wc = collections.Counter()
     for r in win:
-        n = r["Kernel_Name"].split("(")[0][:70]
+        n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:70]
         wt[n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         wc[n] += 1
     WS = sum(wt.values())
