@@ -625,7 +625,7 @@ class LoweredProgram:
         staged = self._stage_wgrads(wg, ls, anchor_of)
         # MDA_FIN_SPLIT=1 (opt-in; measured neutral: A 31.53-31.58k vs 31.57-31.62k, C 6.89k vs 6.86k): one
         # finalize per stream, right after that stream's batches
-        split_ok = (staged is None and not self._fan_out_wgrads() and any(l.stream == 0 for l in wg)
+        split_ok = (not staged and not self._fan_out_wgrads() and any(l.stream == 0 for l in wg)
                     and all(l.owner is not None for l in wg))
         # early optimizer: each side stream finalizes its convs and runs Adam + the bf16 re-pack on every
         # parameter only it produces gradients for, overlapping the main stream's remaining backward
@@ -650,9 +650,10 @@ class LoweredProgram:
                 batched.append(Launch("wgrad_batched", k_wgrad_batched, key, table, len(group), nblocks, stream=st))
                 costs.append(sum(_wgrad_cost(key % WGRAD_AOL_CFG, l.args[1], l.args[2]) for l in group))
             pos = max((i for i, k in enumerate(keep) if k.stream == st), default=len(keep) - 1) + 1
-            if staged is not None and st == staged[0]:
-                pos = keep.index(staged[1]) + 1
-                batched[0].waits = ("wgstage",)
+            if staged and st in staged:
+                anchor, tag = staged[st]
+                pos = keep.index(anchor) + 1
+                batched[0].waits = (tag,)
             if st == 0 and len(batched) > 1 and pos > 0 and self._fan_out_wgrads():
                 # the main stream's batches form the step's tail (nothing else is left to overlap them):
                 # fan them out over the side streams from one fork point so the tile configs run side by
@@ -771,8 +772,8 @@ class LoweredProgram:
         unused (Model A/B).  Returns (stream, anchor launch) or None."""
         import os
         mode = os.environ.get("MDA_WGRAD_STAGE", self.default_wgrad_stage)
-        if mode == "join":
-            return self._stage_wgrads_join(wg, ls)
+        if mode in ("join", "join2"):
+            return self._stage_wgrads_join(wg, ls, anchor_of if mode == "join2" else None)
         frac = float(mode)
         wg0 = [l for l in wg if l.stream == 0]
         n1 = int(len(wg0) * frac)
@@ -787,16 +788,24 @@ class LoweredProgram:
             self.bwd.alias["wgstage"] = anchor.record
         for l in wg0[:n1]:
             l.stream = self.STAGE_STREAM
-        return self.STAGE_STREAM, anchor
+        return {self.STAGE_STREAM: (anchor, "wgstage")}
+
+    def _mark(self, anchor: Launch, tag: str):
+        if anchor.record is None:
+            anchor.record = tag
+        else:
+            self.bwd.alias[tag] = anchor.record
 
     default_wgrad_stage = "0"  # engine/inception.py: "join"
 
-    def _stage_wgrads_join(self, wg: List[Launch], ls: List[Launch]):
-        """MDA_WGRAD_STAGE=join (Model C's default): once side stream 2 has issued its last backward launch
-        (the Inception blocks are done and only the single-stream stem is left on the main stream), the main
-        stream's weight gradients of every layer before that point are batched on stream 2, waiting on the
-        next main-stream launch -- they overlap the stem's backward chain instead of queueing at the step's
-        tail behind it.  Returns (stream, anchor launch) or None."""
+    def _stage_wgrads_join(self, wg: List[Launch], ls: List[Launch], anchor_of: Optional[dict] = None):
+        """MDA_WGRAD_STAGE=join: once side stream 2 has issued its last backward launch (the Inception blocks
+        are done and only the single-stream stem is left on the main stream), the main stream's weight
+        gradients of every layer before that point are batched on stream 2, waiting on the next main-stream
+        launch -- they overlap the stem's backward chain instead of queueing at the step's tail.
+        MDA_WGRAD_STAGE=join2 (``anchor_of`` given) also moves the first half (program order: the deepest) of
+        the remaining main-stream weight gradients -- the stem's -- to stream 1, right after the last of
+        their dy producers.  Returns {stream: (anchor launch, event tag)} or None."""
         S = self.STAGE_STREAM
         fin = next(i for i, l in enumerate(ls) if l.name == "wgrad_finalize")
         last2 = max((i for i in range(fin) if ls[i].stream == S and ls[i].name != "conv_wgrad"), default=None)
@@ -808,14 +817,21 @@ class LoweredProgram:
         staged = [l for l in wg if l.stream == 0 and ls.index(l) < ai]
         if not staged:
             return None
-        anchor = ls[ai]
-        if anchor.record is None:
-            anchor.record = "wgstage"
-        else:
-            self.bwd.alias["wgstage"] = anchor.record
+        out = {S: (ls[ai], "wgstage")}
+        self._mark(ls[ai], "wgstage")
         for l in staged:
             l.stream = S
-        return S, anchor
+        if anchor_of is not None:
+            rest = [l for l in wg if l.stream == 0 and ls.index(l) > ai]
+            g1 = rest[:len(rest) // 2]
+            a1 = anchor_of.get(id(g1[-1])) if g1 else None
+            last1 = max((i for i in range(fin) if ls[i].stream == 1 and ls[i].name != "conv_wgrad"), default=-1)
+            if a1 is not None and ls.index(a1) > last1:
+                out[1] = (a1, "wgstage1")
+                self._mark(a1, "wgstage1")
+                for l in g1:
+                    l.stream = 1
+        return out
 
     @staticmethod
     def _fan_out_wgrads() -> bool:

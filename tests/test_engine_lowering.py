@@ -116,14 +116,16 @@ def test_wgrad_batching_structure():
         _check_event_order(p.bwd)
 
 
-def test_wgrad_join_stage_structure(monkeypatch):
-    """Model C (MDA_WGRAD_STAGE=join): the main stream's weight gradients of the Inception blocks move to
+@pytest.mark.parametrize("mode", ["join", "join2"])
+def test_wgrad_join_stage_structure(monkeypatch, mode):
+    """Model C (MDA_WGRAD_STAGE=join / join2): the main stream's weight gradients of the Inception blocks move to
     stream 2, batched right after the first main-stream launch that follows stream 2's last backward launch
     (waiting on its event); the stem's weight gradients stay at the main stream's tail; every conv is in
-    exactly one batch and the finalize waits for every stream's last batch."""
+    exactly one batch and the finalize waits for every stream's last batch.  join2 also moves the first half
+    of the stem's weight gradients to stream 1, after their last dy producer."""
     from mtl_das_pytorch_amd.engine.inception import InceptionProgram
     from mtl_das_pytorch_amd.models import Multi_Classifier
-    monkeypatch.setenv("MDA_WGRAD_STAGE", "join")
+    monkeypatch.setenv("MDA_WGRAD_STAGE", mode)
     monkeypatch.setenv("MDA_EARLY_OPT", "0")
     p = InceptionProgram(Multi_Classifier(), 4, "cpu")
     ls = p.bwd.launches
@@ -141,6 +143,10 @@ def test_wgrad_join_stage_structure(monkeypatch):
     s2 = [l for l in b if l.stream == 2]
     assert s2[0].waits == ("wgstage",) and ls.index(s2[0]) == ls.index(anchor) + 1
     assert all(ls.index(l) > ls.index(last2_l) for l in s2)
+    if mode == "join2":
+        s1 = [l for l in b if l.stream == 1]
+        assert s1[0].waits == ("wgstage1",) and ls.index(s1[0]) > ls.index(anchor)
+        assert sum(l.args[2] for l in b if l.stream == 0) == len(tail) - len(tail) // 2
     fin = ls[-1]
     assert fin.name == "wgrad_finalize" and set(fin.waits) == {f"wgrads_s{s}" for s in {l.stream for l in b}}
     _check_event_order(p.bwd)
