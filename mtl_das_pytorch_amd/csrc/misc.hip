@@ -59,37 +59,55 @@ int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, 
 }
 
 
+DEV void unpack8(const uint4& u, float* v) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+// 3x3 pools of the Inception model: MAX = 1 max pool stride 2 (no padding), MAX = 0 average pool stride 1
+// padding 1 (count_include_pad: always /9).  One thread per (output pixel, 8-channel group).  All nine
+// window loads are issued before any is consumed (with the load and its use in the same bounds-checked
+// region, each tap waited for its own memory round trip), and the index math is 32-bit (n < 2^31,
+// checked by the launcher).
 template <int MAX>
 __global__ __launch_bounds__(256) void pool3_fwd_kernel(PoolArgs a) {
   const int CG = a.C >> 3;
-  const int64_t n = (int64_t)a.B * a.Ho * a.Wo * CG;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int cg = (int)(i % CG);
-    const int64_t p = i / CG;
-    const int b = (int)(p / (a.Ho * a.Wo));
-    const int r = (int)(p - (int64_t)b * a.Ho * a.Wo);
+  const int HWo = a.Ho * a.Wo;
+  const int n = a.B * HWo * CG;
+  constexpr int s = MAX ? 2 : 1, pd = MAX ? 0 : 1;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int p = i / CG, cg = i - p * CG;
+    const int b = p / HWo, r = p - b * HWo;
     const int oh = r / a.Wo, ow = r - oh * a.Wo;
+    uint4 raw[9];
+    bool ok[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ih = oh * s - pd + t / 3, iw = ow * s - pd + t % 3;
+      ok[t] = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      raw[t] = ok[t] ? *reinterpret_cast<const uint4*>(a.x + ((int64_t)(b * a.H + ih) * a.W + iw) * a.ldx + cg * 8)
+                     : make_uint4(0, 0, 0, 0);
+    }
     float acc[8];
     int am[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { acc[j] = MAX ? -INFINITY : 0.f; am[j] = 0; }
-    const int s = MAX ? 2 : 1, pd = MAX ? 0 : 1;
-    for (int kh = 0; kh < 3; ++kh) {
-      const int ih = oh * s - pd + kh;
-      if (ih < 0 || ih >= a.H) continue;
-      for (int kw = 0; kw < 3; ++kw) {
-        const int iw = ow * s - pd + kw;
-        if (iw < 0 || iw >= a.W) continue;
-        float v[8];
-        load8(a.x + ((int64_t)(b * a.H + ih) * a.W + iw) * a.ldx + cg * 8, v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          // torch semantics: first max in row-major order, and a NaN wins (propagates; last NaN's index)
-          if (MAX) {
-            if (v[j] > acc[j] || isnan(v[j])) { acc[j] = v[j]; am[j] = kh * 3 + kw; }
-          } else {
-            acc[j] += v[j];
-          }
+    for (int t = 0; t < 9; ++t) {
+      if (MAX && !ok[t]) continue;  // (the models' max-pool windows are always inside the map)
+      float v[8];
+      unpack8(raw[t], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // torch semantics: first max in row-major order, and a NaN wins (propagates; last NaN's index)
+        if (MAX) {
+          if (v[j] > acc[j] || isnan(v[j])) { acc[j] = v[j]; am[j] = t; }
+        } else {
+          acc[j] += v[j];
         }
       }
     }
@@ -97,46 +115,78 @@ __global__ __launch_bounds__(256) void pool3_fwd_kernel(PoolArgs a) {
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) { lo |= (uint32_t)am[j] << (8 * j); hi |= (uint32_t)am[j + 4] << (8 * j); }
-      *reinterpret_cast<uint2*>(a.am + p * a.C + cg * 8) = make_uint2(lo, hi);
+      *reinterpret_cast<uint2*>(a.am + (int64_t)p * a.C + cg * 8) = make_uint2(lo, hi);
     }
     if (!MAX) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
     }
-    store8(a.y + p * a.ldy + cg * 8, acc);
+    store8(a.y + (int64_t)p * a.ldy + cg * 8, acc);
   }
 }
 
+// Gradient of the input: sum over the output windows covering an input pixel (<= 4 for the stride-2 max
+// pool, <= 9 for the average pool) and over the fp32 gradient sources; per source, every window's loads are
+// issued before any is consumed.  MAX = 1: max pool, the argmax stored by the training forward routes the
+// gradient (a.am); MAX = 2: max pool without it (MDA_POOL_ARGMAX=0), each window is re-read to find its
+// maximum (a separate instantiation: sharing one kernel spilled the argmax path to scratch); MAX = 0: average.
 template <int MAX>
 __global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {
   const int CG = a.C >> 3;
-  const int64_t n = (int64_t)a.B * a.H * a.W * CG;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int cg = (int)(i % CG);
-    const int64_t p = i / CG;
-    const int b = (int)(p / (a.H * a.W));
-    const int r = (int)(p - (int64_t)b * a.H * a.W);
+  const int HW = a.H * a.W;
+  const int n = a.B * HW * CG;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int p = i / CG, cg = i - p * CG;
+    const int b = p / HW, r = p - b * HW;
     const int ih = r / a.W, iw = r - ih * a.W;
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    if (MAX) {
-      // windows (stride 2, no pad) covering ih: oh in [ceil((ih-2)/2), ih/2]
+    if (MAX == 1) {
+      // windows (stride 2, no pad) covering ih: oh in [ceil((ih-2)/2), ih/2] -- at most 2 x 2
+      const int oh0 = max(0, (ih - 1) >> 1), oh1 = min(a.Ho - 1, ih >> 1);
+      const int ow0 = max(0, (iw - 1) >> 1), ow1 = min(a.Wo - 1, iw >> 1);
+      uint2 w[4];
+      int q[4], me[4];
+      bool ok[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int oh = oh0 + (t >> 1), ow = ow0 + (t & 1);
+        ok[t] = oh <= oh1 && ow <= ow1 && ih <= 2 * oh + 2 && iw <= 2 * ow + 2;
+        q[t] = (b * a.Ho + oh) * a.Wo + ow;
+        me[t] = (ih - 2 * oh) * 3 + (iw - 2 * ow);
+        w[t] = ok[t] ? *reinterpret_cast<const uint2*>(a.am + (int64_t)q[t] * a.C + cg * 8) : make_uint2(0, 0);
+      }
+      for (int sidx = 0; sidx < a.g.n; ++sidx) {
+        const float* gp = a.g.p[sidx];
+        const int ld = a.g.ld[sidx];
+        float4 g0[4], g1[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float* src = gp + (int64_t)q[t] * ld + cg * 8;
+          g0[t] = ok[t] ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
+          g1[t] = ok[t] ? *reinterpret_cast<const float4*>(src + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {  // (a window outside the range has w = 0 and g = 0: adds nothing)
+          const uint32_t m = (uint32_t)me[t];
+          acc[0] += ((w[t].x & 255u) == m) ? g0[t].x : 0.f;
+          acc[1] += (((w[t].x >> 8) & 255u) == m) ? g0[t].y : 0.f;
+          acc[2] += (((w[t].x >> 16) & 255u) == m) ? g0[t].z : 0.f;
+          acc[3] += ((w[t].x >> 24) == m) ? g0[t].w : 0.f;
+          acc[4] += ((w[t].y & 255u) == m) ? g1[t].x : 0.f;
+          acc[5] += (((w[t].y >> 8) & 255u) == m) ? g1[t].y : 0.f;
+          acc[6] += (((w[t].y >> 16) & 255u) == m) ? g1[t].z : 0.f;
+          acc[7] += ((w[t].y >> 24) == m) ? g1[t].w : 0.f;
+        }
+      }
+    } else if (MAX == 2) {
       const int oh0 = max(0, (ih - 1) >> 1), oh1 = min(a.Ho - 1, ih >> 1);
       const int ow0 = max(0, (iw - 1) >> 1), ow1 = min(a.Wo - 1, iw >> 1);
       for (int oh = oh0; oh <= oh1; ++oh)
         for (int ow = ow0; ow <= ow1; ++ow) {
           if (ih < 2 * oh || ih > 2 * oh + 2 || iw < 2 * ow || iw > 2 * ow + 2) continue;
           const int me = (ih - 2 * oh) * 3 + (iw - 2 * ow);
-          if (a.am) {  // argmax stored by the forward: one 8-byte load instead of the 9-pixel window
-            const uint2 w = *reinterpret_cast<const uint2*>(a.am + ((int64_t)(b * a.Ho + oh) * a.Wo + ow) * a.C + cg * 8);
-            float g[8];
-            gsum8(a.g, 0, (int64_t)(b * a.Ho + oh) * a.Wo + ow, cg * 8, g);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if ((int)(((j < 4 ? w.x : w.y) >> (8 * (j & 3))) & 255u) == me) acc[j] += g[j];
-            continue;
-          }
           float mx[8];
           int am[8];
 #pragma unroll
@@ -155,26 +205,42 @@ __global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {
           for (int j = 0; j < 8; ++j) if (am[j] == me) acc[j] += g[j];
         }
     } else {
-      for (int oh = max(0, ih - 1); oh <= min(a.Ho - 1, ih + 1); ++oh)
-        for (int ow = max(0, iw - 1); ow <= min(a.Wo - 1, iw + 1); ++ow) {
-          float g[8];
-          gsum8(a.g, 0, (int64_t)(b * a.Ho + oh) * a.Wo + ow, cg * 8, g);
+      // average pool, stride 1, padding 1: the output windows oh in [ih-1, ih+1], ow in [iw-1, iw+1]
+      for (int sidx = 0; sidx < a.g.n; ++sidx) {
+        const float* gp = a.g.p[sidx];
+        const int ld = a.g.ld[sidx];
+        float4 g0[9], g1[9];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] += g[j] * (1.f / 9.f);
+        for (int t = 0; t < 9; ++t) {
+          const int oh = ih - 1 + t / 3, ow = iw - 1 + t % 3;
+          const bool ok = oh >= 0 && oh < a.Ho && ow >= 0 && ow < a.Wo;
+          const float* src = gp + (int64_t)((b * a.Ho + oh) * a.Wo + ow) * ld + cg * 8;
+          g0[t] = ok ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
+          g1[t] = ok ? *reinterpret_cast<const float4*>(src + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          acc[0] += g0[t].x; acc[1] += g0[t].y; acc[2] += g0[t].z; acc[3] += g0[t].w;
+          acc[4] += g1[t].x; acc[5] += g1[t].y; acc[6] += g1[t].z; acc[7] += g1[t].w;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
     }
-    store8f(a.dx + p * a.lddx + cg * 8, acc);
+    store8f(a.dx + (int64_t)p * a.lddx + cg * 8, acc);
   }
 }
 
 int launch_pool3(int is_max, int backward, const PoolArgs& a, hipStream_t st) {
   const int64_t n = (int64_t)a.B * (backward ? a.H * a.W : a.Ho * a.Wo) * (a.C / 8);
+  if (n >= (1ll << 31) || a.C % 8) return -2;  // 32-bit index math in the kernels, 8-channel groups
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
   if (!backward) {
     if (is_max) hipLaunchKernelGGL(pool3_fwd_kernel<1>, dim3(blocks), dim3(256), 0, st, a);
     else hipLaunchKernelGGL(pool3_fwd_kernel<0>, dim3(blocks), dim3(256), 0, st, a);
   } else {
-    if (is_max) hipLaunchKernelGGL(pool3_bwd_kernel<1>, dim3(blocks), dim3(256), 0, st, a);
+    if (is_max && a.am) hipLaunchKernelGGL(pool3_bwd_kernel<1>, dim3(blocks), dim3(256), 0, st, a);
+    else if (is_max) hipLaunchKernelGGL(pool3_bwd_kernel<2>, dim3(blocks), dim3(256), 0, st, a);
     else hipLaunchKernelGGL(pool3_bwd_kernel<0>, dim3(blocks), dim3(256), 0, st, a);
   }
   return (int)hipGetLastError();
