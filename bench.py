@@ -56,9 +56,12 @@ def main():
                     help="DP gradient buckets overlapped with the backward (default: the model's, 1 on one GPU)")
     ap.add_argument("--heldout", type=int, default=1024, help="held-out samples per GPU evaluated after timing")
     ap.add_argument("--no-tune", action="store_true", help="skip per-layer kernel autotuning (cached table only)")
+    ap.add_argument("--in_channels", type=int, default=1,
+                    help="input channels of the synthetic DAS matrices (reference 1; BASELINE north star 2)")
     args = ap.parse_args()
 
     import torch
+    import torch.distributed as dist
     from mtl_das_pytorch_amd.data.synthetic import generate
     from mtl_das_pytorch_amd.engine.inception import InceptionProgram
     from mtl_das_pytorch_amd.engine.mtl import MTLProgram
@@ -68,13 +71,15 @@ def main():
     from mtl_das_pytorch_amd.parallel.dist import (FlatGradAllReducer, ShardedIndexSampler,
                                                    broadcast_module_state, init_distributed, shutdown)
 
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws != args.gpus:  # fail before touching the GPU: a mislaunch would report the wrong n_gpus
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}; launch one rank per GPU with "
+                 f"torch.distributed.run --nproc-per-node {args.gpus}")
     ctx = init_distributed()
     world = ctx.world
-    if world != args.gpus and ctx.is_main:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting WORLD_SIZE", file=sys.stderr)
     dev = ctx.device
     torch.manual_seed(1234)  # identical init on every rank (then broadcast for certainty)
-    model = build_model(args.model)
+    model = build_model(args.model, in_channels=args.in_channels)
     joint = args.model == "multi_classifier"
     prog = InceptionProgram(model, args.batch, dev) if joint else MTLProgram(model, args.batch, dev)
     prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world)
@@ -88,10 +93,10 @@ def main():
                      measure=not args.no_tune)
     f = prog.flat
     broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
-    X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev)
+    X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev, in_channels=args.in_channels)
     labels = encode_joint(d, e) if joint else torch.stack([d, e], 1)
     runner = StepRunner(prog, X, labels, use_graph=not args.no_graph,
-                        allreduce=FlatGradAllReducer(ctx) if (world > 1 or len(buckets) > 1) else None)
+                        allreduce=FlatGradAllReducer(ctx) if (ctx.enabled or len(buckets) > 1) else None)
     runner.set_lr(1e-3 / 1.5)  # reference: lr/1.5 applied at the epoch-0 validation
     sampler = ShardedIndexSampler(args.dataset_size * world, args.batch, ctx, seed=7)
     # indices address this rank's resident shard
@@ -119,7 +124,7 @@ def main():
     # "event-cls accuracy" half) on samples no rank trained on, BN in eval mode (running statistics)
     mh = None
     if args.heldout >= args.batch:
-        Xh, dh, eh = generate(args.heldout, seed=500000 + ctx.rank, device=dev)
+        Xh, dh, eh = generate(args.heldout, seed=500000 + ctx.rank, device=dev, in_channels=args.in_channels)
         runner.set_eval_source(Xh, encode_joint(dh, eh) if joint else torch.stack([dh, eh], 1))
         runner.reset_metrics()
         for i in range(0, args.heldout - args.batch + 1, args.batch):
@@ -139,19 +144,23 @@ def main():
         "scaling": "weak",
         "vs_baseline": round(value / BASELINE_VALUE, 3),
         "dtype": "bf16",
-        "data": "synthetic (DAS time-space matrices 1x100x250 from the on-device generator, HBM-resident, "
-                "random-init weights)",
+        "data": f"synthetic (DAS time-space matrices {args.in_channels}x100x250 from the on-device generator, "
+                "HBM-resident, random-init weights)",
         "config": {"model": MODEL_NAMES.get(args.model, args.model),
-                   "global_batch": args.batch * world, "seq_len": 250, "input_shape": [1, 100, 250],
+                   "global_batch": args.batch * world, "seq_len": 250, "input_shape": [args.in_channels, 100, 250],
                    "parallelism": f"dp{world}"},
         "train_acc_timed_steps": _accs(m, joint),
         "heldout_acc_after_timed_steps": _accs(mh, joint) if mh is not None else None,
+        "heldout_note": "held-out accuracy after only warmup + timed steps of training (near initialisation), "
+                        "not a converged accuracy; converged numbers: docs/ACCURACY.md",
         "heldout_samples": (args.heldout // args.batch) * args.batch * world,
         "train_steps_before_heldout": args.warmup + args.steps,
         "vs_eager_pytorch_mi355x": (round(value / (EAGER_BY_MODEL[args.model] * world), 3)
                                     if args.model in EAGER_BY_MODEL else None),
         "hip_graph": not args.no_graph,
         "grad_buckets_mb": [round((hi - lo) * 4 / 2 ** 20, 2) for lo, hi in buckets],
+        "dist_backend": ctx.backend,
+        "rccl_ranks": dist.get_world_size() if ctx.backend == "nccl" else 0,
         "baseline_note": "vs_baseline divides by BASELINE.md's 176.1 samples/s (reference on CPU, the only "
                          "throughput number it has); vs_eager_pytorch_mi355x divides by the reference-style "
                          "eager fp32 PyTorch step of the same model measured on MI355X (A: 4037 samples/s/GPU)",

@@ -88,25 +88,6 @@ BNArgs parse_bn(const py::dict& d) {
   return b;
 }
 
-// Apply-on-load of a BN-tail backward (ConvArgs::ao / WgradArgs::ao); C = the dy channel count.
-AolArgs parse_aol(const py::dict& o, int C, bool dgrad) {
-  AolArgs r{};
-  r.g = P<const float>(o, "g"); r.ggs = I(o, "ggs"); r.ldg = (int)I(o, "ldg");
-  r.y = P<const bf16_t>(o, "y"); r.ygs = I(o, "ygs"); r.ldy = (int)I(o, "ldy");
-  r.coef = P<float>(o, "coef");
-  r.kind = (int)I(o, "kind");
-  if (dgrad) {
-    r.bn = parse_bn(o["bn"].cast<py::dict>());
-    r.part = P<const double>(o, "part");
-    r.dgamma = P<float>(o, "dgamma"); r.dbeta = P<float>(o, "dbeta"); r.pgs = I(o, "pgs");
-    if (!r.part || !r.bn.gamma || r.bn.C != C || !r.bn.training) throw std::runtime_error("bad apply-on-load BN arguments");
-  }
-  if (!r.g || !r.y || !r.coef || r.ldg % 8 || r.ldy % 8 || r.ggs % 8 || r.ygs % 8 ||
-      (r.kind != ACT_NONE && r.kind != ACT_RELU))
-    throw std::runtime_error("bad apply-on-load arguments");
-  return r;
-}
-
 ConvArgs parse_conv(int mode, py::dict d);
 
 void conv(int mode, int cfg, int G, int64_t stream, py::dict d) {
@@ -119,8 +100,8 @@ py::tuple conv_workspace(int mode, int cfg, int G, py::dict d) {
   ConvArgs a = parse_conv(mode, d);
   int64_t ws = 0, nt = 0;
   int rc = 0;
-  if (cfg >= CONV_DEEP_CFG0) rc = (cfg < CONV_DEEP_CFG0 + CONV_DEEP_NCFG && !(mode != MODE_FWD && a.aol)) ? 0 : -1;
-  else if (cfg >= CONV_LDS_CFG0) rc = a.nr ? -1 : conv_lds_workspace(mode, a, G, cfg, ws, nt);
+  if (cfg >= CONV_DEEP_CFG0) rc = cfg < CONV_DEEP_CFG0 + CONV_DEEP_NCFG ? 0 : -1;
+  else if (cfg >= CONV_LDS_CFG0) rc = conv_lds_workspace(mode, a, G, cfg, ws, nt);
   return py::make_tuple(rc, ws, nt);
 }
 
@@ -165,21 +146,9 @@ ConvArgs parse_conv(int mode, py::dict d) {
     a.nbn = parse_bn(n["bn"].cast<py::dict>());
     a.nol = 1;
     a.nol_kind = (int)I(n, "kind");
-    if (a.nol_kind == ADD_RELU) {  // residual-on-load
-      py::dict r = n["r"].cast<py::dict>();
-      a.nr = P<const bf16_t>(r, "p"); a.nrgs = I(r, "gs"); a.ldnr = (int)I(r, "ld");
-      if (n.contains("bn2") && !n["bn2"].is_none()) { a.nbn2 = parse_bn(n["bn2"].cast<py::dict>()); a.nr_bn = 1; }
-      if (!a.nr || a.ldnr % 8 || (a.nr_bn && a.nbn2.C != a.Cs))
-        throw std::runtime_error("conv: bad residual-on-load arguments");
-    }
     if (mode != MODE_FWD || a.src.C1 != 0 || a.nbn.C != a.Cs ||
-        (a.nol_kind != ACT_NONE && a.nol_kind != ACT_RELU && a.nol_kind != ADD_RELU) || (a.nbn.training && !a.nbn.stats))
+        (a.nol_kind != ACT_NONE && a.nol_kind != ACT_RELU) || (a.nbn.training && !a.nbn.stats))
       throw std::runtime_error("conv: bad normalise-on-load arguments");
-  }
-  if (d.contains("aol") && !d["aol"].is_none()) {  // dgrad: dy operand = BN-tail backward applied on load
-    if (mode != MODE_DGRAD || a.src.C1 != 0) throw std::runtime_error("conv: apply-on-load needs a one-segment dgrad");
-    a.ao = parse_aol(d["aol"].cast<py::dict>(), a.Cs, true);
-    a.aol = 1;
   }
   a.ws = P<float>(d, "ws");
   a.cnt = P<unsigned>(d, "cnt");
@@ -194,15 +163,12 @@ void wgrad(int cfg, int G, int64_t stream, py::dict d) {
 
 // Packs the WgradJob table of a batched weight-gradient launch; returns (bytes, total blocks).
 py::tuple wgrad_table(int cfg, py::list dicts, py::list groups) {
-  const bool aol = cfg >= WGRAD_AOL_CFG;  // the AOL instantiation: every job must apply on load
-  if (aol) cfg -= WGRAD_AOL_CFG;
   std::vector<WgradJob> jobs(dicts.size());
   int64_t b0 = 0;
   for (size_t i = 0; i < jobs.size(); ++i) {
     WgradJob& j = jobs[i];
     j = WgradJob{};
     j.a = parse_wgrad(dicts[i].cast<py::dict>());
-    if ((j.a.aol != 0) != aol) throw std::runtime_error("wgrad_table: apply-on-load jobs need the AOL cfg and vice versa");
     j.G = groups[i].cast<int>();
     j.ntiles = wgrad_ntiles(cfg, j.a);
     if (j.ntiles < 0) throw std::runtime_error("wgrad_table: cfg " + std::to_string(cfg) + " invalid for job " + std::to_string(i));
@@ -238,10 +204,6 @@ WgradArgs parse_wgrad(const py::dict& d) {
     if (!a.nol_consts || a.src.C1 != 0 || (a.nol_kind != ACT_NONE && a.nol_kind != ACT_RELU))
       throw std::runtime_error("wgrad: bad normalise-on-load arguments");
   }
-  if (d.contains("aol") && !d["aol"].is_none()) {
-    a.ao = parse_aol(d["aol"].cast<py::dict>(), a.Co, false);
-    a.aol = 1;
-  }
   return a;
 }
 
@@ -269,17 +231,6 @@ TailArgs parse_tail(const py::dict& d) {
   a.pgs = I(d, "pgs");
   a.gscale = (float)F(d, "gscale", 1.0);
   a.tsc = P<uint64_t>(d, "tsc");
-  if (d.contains("prev") && !d["prev"].is_none()) {  // apply pass: partial statistics of the previous tail
-    py::dict q = d["prev"].cast<py::dict>();
-    a.py = P<const bf16_t>(q, "y"); a.ldpy = (int)I(q, "ldy");
-    a.pr = P<const bf16_t>(q, "r"); a.ldpr = (int)I(q, "ldr");
-    a.pbn = parse_bn(q["bn"].cast<py::dict>());
-    if (q.contains("bn2") && !q["bn2"].is_none()) { a.pbn2 = parse_bn(q["bn2"].cast<py::dict>()); a.pr_bn = 1; }
-    a.pkind = (int)I(q, "kind");
-    a.ppart = P<double>(q, "part");
-    if (!a.ppart || a.pbn.C != a.C || (a.pr_bn && a.pbn2.C != a.C) || a.ldpy % 8 || a.ldpr % 8)
-      throw std::runtime_error("tail: bad previous-tail statistics arguments");
-  }
   if (a.C % 8 || a.C > 2048) throw std::runtime_error("tail: C must be a multiple of 8 and <= 2048");
   return a;
 }
@@ -367,8 +318,6 @@ void adam_pack(int64_t stream, py::dict d) {
   a.b1 = (float)F(d, "b1", 0.9); a.b2 = (float)F(d, "b2", 0.999); a.eps = (float)F(d, "eps", 1e-8);
   a.wd = (float)F(d, "wd", 0.0); a.grad_scale = (float)F(d, "grad_scale", 1.0);
   a.update = (int)I(d, "update", 1);
-  a.ticket = P<unsigned>(d, "ticket");
-  a.fused = (int)I(d, "fused", 0);
   check(launch_adam_pack(a, P<const OptSeg>(d, "segs"), (int)I(d, "nsegs"), I(d, "nblocks"), S(stream)), "adam_pack");
 }
 

@@ -145,11 +145,6 @@ DEV void tail_fwd_impl(const TailArgs& a) {
 template <int KIND>
 __global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) { tail_fwd_impl<KIND>(a); }
 
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-
 // ------------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------------
@@ -340,29 +335,16 @@ DEV void bnb_reduce_impl(const TailArgs& a) {
   }
 }
 
-// PREV (ADD_RELU with identity shortcut, apply-only backward): the side output dz is also a gradient
-// source of the previous tail (TailArgs::ppart); its partial statistics are accumulated here, so that tail
-// needs no reduce pass of its own over this source.
-template <int KIND, int CGB, bool PREV>
+template <int KIND, int CGB>
 DEV void bnb_apply_impl(const TailArgs& a) {
   constexpr int PL = BNB_T / CGB, CB = 8 * CGB;
   __shared__ float s_x[2][5][CB];
   __shared__ float s_red[BNB_T];
   __shared__ float s_coef[2][3][CB];
-  __shared__ float s_p[PREV ? 8 : 1][CB];              // previous tail: BN, BN2 (scale, shift, mean, invstd)
-  __shared__ float s_pp[PREV ? 16 : 1][3][CB];         // its partial sums per 16-lane row
   const int z = blockIdx.z, chunk = blockIdx.x;
   const int cgl = threadIdx.x % CGB, pl = threadIdx.x / CGB;
   const int cblk = blockIdx.y * CB, c = cblk + cgl * 8;
   constexpr bool two = KIND == ADD_RELU2;
-  if (PREV) {
-    for (int t = threadIdx.x; t < 2 * CB; t += BNB_T) {
-      const int k = t / CB, j = t - k * CB;
-      float sc = 0.f, sh = 0.f, mu = 0.f, inv = 0.f;
-      if (k == 0 || a.pr_bn) bn_channel_bwd(k ? a.pbn2 : a.pbn, 0, cblk + j, sc, sh, mu, inv);
-      s_p[4 * k][j] = sc; s_p[4 * k + 1][j] = sh; s_p[4 * k + 2][j] = mu; s_p[4 * k + 3][j] = inv;
-    }
-  }
   BwdCtx X;
   bnb_ctx<KIND, CGB>(a, z, cblk, cgl, X, s_x);
   // the NREP replicas of this block's channels: item = (stat, channel), Q threads per item
@@ -412,9 +394,6 @@ DEV void bnb_apply_impl(const TailArgs& a) {
   const int p0 = chunk * a.chunk_px, p1 = min(M, p0 + a.chunk_px);
   const bf16_t* yz = a.y + a.ygs * z;
   const float* dzz = a.dzbuf ? a.dzbuf + a.dzgs * z : nullptr;
-  float q0[8], q1[8], q2[8];  // PREV partial sums
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { q0[j] = 0.f; q1[j] = 0.f; q2[j] = 0.f; }
   for (int p = p0 + pl; p < p1; p += PL) {
     float dz[8], y[8], o[8];
     if (dzz) {
@@ -424,24 +403,6 @@ DEV void bnb_apply_impl(const TailArgs& a) {
       compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
       if ((KIND == SIGMUL || KIND == ADD_RELU) && a.side && a.apply_side)
         store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
-      if (PREV) {  // side (= dz, identity shortcut) through the previous tail's activation derivative
-        float pyv[8], prv[8];
-        load8(a.py + (int64_t)p * a.ldpy + c, pyv);
-        if (a.pkind == ADD_RELU) load8(a.pr + (int64_t)p * a.ldpr + c, prv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int q = cgl * 8 + j;
-          const float t = pyv[j] * s_p[0][q] + s_p[1][q];
-          float f = 0.f, x2 = 0.f;
-          if (a.pkind == ADD_RELU) {
-            f = prv[j];
-            if (a.pr_bn) { x2 = (f - s_p[6][q]) * s_p[7][q]; f = f * s_p[4][q] + s_p[5][q]; }
-          }
-          const float d = (t + f) > 0.f ? side[j] : 0.f;
-          const float x1 = (pyv[j] - s_p[2][q]) * s_p[3][q];
-          q0[j] += d; q1[j] += d * x1; q2[j] += d * x2;
-        }
-      }
     }
     load8(yz + (int64_t)p * a.ldy + c, y);
 #pragma unroll
@@ -455,28 +416,10 @@ DEV void bnb_apply_impl(const TailArgs& a) {
       store8(a.dy2 + a.d2gs * z + (int64_t)p * a.ldd2 + c, o);
     }
   }
-  if (PREV) {  // block reduction of the previous tail's partial sums -> fp64 replica chunk % NREP
-    const int lane = threadIdx.x & 63, row = threadIdx.x >> 4;
-    const bool top = (lane & 15) >= 16 - CGB;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float t0 = row_stride_sum<CGB>(q0[j]), t1 = row_stride_sum<CGB>(q1[j]), t2 = row_stride_sum<CGB>(q2[j]);
-      if (top) { s_pp[row][0][cgl * 8 + j] = t0; s_pp[row][1][cgl * 8 + j] = t1; s_pp[row][2][cgl * 8 + j] = t2; }
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < 3 * CB; t += BNB_T) {
-      const int k = t / CB, q = t - k * CB;
-      if (k == 2 && !a.pr_bn) continue;
-      float v = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v += s_pp[r][k][q];
-      atomicAdd(a.ppart + ((int64_t)(chunk % a.pbn.pnrep) * 3 + k) * a.C + cblk + q, (double)v);
-    }
-  }
 }
 
 // Kernels: plain, and with the register budget of 5 waves per SIMD (<= 96 VGPRs) for the kinds that fit it
-// without spilling (every kind but the two-BN residual tail and the pooling tail; the PREV apply spills).
+// without spilling (every kind but the two-BN residual tail and the pooling tail).
 // These passes are latency-bound, and occupancy is what hides the latency (measured: forward tails at 4
 // instead of 6 waves per SIMD cost Model A 150 us per step).
 template <int KIND, int CGB>
@@ -485,11 +428,11 @@ template <int KIND, int CGB, int W>
 __global__ __launch_bounds__(BNB_T) __attribute__((amdgpu_waves_per_eu(W))) void bnb_reduce_kernel_w(TailArgs a) {
   bnb_reduce_impl<KIND, CGB>(a);
 }
-template <int KIND, int CGB, bool PREV>
-__global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) { bnb_apply_impl<KIND, CGB, PREV>(a); }
+template <int KIND, int CGB>
+__global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) { bnb_apply_impl<KIND, CGB>(a); }
 template <int KIND, int CGB, int W>
 __global__ __launch_bounds__(BNB_T) __attribute__((amdgpu_waves_per_eu(W))) void bnb_apply_kernel_w(TailArgs a) {
-  bnb_apply_impl<KIND, CGB, false>(a);
+  bnb_apply_impl<KIND, CGB>(a);
 }
 // waves per SIMD each kind's passes fit without spilling (hipcc -Rpass-analysis=kernel-resource-usage, gfx950);
 // 0 = the compiler's default allocation
@@ -621,9 +564,6 @@ int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t 
 int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, hipStream_t st) {
   if (fused == 2 && a.dzbuf) return -5;  // apply-only recomputes dz from the sources (every kind)
   if (fused == 3 && (a.dzbuf || a.dy || a.side || a.dgamma || a.dbeta)) return -5;
-  if (a.ppart && (kind != ADD_RELU || a.r_bn || G != 1 || !a.side || fused != 2 || !a.py ||
-                  (a.pkind != ADD_RELU && a.pkind != ACT_RELU) || (a.pkind == ADD_RELU && !a.pr)))
-    return -6;
   TailArgs b = a;
   b.apply_side = fused == 2;
   const int kk = (kind == ADD_RELU && a.r_bn) ? ADD_RELU2 : kind;  // kernel kind
@@ -651,32 +591,19 @@ int launch_tail_bwd(int kind, const TailArgs& a, int G, int nchunk, int fused, h
   }
   if (!a.part || a.chunk_px <= 0 || nchunk <= 0) return -4;
   const int cgb = bnb_cgb(a.C);
-  static const int bw = env_int("MDA_BNB_WAVES", 1);  // per-kind register budgets (occupancy experiment)
   dim3 grid(nchunk, a.C / (8 * cgb), G);
 #define KC(X, CG)                                                                                    \
   if (fused != 2) {                                                                                  \
-    bool done = false;                                                                               \
-    if constexpr (bnb_waves<X>() > 0) {                                                              \
-      if (bw) {                                                                                      \
-        hipLaunchKernelGGL((bnb_reduce_kernel_w<X, CG, bnb_waves<X>()>), grid, dim3(BNB_T), 0, st, b); \
-        done = true;                                                                                 \
-      }                                                                                              \
-    }                                                                                                \
-    if (!done) hipLaunchKernelGGL((bnb_reduce_kernel<X, CG>), grid, dim3(BNB_T), 0, st, b);           \
+    if constexpr (bnb_waves<X>() > 0)                                                                \
+      hipLaunchKernelGGL((bnb_reduce_kernel_w<X, CG, bnb_waves<X>()>), grid, dim3(BNB_T), 0, st, b); \
+    else                                                                                             \
+      hipLaunchKernelGGL((bnb_reduce_kernel<X, CG>), grid, dim3(BNB_T), 0, st, b);                   \
   }                                                                                                  \
   if (fused == 3) break;                                                                             \
-  if (X == ADD_RELU && b.ppart) {                                                                    \
-    hipLaunchKernelGGL((bnb_apply_kernel<X, CG, (X == ADD_RELU)>), grid, dim3(BNB_T), 0, st, b);     \
-  } else {                                                                                           \
-    bool done = false;                                                                               \
-    if constexpr (bnb_waves<X>() > 0) {                                                              \
-      if (bw) {                                                                                      \
-        hipLaunchKernelGGL((bnb_apply_kernel_w<X, CG, bnb_waves<X>()>), grid, dim3(BNB_T), 0, st, b); \
-        done = true;                                                                                 \
-      }                                                                                              \
-    }                                                                                                \
-    if (!done) hipLaunchKernelGGL((bnb_apply_kernel<X, CG, false>), grid, dim3(BNB_T), 0, st, b);    \
-  }
+  if constexpr (bnb_waves<X>() > 0)                                                                  \
+    hipLaunchKernelGGL((bnb_apply_kernel_w<X, CG, bnb_waves<X>()>), grid, dim3(BNB_T), 0, st, b);    \
+  else                                                                                               \
+    hipLaunchKernelGGL((bnb_apply_kernel<X, CG>), grid, dim3(BNB_T), 0, st, b);
 #define K(X)                                                   \
   case X:                                                      \
     if (cgb == 1) { KC(X, 1) } else if (cgb == 2) { KC(X, 2) } \

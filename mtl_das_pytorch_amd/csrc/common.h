@@ -27,20 +27,6 @@ typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t bf16_t;  // raw bf16 storage
 
-// Logical block index with XCD locality for streaming kernels whose neighbouring blocks share cache lines:
-// the dispatcher hands consecutive workgroups round-robin to the 8 XCDs (each with its own L2); with
-// remapping, XCD x runs the contiguous logical range [x * n/8, (x + 1) * n/8).  Blocks past the last
-// multiple of 8 keep their index.  remap == 0 returns bid unchanged.  Opt-in (MDA_XCD_REMAP=1): measured
-// slower on wgrad_finalize (C 105.6 -> 109.6 us) and the pack (62.2 -> 66.9 us).
-inline int env_flag(const char* name, int dflt) {  // host: integer environment switch
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-DEV int xcd_block(int bid, int nblocks, int remap) {
-  const int per = nblocks >> 3;
-  if (!remap || bid >= per * 8) return bid;
-  return (bid & 7) * per + (bid >> 3);
-}
 DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 // round-to-nearest-even; NaN-preserving via the hardware conversion
 DEV bf16_t f2bf(float f) {

@@ -39,41 +39,9 @@ DEV int encode_kg(int i, int Ktot, int Cs8, int KW, int C0) {
 }
 
 template <int MODE>
-constexpr bool is_fwd() { return MODE == MODE_FWD || MODE == MODE_FWD_NOL || MODE == MODE_FWD_ROL; }
+constexpr bool is_fwd() { return MODE == MODE_FWD || MODE == MODE_FWD_NOL; }
 template <int MODE>
-constexpr bool has_aol() { return MODE == MODE_DGRAD_AOL || MODE == MODE_DGRAD_AOL_BNS; }
-template <int MODE>
-constexpr bool has_bns() { return MODE == MODE_DGRAD_BNS || MODE == MODE_DGRAD_AOL_BNS; }
-
-// Apply-on-load of a BN-tail backward: from the tail's fp32 upstream gradient g and pre-BN y (8 channels
-// [c, c+8) of each real fragment), dy = A*dz + B*y + C with dz = g * act'(y*scale + shift), rounded to bf16
-// exactly as the tail's apply pass stored it; padding fragments are zero.  s_aol = [5][C]: A, B, C, scale,
-// shift per channel.
-template <int FM>
-DEV void aol_apply(bf16x8* bfr, const float4 (*gq)[2], const uint4* yq, uint32_t okm, int c, const float* s_aol,
-                   int C, bool relu) {
-  const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
-  float A[8], Bc[8], Cc[8], sc[8], sh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    A[j] = s_aol[c + j]; Bc[j] = s_aol[C + c + j]; Cc[j] = s_aol[2 * C + c + j];
-    sc[j] = s_aol[3 * C + c + j]; sh[j] = s_aol[4 * C + c + j];
-  }
-#pragma unroll
-  for (int f = 0; f < FM; ++f) {
-    if (!((okm >> f) & 1)) { bfr[f] = zero8; continue; }
-    const uint32_t w[4] = {yq[f].x, yq[f].y, yq[f].z, yq[f].w};
-    const float g[8] = {gq[f][0].x, gq[f][0].y, gq[f][0].z, gq[f][0].w, gq[f][1].x, gq[f][1].y, gq[f][1].z, gq[f][1].w};
-    bf16x8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float y = __uint_as_float((j & 1) ? (w[j >> 1] & 0xffff0000u) : (w[j >> 1] << 16));
-      const float dz = relu ? ((y * sc[j] + sh[j]) > 0.f ? g[j] : 0.f) : g[j];
-      v[j] = (short)f2bf(A[j] * dz + Bc[j] * y + Cc[j]);
-    }
-    bfr[f] = v;
-  }
-}
+constexpr bool has_bns() { return MODE == MODE_DGRAD_BNS; }
 
 // Normalise-on-load: the 8 channels [c, c+8) of an im2col fragment are pre-BN conv outputs y; the operand
 // is act(y * scale + shift) (act = ReLU or identity), rounded to bf16 exactly as the BN tail that used to
@@ -107,34 +75,13 @@ DEV void nol_apply(bf16x8* bfr, uint32_t okm, const float* k, bool relu) {
   }
 }
 
-// Residual-on-load: operand = relu(y * scale + shift + r'), r' = r or r * scale2 + shift2 -- the exact
-// expression (and rounding) of the ADD_RELU tail that materialises the residual block's output.
-// s_nol = [4][Cs]: scale, shift, scale2, shift2.
-template <int FM>
-DEV void rol_apply(bf16x8* bfr, const bf16x8* rq, uint32_t okm, int c, const float* s_nol, int Cs, bool r_bn) {
-#pragma unroll
-  for (int f = 0; f < FM; ++f) {
-    if (!((okm >> f) & 1)) continue;
-    bf16x8 v = bfr[f];
-    const bf16x8 r = rq[f];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float x = __uint_as_float(((uint32_t)(uint16_t)v[j]) << 16) * s_nol[c + j] + s_nol[Cs + c + j];
-      float rr = __uint_as_float(((uint32_t)(uint16_t)r[j]) << 16);
-      if (r_bn) rr = rr * s_nol[2 * Cs + c + j] + s_nol[3 * Cs + c + j];
-      v[j] = (short)f2bf(fmaxf(x + rr, 0.f));
-    }
-    bfr[f] = v;
-  }
-}
-
 // One wave's fragment loads for k-step `ks`: FM im2col fragments (B operand) + FN weight fragments (A).
 // okm / cch: which im2col fragments hold real (not padding) data and their first channel (for NOL).
 template <int MODE, int FN, int FM>
 DEV void conv_load_stage(const ConvArgs& a, const int* s_tab, int ks, int kgl, int l16, int n_base,
                          const int* pb, const int* py, const int* px, const bool* pv, const bf16_t* base0,
                          const bf16_t* base1, int ld0, int ld1, const bf16_t* wz, bf16x8* afr, bf16x8* bfr,
-                         uint32_t& okm, int& cch, float4 (*gq)[2], uint4* yq, bf16x8* rq, int z) {
+                         uint32_t& okm, int& cch) {
   const bf16x8 zero8 = {0, 0, 0, 0, 0, 0, 0, 0};
   const int e = s_tab[ks * 4 + kgl];
   const bool valid = (e >> 29) & 1;
@@ -158,25 +105,11 @@ DEV void conv_load_stage(const ConvArgs& a, const int* s_tab, int ks, int kgl, i
       if (a.sw == 2) { ok = ok && !(nw & 1); iw = nw >> 1; } else if (a.sw == 1) { iw = nw; } else { ok = ok && (nw % a.sw == 0); iw = nw / a.sw; }
       ok = ok && ih < a.Hs && iw < a.Ws;
     }
-    if (has_aol<MODE>()) {  // raw g / y of the tail; the transform runs when the stage is consumed
-      if (ok) {
-        const int64_t pix = (int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw;
-        const float* gp = a.ao.g + a.ao.ggs * z + pix * a.ao.ldg + c;
-        gq[f][0] = *reinterpret_cast<const float4*>(gp);
-        gq[f][1] = *reinterpret_cast<const float4*>(gp + 4);
-        yq[f] = *reinterpret_cast<const uint4*>(a.ao.y + a.ao.ygs * z + pix * a.ao.ldy + c);
-      }
-    } else {
-      // unconditional load from a valid address, zeroed after: no exec-masked branch around the load, so the
-      // waitcnt pass can count the loads of every pipeline stage exactly instead of draining with vmcnt(0)
-      const bf16_t* q = ok ? sb + ((int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw) * sld + c : sb;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(q);
-      bfr[f] = ok ? v : zero8;
-      if (MODE == MODE_FWD_ROL) {  // the residual r at the same pixel and channels
-        const int64_t pix = ok ? (int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw : 0;
-        rq[f] = *reinterpret_cast<const bf16x8*>(a.nr + a.nrgs * z + pix * a.ldnr + c);
-      }
-    }
+    // unconditional load from a valid address, zeroed after: no exec-masked branch around the load, so the
+    // waitcnt pass can count the loads of every pipeline stage exactly instead of draining with vmcnt(0)
+    const bf16_t* q = ok ? sb + ((int64_t)(pb[f] * a.Hs + ih) * a.Ws + iw) * sld + c : sb;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(q);
+    bfr[f] = ok ? v : zero8;
     okm |= (uint32_t)ok << f;
   }
 #pragma unroll
@@ -231,42 +164,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // LDS, and block (0, 0) of each group performs that BN's running-statistics update and publishes its
   // batch constants for the backward (the work of the forward tail this mode replaces)
   constexpr bool NOL = MODE == MODE_FWD_NOL;
-  constexpr bool ROL = MODE == MODE_FWD_ROL;
-  // (ROL: the block's tail still runs -- on another stream -- and owns the running-statistics update)
-  if (NOL || ROL) bn_prepare(a.nbn, z, s_nol, s_nol + a.Cs, nullptr, nullptr, NOL && blockIdx.x == 0 && blockIdx.y == 0);
-  if (ROL && a.nr_bn) bn_prepare(a.nbn2, z, s_nol + 2 * a.Cs, s_nol + 3 * a.Cs, nullptr, nullptr, false);
+  if (NOL) bn_prepare(a.nbn, z, s_nol, s_nol + a.Cs, nullptr, nullptr, blockIdx.x == 0 && blockIdx.y == 0);
   const bool nol_relu = a.nol_kind == ACT_RELU;
-  // MODE_DGRAD_AOL(_BNS): the dy operand is the BN-tail backward applied on load.  Per dy channel: the
-  // fused statistics (rows 0/1 of ao.part) and the BN constants give dy = A*dz + B*y + C; block (0, 0)
-  // writes d(gamma), d(beta) and the coefficient table the weight gradient uses.
-  constexpr bool AOL = has_aol<MODE>();
-  float* s_aol = s_bn + (want_bnb ? 8 * BN_T : 0);  // [5][Cs], after the fused-statistics constants
-  if (AOL) {
-    const AolArgs& o = a.ao;
-    const int C = a.Cs;
-    const bool first = blockIdx.x == 0 && blockIdx.y == 0;
-    for (int c = threadIdx.x; c < C; c += 256) {
-      const double* pp = o.part + (int64_t)z * NREP * 3 * C;
-      double sd = 0.0, sx = 0.0;
-#pragma unroll 8
-      for (int r = 0; r < o.bn.pnrep; ++r) { sd += pp[(r * 3) * C + c]; sx += pp[(r * 3 + 1) * C + c]; }
-      float sc, sh, mu, inv;
-      bn_channel_bwd(o.bn, z, c, sc, sh, mu, inv);
-      const float gam = o.bn.gamma[o.bn.pstride * z + c];
-      const float inv_n = 1.f / (float)o.bn.count;
-      const float mdz = (float)sd * inv_n, mdx = (float)sx * inv_n;
-      const float k[5] = {gam * inv, -gam * inv * inv * mdx, gam * inv * (mu * inv * mdx - mdz), sc, sh};
-#pragma unroll
-      for (int q = 0; q < 5; ++q) s_aol[q * C + c] = k[q];
-      if (first) {
-#pragma unroll
-        for (int q = 0; q < 5; ++q) o.coef[((int64_t)z * 5 + q) * C + c] = k[q];
-        if (o.dgamma) o.dgamma[o.pgs * z + c] = (float)sx;
-        if (o.dbeta) o.dbeta[o.pgs * z + c] = (float)sd;
-      }
-    }
-  }
-  const bool aol_relu = a.ao.kind == ACT_RELU;
   __syncthreads();
 
   // wave index through readfirstlane: the compiler then knows every K-loop bound and guard below is
@@ -332,20 +231,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   bf16x8 af[PD][FN], bq[PD][FM];
   uint32_t okq[PD];
   int ccq[PD];
-  constexpr int PG = AOL ? PD : 1;  // AOL raw stage data (eliminated in the other modes)
   float nk[NOL ? PD : 1][16];       // NOL: the stage's BN scale / shift
-  bf16x8 rqs[ROL ? PD : 1][FM];     // ROL: the stage's residual fragments
-  float4 gq[PG][FM][2];
-  uint4 yq[PG][FM];
 #define LOAD_STAGE(KS, J) do { \
   conv_load_stage<MODE, FN, FM>(a, s_tab, KS, kgl, l16, n_base, pb, py, px, pv, base0, base1, ld0, ld1, wz, af[J], bq[J], \
-                                okq[J], ccq[J], gq[AOL ? (J) : 0], yq[AOL ? (J) : 0], rqs[ROL ? (J) : 0], z); \
+                                okq[J], ccq[J]); \
   if (NOL) nol_fetch(nk[NOL ? (J) : 0], ccq[J], s_nol, a.Cs); } while (0)
-  // NOL / AOL: the operand transform runs when the stage is consumed, so the loads stay in flight meanwhile
+  // NOL: the operand transform runs when the stage is consumed, so the loads stay in flight meanwhile
 #define MMA_STAGE(J)                                                                                      \
   if (NOL) nol_apply<FM>(bq[J], okq[J], nk[NOL ? (J) : 0], nol_relu);                                     \
-  if (ROL) rol_apply<FM>(bq[J], rqs[ROL ? (J) : 0], okq[J], ccq[J], s_nol, a.Cs, a.nr_bn);                  \
-  if (AOL) aol_apply<FM>(bq[J], gq[AOL ? (J) : 0], yq[AOL ? (J) : 0], okq[J], ccq[J], s_aol, a.Cs, aol_relu); \
   _Pragma("unroll") for (int i = 0; i < FN; ++i)                                                          \
   _Pragma("unroll") for (int f = 0; f < FM; ++f)                                                          \
     acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[J][i], bq[J][f], acc[i][f], 0, 0, 0);
@@ -529,9 +422,7 @@ DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
 // Block: 256 threads, output tile TN (rows = cout) x TK (cols = k), MCH pixels staged per iteration.
 // Global loads of chunk c+1 are issued into registers before the MFMAs of chunk c (which read LDS), so
 // the load latency overlaps compute; one LDS image per operand, two barriers per chunk.
-// AOL: dy is the BN-tail backward applied on load (fp32 g + bf16 y of the tail, coefficient table written
-// by the same conv's dgrad), so the tail never materialises dy.
-template <int TN, int TK, int MCH, bool AOL>
+template <int TN, int TK, int MCH>
 DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const int z) {
   // Row pitch 16 x odd elements (TN + 16 for even multiples of 16): with the row permutation below the 32
   // lanes of one ds_read_b64_tr_b16 read rows 0-7 of a 16-row block, whose 8-bank windows then tile the 64
@@ -542,7 +433,6 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
   __shared__ __attribute__((aligned(16))) bf16_t s_x[MCH * LDX];
   __shared__ int s_tab[TK / 8];
   __shared__ float s_nsc[TK], s_nsh[TK];  // normalise-on-load constants of this tile's input channels
-  __shared__ float s_acf[AOL ? 5 * TN : 1];  // apply-on-load A, B, C, scale, shift of this tile's dy channels
   constexpr int FN = TN / 16, FK = TK / 16, NFR = FN * FK;
   constexpr int FPW = (NFR + 3) / 4;  // fragments per wave
   constexpr int VY = MCH * (TN / 8), VX = MCH * (TK / 8);
@@ -563,12 +453,6 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
     }
   }
 
-  if (AOL) {
-    for (int t = threadIdx.x; t < 5 * TN; t += 256) {
-      const int q = t / TN, n = n0 + t - q * TN;
-      s_acf[t] = n < a.Co ? a.ao.coef[((int64_t)z * 5 + q) * a.Co + n] : 0.f;
-    }
-  }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int HWo = a.Ho * a.Wo;
   const int M = a.B * HWo;
@@ -584,11 +468,9 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
   __syncthreads();
 
   uint4 ry[NY], rx[NX];
-  float4 rg[NY][2];  // AOL: the tail's upstream gradient (ry then holds its pre-BN y)
-  uint32_t rok = 0, ryok = 0;  // which rx hold real input (not zero padding); which ry are real rows (AOL)
+  uint32_t rok = 0;  // which rx hold real input (not zero padding)
   auto load_chunk = [&](int mc) {
     rok = 0;
-    ryok = 0;
 #pragma unroll
     for (int i = 0; i < NY; ++i) {
       const int v = threadIdx.x + 256 * i;
@@ -596,17 +478,7 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
       if (v < VY) {
         const int p = v / (TN / 8), cg = v - p * (TN / 8);
         const int m = mc + p, n = n0 + cg * 8;
-        if (m < mend && n < a.Co) {
-          if (AOL) {
-            const float* gp = a.ao.g + a.ao.ggs * z + (int64_t)m * a.ao.ldg + n;
-            rg[i][0] = *reinterpret_cast<const float4*>(gp);
-            rg[i][1] = *reinterpret_cast<const float4*>(gp + 4);
-            ry[i] = *reinterpret_cast<const uint4*>(a.ao.y + a.ao.ygs * z + (int64_t)m * a.ao.ldy + n);
-            ryok |= 1u << i;
-          } else {
-            ry[i] = *reinterpret_cast<const uint4*>(dyz + (int64_t)m * a.ldd + n);
-          }
-        }
+        if (m < mend && n < a.Co) ry[i] = *reinterpret_cast<const uint4*>(dyz + (int64_t)m * a.ldd + n);
       }
     }
 #pragma unroll
@@ -638,26 +510,7 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
       const int v = threadIdx.x + 256 * i;
       if (v < VY) {
         const int p = v / (TN / 8), cg = v - p * (TN / 8);
-        uint4 u = ry[i];
-        if (AOL && ((ryok >> i) & 1)) {
-          const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
-          const float g[8] = {rg[i][0].x, rg[i][0].y, rg[i][0].z, rg[i][0].w,
-                              rg[i][1].x, rg[i][1].y, rg[i][1].z, rg[i][1].w};
-          uint32_t o4[4];
-#pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            float d[2];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int j = cg * 8 + 2 * h + e;
-              const float y = __uint_as_float(e ? (w4[h] & 0xffff0000u) : (w4[h] << 16));
-              const float dz = (a.ao.kind == ACT_RELU && !(y * s_acf[3 * TN + j] + s_acf[4 * TN + j] > 0.f)) ? 0.f : g[2 * h + e];
-              d[e] = s_acf[j] * dz + s_acf[TN + j] * y + s_acf[2 * TN + j];
-            }
-            o4[h] = (uint32_t)f2bf(d[0]) | ((uint32_t)f2bf(d[1]) << 16);
-          }
-          u = make_uint4(o4[0], o4[1], o4[2], o4[3]);
-        }
+        const uint4 u = ry[i];
         *reinterpret_cast<uint4*>(&s_dy[p * LDY + cg * 8]) = u;
       }
     }
@@ -721,9 +574,9 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
   }
 }
 
-template <int TN, int TK, int MCH, bool AOL>
+template <int TN, int TK, int MCH>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
-  wgrad_block<TN, TK, MCH, AOL>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  wgrad_block<TN, TK, MCH>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Horizontally batched weight gradients: every conv of a backward pass that uses this tile config, in
@@ -731,7 +584,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 // the step ends, so all of them are deferred to the end of the backward pass; the ~40 (Model A) / ~90
 // (Model C) small launches become <= 8 large ones that fill the 256 CUs (the deep, small-M layers run
 // side by side instead of one after another).  Block -> job by binary search over the jobs' first blocks.
-template <int TN, int TK, int MCH, bool AOL>
+template <int TN, int TK, int MCH>
 __global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob* __restrict__ jobs, int nj) {
   int lo = 0, hi = nj - 1;
   while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
@@ -739,7 +592,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob*
   const int local = (int)((int64_t)blockIdx.x - J.block0);
   const int per_z = J.ntiles * J.a.splits;
   const int z = local / per_z, r = local - z * per_z;
-  wgrad_block<TN, TK, MCH, AOL>(J.a, r % J.ntiles, r / J.ntiles, z);
+  wgrad_block<TN, TK, MCH>(J.a, r % J.ntiles, r / J.ntiles, z);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -920,9 +773,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const Wgr
 //   the split reads are coalesced; lane q sums splits q, q + lanes, ... with 8 loads in flight and the
 //   lane partials are added in lane order through LDS -- deterministic.
 // Descriptors own whole blocks, so the mapping is uniform within a block.
-__global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale, int remap) {
+__global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale) {
   __shared__ float s_part[256];
-  const int bx = xcd_block((int)blockIdx.x, (int)gridDim.x, remap);
+  const int bx = (int)blockIdx.x;
   int lo = 0, hi = nd - 1;  // last descriptor with block0 <= bx
   while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (descs[mid].block0 <= (int64_t)bx) lo = mid; else hi = mid - 1; }
   const WgFinDesc& D = descs[lo];
@@ -1015,21 +868,18 @@ template <int MODE>
 static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
   const int M = a.B * a.Ho * a.Wo;
   const bool deep = cfg >= CONV_DEEP_CFG0;  // pipeline depth 4 (the same tile as cfg - CONV_DEEP_CFG0)
-  if (deep) {
-    if (has_aol<MODE>()) return -1;  // apply-on-load stages hold fp32 g + bf16 y: too many registers
-    cfg -= CONV_DEEP_CFG0;
-  }
+  if (deep) cfg -= CONV_DEEP_CFG0;
   const int nkg4 = ((a.Kpad / 8) + 3) & ~3;
 #define LAUNCH_CFG(WN, WM, WAN, WAM, KS)                                                                \
   if (!deep) LAUNCH_PD(WN, WM, WAN, WAM, KS, 2)                                                         \
-  else if constexpr (!has_aol<MODE>()) LAUNCH_PD(WN, WM, WAN, WAM, KS, 4)
+  else LAUNCH_PD(WN, WM, WAN, WAM, KS, 4)
 #define LAUNCH_PD(WN, WM, WAN, WAM, KS, PD)                                                             \
   {                                                                                                     \
     constexpr int TILE = (WN / 16) * (WM / 16) * 4 * 64;                                                \
     size_t red = (size_t)(KS - 1) * WAN * WAM * TILE;                                                   \
     size_t st2 = (size_t)WAM * WN * WAN * 3;                                                            \
     size_t lds = (size_t)nkg4 * 4 + (red > st2 ? red : st2) * 4 +                                        \
-                 (a.nol ? (a.nr ? 4 : 2) * a.Cs * 4 : (a.bpart ? 8 * WN * WAN * 4 : 0) + (a.aol ? 5 * a.Cs * 4 : 0)); \
+                 (a.nol ? 2 * a.Cs * 4 : (a.bpart ? 8 * WN * WAN * 4 : 0)); \
     dim3 grid((M + WM * WAM - 1) / (WM * WAM), (a.N + WN * WAN - 1) / (WN * WAN), G);                    \
     hipLaunchKernelGGL((conv_igemm_kernel<MODE, WN, WM, WAN, WAM, KS, PD>), grid, dim3(256), lds, st, a); \
   }
@@ -1057,16 +907,11 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
   if (cfg >= CONV_LDS_CFG0 && cfg < CONV_DEEP_CFG0) {  // LDS-staged kernels (conv_lds.hip)
-    if (a.nr) return -1;  // residual-on-load: register-pipelined kernels only
     const int m = mode == MODE_FWD ? (a.nol ? MODE_FWD_NOL : MODE_FWD) : (a.bpart ? MODE_DGRAD_BNS : MODE_DGRAD);
     return launch_conv_lds(m, a, G, cfg, st);
   }
-  if (mode == MODE_FWD) {
-    if (a.nol && a.nr) return launch_conv_cfg<MODE_FWD_ROL>(a, G, cfg, st);
+  if (mode == MODE_FWD)
     return a.nol ? launch_conv_cfg<MODE_FWD_NOL>(a, G, cfg, st) : launch_conv_cfg<MODE_FWD>(a, G, cfg, st);
-  }
-  if (a.aol)
-    return a.bpart ? launch_conv_cfg<MODE_DGRAD_AOL_BNS>(a, G, cfg, st) : launch_conv_cfg<MODE_DGRAD_AOL>(a, G, cfg, st);
   return a.bpart ? launch_conv_cfg<MODE_DGRAD_BNS>(a, G, cfg, st) : launch_conv_cfg<MODE_DGRAD>(a, G, cfg, st);
 }
 
@@ -1096,7 +941,7 @@ int wgrad_ntiles(int cfg, const WgradArgs& a) {
     const int Wo8 = (a.Wo + 7) & ~7;
     const bool seg_ok = a.src.C1 == 0 || a.src.C0 % CB == 0;
     if (a.KH != 3 || a.KW != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1 || a.Hi != a.Ho ||
-        a.Wi != a.Wo || a.Cs % CB || Wo8 > W8 || a.aol || !seg_ok || a.Kpad < 9 * a.Cs)
+        a.Wi != a.Wo || a.Cs % CB || Wo8 > W8 || !seg_ok || a.Kpad < 9 * a.Cs)
       return -2;
     return ((a.Npad + TN - 1) / TN) * (a.Cs / CB);
   }
@@ -1121,8 +966,7 @@ int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st) {
 #define LAUNCH_WG(TN, TK, MCH)                                                                      \
   {                                                                                                 \
     dim3 grid(((a.Npad + TN - 1) / TN) * (a.Kpad / TK), a.splits, G);                               \
-    if (a.aol) hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, MCH, true>), grid, dim3(256), 0, st, a); \
-    else hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, MCH, false>), grid, dim3(256), 0, st, a);      \
+    hipLaunchKernelGGL((conv_wgrad_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, a);                \
     break;                                                                                          \
   }
   int TN_, TK_;
@@ -1143,15 +987,10 @@ int wgrad_tile_shape(int cfg, int& TN, int& TK) {
   return 0;
 }
 
-// cfg >= WGRAD_AOL_CFG: the apply-on-load instantiation of tile config cfg - WGRAD_AOL_CFG (every job of
-// the table has aol set).
 int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st) {
   if (nblocks <= 0) return 0;
   dim3 grid((unsigned)nblocks);
-  const bool aol = cfg >= WGRAD_AOL_CFG;
-  if (aol) cfg -= WGRAD_AOL_CFG;
   if (cfg >= WGRAD_PATCH_CFG0) {
-    if (aol) return -2;
 #define LAUNCH_WGPB(TN, CB, W8)                                                                                 \
   hipLaunchKernelGGL((conv_wgrad_patch_batched_kernel<TN, CB, W8>), grid, dim3(256), 0, st, d_jobs, nj); \
   break;
@@ -1163,8 +1002,7 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
     return (int)hipGetLastError();
   }
 #define LAUNCH_WGB(TN, TK, MCH)                                                                              \
-  if (aol) hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH, true>), grid, dim3(256), 0, st, d_jobs, nj); \
-  else hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH, false>), grid, dim3(256), 0, st, d_jobs, nj); \
+  hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, d_jobs, nj); \
   break;
   switch (cfg) {
     WGRAD_CFG_CASES(LAUNCH_WGB)
@@ -1176,8 +1014,7 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
 
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st) {
   if (nblocks <= 0) return 0;
-  static const int remap = env_flag("MDA_XCD_REMAP", 0);
-  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, d_descs, nd, scale, remap);
+  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, d_descs, nd, scale);
   return (int)hipGetLastError();
 }
 

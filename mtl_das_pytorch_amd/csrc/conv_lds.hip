@@ -497,7 +497,6 @@ int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_
   LdsCfg c;
   int rc = decode_cfg(cfg, c);
   if (rc) return rc;
-  if (a.aol) return -2;
   LdsPlan pl;
   int gx;
   rc = make_plan(mode, a, c, pl, gx);
@@ -512,7 +511,6 @@ int launch_conv_lds(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st)
   LdsCfg c;
   int rc = decode_cfg(cfg, c);
   if (rc) return rc;
-  if (a.aol) return -2;  // apply-on-load dgrads (opt-in, conv.hip) are not staged here
   switch (mode) {
     case MODE_FWD: return launch_mode<MODE_FWD>(a, G, c, st);
     case MODE_FWD_NOL: return launch_mode<MODE_FWD_NOL>(a, G, c, st);

@@ -6,25 +6,8 @@
 
 namespace mda {
 
-// 2: dgrad + fused BN-backward statistics; 3: forward with normalise-on-load of its input;
-// 5: dgrad with apply-on-load of its dy operand; 6: both 2 and 5
-// 7: forward with residual-on-load (normalise-on-load of a residual block's output: relu(BN(y) + r'))
-enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD_BNS = 2, MODE_FWD_NOL = 3, MODE_DGRAD_AOL = 5, MODE_DGRAD_AOL_BNS = 6,
-       MODE_FWD_ROL = 7 };
-
-// Apply-on-load of a BN-tail backward (ACT_NONE / ACT_RELU): the conv operand dy = A*dz + B*y + C with
-// dz = g * act'(y * scale + shift) is computed from the tail's fp32 upstream gradient g and its pre-BN y
-// when loaded, so the tail's apply pass never runs.
-struct AolArgs {
-  const float* g; int64_t ggs; int ldg;     // upstream fp32 gradient of the tail output
-  const bf16_t* y; int64_t ygs; int ldy;    // the tail's pre-BN input
-  BNArgs bn;                                // its BN (constants from bn.consts)
-  const double* part;                       // [G][NREP][3][C] rows 0/1: sum dz, sum dz*xhat (fused stats)
-  float* coef;                              // [G][5][C] A, B, C, scale, shift: written by the dgrad's block
-                                            // (0, 0), read by the weight gradient
-  float* dgamma; float* dbeta; int64_t pgs; // written by the dgrad's block (0, 0)
-  int kind;
-};
+// 2: dgrad + fused BN-backward statistics; 3: forward with normalise-on-load of its input
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD_BNS = 2, MODE_FWD_NOL = 3 };
 
 struct ConvArgs {
   Src2 src;
@@ -66,15 +49,6 @@ struct ConvArgs {
   // group updates that BN's running statistics and publishes its constants (BNArgs::consts).
   BNArgs nbn;
   int nol, nol_kind;
-  // ... residual-on-load (nol_kind ADD_RELU, MODE_FWD_ROL): the input is a residual block's output
-  // relu(BN(y) + r'), r' = r (identity shortcut) or BN2(r) (projection, nr_bn = 1), computed on load from
-  // the block's pre-BN y (src) and r -- the block's ADD_RELU tail then runs off the critical stream
-  const bf16_t* nr; int64_t nrgs; int ldnr;
-  BNArgs nbn2;
-  int nr_bn;
-  // DGRAD only, optional (aol = 0 off): the dy operand is applied on load (AolArgs)
-  AolArgs ao;
-  int aol;
   // LDS-staged kernels (cfg >= CONV_LDS_CFG0, conv_lds.hip) with a cross-block split of K: fp32 partial
   // tiles [G][tiles][splits][BM*BN] and one arrival ticket per output tile (zero-initialised; the reducing
   // block resets it), sized by conv_lds_workspace
@@ -119,10 +93,6 @@ struct WgradArgs {
   // rebuilt the same way from the BN constants the forward published ([G][4][Cs]: scale, shift, ...)
   const float* nol_consts;
   int nol, nol_kind;
-  // optional (aol = 0 off): the dy operand is applied on load from ao.g / ao.y with the coefficient table
-  // ao.coef written by the matching dgrad
-  AolArgs ao;
-  int aol;
 };
 
 // One conv of a horizontally batched weight-gradient launch (device table, built by wgrad_table).
@@ -172,15 +142,6 @@ struct TailArgs {
   // the side output itself (apply_side)
   int apply_side;
   float gscale;                     // factor on the d(gamma), d(beta) the apply writes (SyncBN: 1 / world)
-  // apply pass, optional (ppart non-null, ADD_RELU with identity shortcut): the side output dz is also a
-  // gradient source of the PREVIOUS tail (the block input's own ACT_RELU / ADD_RELU tail, same pixel grid
-  // and channels): accumulate that tail's partial statistics sum(dz'), sum(dz' xhat'), sum(dz' xhat2')
-  // with dz' = side * relu'(BN(py) + pr') into ppart ([NREP][3][C], group 0)
-  const bf16_t* py; int ldpy;
-  const bf16_t* pr; int ldpr;
-  BNArgs pbn, pbn2;
-  int pkind, pr_bn;
-  double* ppart;
 };
 
 struct HeadArgs {
@@ -251,11 +212,6 @@ struct AdamArgs {
   const float* lr; const float* step;  // device scalars (step = number of completed steps)
   float b1, b2, eps, wd, grad_scale;
   int update;  // 0: pack only
-  // fused update (non-null): ONE launch over an OptSeg table of kind 0 (plain Adam ranges) and kind 2
-  // (conv weight tiles: Adam + both bf16 images); the last block to finish advances the step counter
-  unsigned* ticket;  // fused kernel: the last block advances the step counter (null: leave it, see fused)
-  int fused;         // run the fused Adam + pack kernel over `segs` even without a ticket (a partial
-                     // update inside the backward; the step's last optimizer launch advances the counter)
 };
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
@@ -271,7 +227,6 @@ int wgrad_tile_shape(int cfg, int& TN, int& TK);
 constexpr int WGRAD_PATCH_CFG0 = 12;  // wgrad cfgs 12-15: 3x3/s1 patch kernels (conv.hip wgrad_patch_block)
 int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8);
 int wgrad_ntiles(int cfg, const WgradArgs& a);  // tiles per group of a wgrad launch, < 0: cfg invalid for a
-constexpr int WGRAD_AOL_CFG = 100;  // batched-wgrad cfg offset selecting the apply-on-load kernels
 int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st);
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);

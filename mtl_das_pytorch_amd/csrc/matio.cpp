@@ -12,6 +12,7 @@
 // v7.3 (HDF5) files, complex / sparse / cell / struct variables.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#include <sys/stat.h>
 #include <zlib.h>
 
 #include <atomic>
@@ -124,9 +125,11 @@ float elem_value(const uint8_t* p, uint32_t type, bool swap) {
 }
 
 // Parse one miMATRIX element; if its name is `want`, write its real part row-major into `out`
-// (numel must equal `expect` when expect > 0).  Returns kOk, kNoVariable (other name) or an error.
+// (numel must equal `expect` when expect > 0, and the MATLAB dims must equal `want_dims` when given: a
+// 250 x 100 variable has the numel of a 100 x 250 slot but would land in it transposed).  Returns kOk,
+// kNoVariable (other name) or an error.
 int parse_matrix(const uint8_t* data, size_t nbytes, bool swap, const std::string& want, float* out,
-                 int64_t expect, std::vector<int64_t>* shape) {
+                 int64_t expect, std::vector<int64_t>* shape, const std::vector<int64_t>* want_dims) {
   Cursor c{data, data + nbytes, swap};
   Elem flags, dims, name, real;
   if (!next_elem(c, flags) || flags.type != miUINT32 || flags.nbytes < 8) return kCorrupt;
@@ -147,6 +150,7 @@ int parse_matrix(const uint8_t* data, size_t nbytes, bool swap, const std::strin
   }
   if (shape) *shape = d;
   if (expect > 0 && numel != expect) return kShapeMismatch;
+  if (want_dims && !want_dims->empty() && d != *want_dims) return kShapeMismatch;
   if (!out) return kOk;
   if (!next_elem(c, real)) return kCorrupt;
   const size_t es = type_size(real.type);
@@ -174,16 +178,21 @@ int parse_matrix(const uint8_t* data, size_t nbytes, bool swap, const std::strin
   return kOk;
 }
 
-int inflate_all(const uint8_t* src, size_t n, std::vector<uint8_t>& dst) {
+// `cap`: the largest inflated size accepted (a corrupt or hostile stream cannot make the worker allocate
+// without bound).
+int inflate_all(const uint8_t* src, size_t n, std::vector<uint8_t>& dst, size_t cap) {
   z_stream zs{};
   if (inflateInit(&zs) != Z_OK) return kCorrupt;
-  dst.resize(n * 4 + 4096);
+  dst.resize(std::min(cap, n * 4 + 4096));
   zs.next_in = const_cast<Bytef*>(src);
   zs.avail_in = (uInt)n;
   size_t have = 0;
   int rc;
   do {
-    if (have == dst.size()) dst.resize(dst.size() * 2);
+    if (have == dst.size()) {
+      if (dst.size() >= cap) { inflateEnd(&zs); return kCorrupt; }
+      dst.resize(std::min(cap, dst.size() * 2));
+    }
     zs.next_out = dst.data() + have;
     zs.avail_out = (uInt)(dst.size() - have);
     rc = inflate(&zs, Z_NO_FLUSH);
@@ -196,6 +205,8 @@ int inflate_all(const uint8_t* src, size_t n, std::vector<uint8_t>& dst) {
 }
 
 int read_file(const std::string& path, std::vector<uint8_t>& buf) {
+  struct stat sb;
+  if (::stat(path.c_str(), &sb) != 0 || !S_ISREG(sb.st_mode)) return kIoError;  // directories, devices, fifos
   FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) return kIoError;
   std::fseek(f, 0, SEEK_END);
@@ -210,7 +221,7 @@ int read_file(const std::string& path, std::vector<uint8_t>& buf) {
 
 // Load variable `var` of a Level-5 MAT file as row-major float32.
 int load_mat5(const std::string& path, const std::string& var, float* out, int64_t expect,
-              std::vector<int64_t>* shape) {
+              std::vector<int64_t>* shape, const std::vector<int64_t>* want_dims = nullptr) {
   std::vector<uint8_t> buf;
   int rc = read_file(path, buf);
   if (rc) return rc;
@@ -228,7 +239,9 @@ int load_mat5(const std::string& path, const std::string& var, float* out, int64
     const uint8_t* md = e.data;
     size_t mn = e.nbytes;
     if (e.type == miCOMPRESSED) {
-      if ((rc = inflate_all(e.data, e.nbytes, inflated))) return rc;
+      // the variable is at most expect 8-byte values plus its headers; unknown size: 1 GiB
+      const size_t cap = expect > 0 ? (size_t)expect * 8 + (1u << 20) : ((size_t)1 << 30);
+      if ((rc = inflate_all(e.data, e.nbytes, inflated, cap))) return rc;
       Cursor ic{inflated.data(), inflated.data() + inflated.size(), swap};
       Elem inner;
       if (!next_elem(ic, inner)) return kCorrupt;
@@ -238,7 +251,7 @@ int load_mat5(const std::string& path, const std::string& var, float* out, int64
     } else if (e.type != miMATRIX) {
       continue;
     }
-    rc = parse_matrix(md, mn, swap, var, out, expect, shape);
+    rc = parse_matrix(md, mn, swap, var, out, expect, shape, want_dims);
     if (rc != kNoVariable) return rc;
   }
   return kNoVariable;
@@ -304,10 +317,27 @@ class Pool {
   bool stop_ = false;
 };
 
+// Never lets an exception escape a worker thread (it would std::terminate the training process): a file
+// the native reader cannot handle gets a status and falls back to scipy on the Python side.
+int load_mat5_safe(const std::string& path, const std::string& var, float* out, int64_t expect,
+                   const std::vector<int64_t>* want_dims) {
+  try {
+    return load_mat5(path, var, out, expect, nullptr, want_dims);
+  } catch (const std::bad_alloc&) {
+    return kCorrupt;
+  } catch (...) {
+    return kIoError;
+  }
+}
+
 class MatBatchLoader {
  public:
-  MatBatchLoader(std::vector<std::string> paths, std::string var, int64_t numel, int threads)
-      : paths_(std::move(paths)), var_(std::move(var)), numel_(numel), pool_(threads > 0 ? threads : 1) {}
+  // dims: the MATLAB dimensions every file's variable must have (empty: numel only)
+  MatBatchLoader(std::vector<std::string> paths, std::string var, std::vector<int64_t> dims, int threads)
+      : paths_(std::move(paths)), var_(std::move(var)), dims_(std::move(dims)), pool_(threads > 0 ? threads : 1) {
+    numel_ = 1;
+    for (int64_t d : dims_) numel_ *= d;
+  }
 
   // Load files idx[0..n) into out[i * numel ...] (float32, row-major).  Returns one status per file.
   std::vector<int> load(const std::vector<int64_t>& idx, int64_t out_ptr) {
@@ -319,7 +349,7 @@ class MatBatchLoader {
         const int64_t f = idx[i];
         st[i] = (f < 0 || f >= (int64_t)paths_.size())
                     ? kIoError
-                    : load_mat5(paths_[f], var_, out + i * numel_, numel_, nullptr);
+                    : load_mat5_safe(paths_[f], var_, out + i * numel_, numel_, &dims_);
       });
     }
     return st;
@@ -330,7 +360,8 @@ class MatBatchLoader {
  private:
   std::vector<std::string> paths_;
   std::string var_;
-  int64_t numel_;
+  std::vector<int64_t> dims_;
+  int64_t numel_ = 1;
   Pool pool_;
 };
 
@@ -340,16 +371,21 @@ void register_matio(py::module& m) {
   m.attr("MAT_OK") = (int)kOk;
   m.def("mat_shape", [](const std::string& path, const std::string& var) {
     std::vector<int64_t> shape;
-    const int rc = load_mat5(path, var, nullptr, 0, &shape);
+    int rc;
+    try {
+      rc = load_mat5(path, var, nullptr, 0, &shape);
+    } catch (...) {
+      rc = kIoError;
+    }
     return py::make_tuple(rc, shape);
   });
   m.def("mat_read", [](const std::string& path, const std::string& var, int64_t out_ptr, int64_t numel) {
     py::gil_scoped_release nogil;
-    return load_mat5(path, var, reinterpret_cast<float*>(static_cast<intptr_t>(out_ptr)), numel, nullptr);
+    return load_mat5_safe(path, var, reinterpret_cast<float*>(static_cast<intptr_t>(out_ptr)), numel, nullptr);
   });
   py::class_<MatBatchLoader>(m, "MatBatchLoader")
-      .def(py::init<std::vector<std::string>, std::string, int64_t, int>(), py::arg("paths"), py::arg("var"),
-           py::arg("numel"), py::arg("threads"))
+      .def(py::init<std::vector<std::string>, std::string, std::vector<int64_t>, int>(), py::arg("paths"),
+           py::arg("var"), py::arg("dims"), py::arg("threads"))
       .def("load", &MatBatchLoader::load)
       .def("__len__", &MatBatchLoader::size)
       .def_property_readonly("threads", &MatBatchLoader::threads);

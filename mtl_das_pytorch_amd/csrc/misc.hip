@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void pool3_fwd_kernel(PoolArgs a) {
 // Gradient of the input: sum over the output windows covering an input pixel (<= 4 for the stride-2 max
 // pool, <= 9 for the average pool) and over the fp32 gradient sources; per source, every window's loads are
 // issued before any is consumed.  MAX = 1: max pool, the argmax stored by the training forward routes the
-// gradient (a.am); MAX = 2: max pool without it (MDA_POOL_ARGMAX=0), each window is re-read to find its
+// gradient (a.am); MAX = 2: max pool without it (eval-mode programs, the functional API without `am`), each window is re-read to find its
 // maximum (a separate instantiation: sharing one kernel spilled the argmax path to scratch); MAX = 0: average.
 template <int MAX>
 __global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {

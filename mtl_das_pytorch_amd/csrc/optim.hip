@@ -19,32 +19,6 @@ namespace mda {
 
 
 
-struct AdamConsts { float c1, c2; };
-DEV AdamConsts adam_consts(const AdamArgs& a) {
-  const float t = a.step[0] + 1.f;
-  return {a.lr[0] / (1.f - powf(a.b1, t)), 1.f / sqrtf(1.f - powf(a.b2, t))};
-}
-// Four independent elements: all loads are issued before any store (the p / m / v pointers may alias as
-// far as the compiler knows, so a load-compute-store loop would serialise on memory latency).
-DEV void adam4(const AdamArgs& a, const AdamConsts& k, const int64_t* idx, const bool* ok, float* np) {
-  float p[4], g[4], m[4], v[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    p[j] = ok[j] ? a.p[idx[j]] : 0.f; g[j] = ok[j] ? a.g[idx[j]] : 0.f;
-    m[j] = ok[j] ? a.m[idx[j]] : 0.f; v[j] = ok[j] ? a.v[idx[j]] : 0.f;
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float gj = g[j] * a.grad_scale + a.wd * p[j];
-    m[j] = a.b1 * m[j] + (1.f - a.b1) * gj;
-    v[j] = a.b2 * v[j] + (1.f - a.b2) * gj * gj;
-    np[j] = p[j] - k.c1 * m[j] / (sqrtf(v[j]) * k.c2 + a.eps);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (ok[j]) { a.p[idx[j]] = np[j]; a.m[idx[j]] = m[j]; a.v[idx[j]] = v[j]; }
-}
-
 // Elementwise Adam over the whole flat buffer (padding slots hold p = g = 0 and stay 0).
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, int64_t n) {
   const float t = a.step[0] + 1.f;
@@ -136,9 +110,9 @@ DEV void pack_fwd_rows_block(const float* __restrict__ W, const OptSeg& S, int b
 // `step` (non-null after an Adam update): the step counter is advanced here -- the pack runs after the
 // Adam kernel that read it, so the separate one-thread launch is not needed.
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, const OptSeg* __restrict__ segs, int ns,
-                                                   float* step, int remap) {
+                                                   float* step) {
   __shared__ float s_t[PACK_ROWS][65];
-  const int bx = xcd_block((int)blockIdx.x, (int)gridDim.x, remap);
+  const int bx = (int)blockIdx.x;
   static_assert(PACK_ROWS * 65 >= PACK_FWD_FLOATS, "pack_fwd_rows_block stages its rows in s_t");
   if (step && blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1.f;
   int lo = 0, hi = ns - 1;
@@ -149,87 +123,9 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, 
   else pack_fwd_rows_block(P + S.off, S, blk, &s_t[0][0]);
 }
 
-// Fused optimizer step: every block of kind 0 updates 1024 consecutive elements of a plain range (BN
-// affine, biases, fc); every block of kind 2 owns one pack_dgrad_tile-shaped tile of a conv weight: it
-// runs Adam on the tile's masters (coalesced along each co's contiguous (ci, tap) run), keeps the new
-// values in LDS and writes BOTH bf16 images from there -- one launch and one pass over the masters instead
-// of Adam followed by a pack that re-reads them.  The step counter (read by every block) is advanced by the
-// last block to take a ticket, which then resets the ticket for the next step.
-__global__ __launch_bounds__(256) void adam_pack_fused_kernel(AdamArgs a, const OptSeg* __restrict__ segs, int ns) {
-  __shared__ float s_t[PACK_ROWS][65];
-  const AdamConsts k = adam_consts(a);
-  int lo = 0, hi = ns - 1;
-  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (segs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
-  const OptSeg& S = segs[lo];
-  const int local = (int)((int64_t)blockIdx.x - S.block0);
-  if (S.kind == 0) {
-    const int64_t e0 = (int64_t)local * 1024 + threadIdx.x;
-    int64_t idx[4]; bool ok[4]; float np[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { ok[j] = e0 + 256 * j < S.n; idx[j] = S.off + e0 + 256 * j; }
-    adam4(a, k, idx, ok, np);
-  } else {
-    const int taps = S.KH * S.KW;
-    const int cit = pack_dgrad_cit(taps);
-    const int nci = (S.Ci + cit - 1) / cit;
-    const int co0 = (local / nci) * 64, ci0 = (local % nci) * cit;
-    const int nci_t = min(cit, S.Ci - ci0), run = nci_t * taps;
-    const int nco = min(64, S.Co - co0);
-    for (int e0 = threadIdx.x; e0 < nco * run; e0 += 1024) {
-      int64_t idx[4]; bool ok[4]; float np[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int e = e0 + 256 * j, col = e / run, r = e - col * run;
-        ok[j] = e < nco * run;
-        idx[j] = S.off + ((int64_t)(co0 + col) * S.Ci + ci0) * taps + r;
-      }
-      adam4(a, k, idx, ok, np);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int e = e0 + 256 * j, col = e / run, r = e - col * run;
-        if (ok[j]) s_t[r][col] = np[j];
-      }
-    }
-    __syncthreads();
-    // data-gradient image [Ci][(tap, co)]: 16-byte chunks of 8 co
-    for (int item = threadIdx.x; item < run * 8; item += 256) {
-      const int r = item >> 3, ch = item & 7;
-      if (ch * 8 >= nco) continue;
-      const int ci = ci0 + r / taps, tap = r % taps;
-      uint32_t w4[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        w4[j] = (uint32_t)f2bf(s_t[r][ch * 8 + 2 * j]) | ((uint32_t)f2bf(s_t[r][ch * 8 + 2 * j + 1]) << 16);
-      *reinterpret_cast<uint4*>(S.wd + (int64_t)ci * S.Kpad_d + tap * S.Co + co0 + ch * 8) =
-          make_uint4(w4[0], w4[1], w4[2], w4[3]);
-    }
-    // forward image [Co][(tap, ci)]: each (co, tap) owns the tile's nci_t consecutive ci
-    for (int e = threadIdx.x; e < nco * taps * nci_t; e += 256) {
-      const int cil = e % nci_t, q = e / nci_t;
-      const int tap = q % taps, col = q / taps;
-      S.wf[(int64_t)(co0 + col) * S.Kpad_f + tap * S.Cs + ci0 + cil] = f2bf(s_t[cil * taps + tap][col]);
-    }
-  }
-  // step counter: the last block (all others have read step[0]) advances it and re-arms the ticket
-  if (!a.ticket) return;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned t = atomicAdd(a.ticket, 1u);
-    if (t == gridDim.x - 1) {
-      const_cast<float*>(a.step)[0] += 1.f;
-      atomicExch(a.ticket, 0u);
-    }
-  }
-}
-
 __global__ void step_inc_kernel(float* step) { step[0] += 1.f; }
 
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st) {
-  if (a.update && (a.ticket || a.fused)) {
-    if (nblocks <= 0) return -2;
-    hipLaunchKernelGGL(adam_pack_fused_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, a, d_segs, ns);
-    return (int)hipGetLastError();
-  }
   if (a.update) {
     const int64_t n4 = a.n >> 2;
     const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
@@ -238,9 +134,8 @@ int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nb
     if (rc) return rc;
   }
   float* step = a.update ? const_cast<float*>(a.step) : nullptr;
-  static const int remap = env_flag("MDA_XCD_REMAP", 0);
   if (nblocks > 0)
-    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, (const float*)a.p, d_segs, ns, step, remap);
+    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, (const float*)a.p, d_segs, ns, step);
   int rc = (int)hipGetLastError();
   if (rc || !a.update || nblocks > 0) return rc;
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);

@@ -201,8 +201,11 @@ class Datasetram(_MatDatasetBase):
         except Exception:  # pragma: no cover
             return None
         first = self._load(0)
+        dims = list(np.shape(load_mat(self.mat_list[0], (self.key,))))  # MATLAB dims every file must have
+        if int(np.prod(dims)) != first.size:
+            return None
         arr = np.empty((len(self.mat_list),) + first.shape, np.float32)
-        st = L.MatBatchLoader(self.mat_list, self.key, first.size, min(16, os.cpu_count() or 1)).load(
+        st = L.MatBatchLoader(self.mat_list, self.key, dims, min(16, os.cpu_count() or 1)).load(
             list(range(len(self.mat_list))), arr.ctypes.data)
         for j, rc in enumerate(st):
             if rc != 0:

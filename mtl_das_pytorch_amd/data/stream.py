@@ -69,7 +69,13 @@ class DiskBatchStream:
         self.labels = torch.zeros((ring * batch,) + lab_shape, dtype=torch.int64, device=self.device)
         self._rows = torch.arange(ring * batch, device=self.device).view(ring, batch)
         lib = _native_loader()
-        self.native = lib.MatBatchLoader(self.paths, key, self.numel, threads) if lib is not None else None
+        self.native = None
+        if lib is not None and self.paths:
+            # the raw variable's dims (a same-numel transposed file is then rejected and read by scipy,
+            # which raises on the shape like the reference's collate would)
+            dims = list(np.shape(load_mat(self.paths[0], (key,))))
+            if int(np.prod(dims)) == self.numel:
+                self.native = lib.MatBatchLoader(self.paths, key, dims, threads)
         self.fallbacks = 0
         self._pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="mda-disk")
         if self.cuda:

@@ -203,15 +203,17 @@ class EngineBackend(Backend):
         self.model_type = model_type
         self.ctx = ctx
         self.names, self.ncls = _report_tasks(model_type)
-        sw = ctx.world if (sync_bn and ctx.enabled) else 1
+        sync = sync_bn and ctx.enabled
+        sw = ctx.world if sync else 1
         if model_type == "multi_classifier":
             self.prog = InceptionProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), sync_world=sw)
         else:
             w = list(loss_weights) if model_type == "MTL" else [1.0]
             self.prog = MTLProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), loss_weights=w, sync_world=sw)
-        if sw > 1:  # SyncBN: BN statistics all-reduced inside the step, which then runs eagerly
+        if sync:  # SyncBN: BN statistics all-reduced inside the step (captured into the HIP graph on RCCL)
             self.prog.enable_sync_bn(ctx.all_reduce_ordered_)
-            use_graph = False
+            if not ctx.capturable_collectives:
+                use_graph = False
         self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world)
         if hasattr(self.prog, "set_rng_stream"):
             self.prog.set_rng_stream(seed, ctx.rank)

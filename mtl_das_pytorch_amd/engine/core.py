@@ -27,6 +27,7 @@ from ..ops.functional import WGRAD_PATCH, WGRAD_TILES, bnb_plan, patch_plan, pat
 from ..ops.hip import lib, ptr
 
 NREP = 32  # must match csrc/common.h
+BN_PX_PER_REP = 256  # forward BN-statistic replicas: about one per this many pixels
 
 
 def pad_to(x: int, m: int) -> int:
@@ -279,17 +280,13 @@ class BNLayer:
         self.part = arena.zeroed((self.G, NREP, 3, self.C), torch.float64)
         # batch constants (scale, shift, mean, invstd) published by the forward tail for the backward
         self.consts = arena.empty((self.G, 4, self.C), torch.float32)
-        # forward replicas in use: about one per 256 pixels (the producing conv then has at most ~16 blocks
-        # per replica address), so small maps are not read back as 32 mostly-empty replicas by every
-        # consumer block (MDA_BN_NREP overrides)
-        import os
-        fixed = int(os.environ.get("MDA_BN_NREP", "0"))
-        px = int(os.environ.get("MDA_BN_PX_PER_REP", "256"))
-        self.nrep = fixed or min(NREP, 1 << max(0, math.ceil(math.log2(max(1, count) / px))))
+        # forward replicas in use: about one per BN_PX_PER_REP pixels (the producing conv then has at most
+        # ~16 blocks per replica address), so small maps are not read back as 32 mostly-empty replicas by
+        # every consumer block (256 / 1,024 / 4,096 measured within noise, docs/PERF.md)
+        self.nrep = min(NREP, 1 << max(0, math.ceil(math.log2(max(1, count) / BN_PX_PER_REP))))
         # backward partial sums (bnb reduce chunks, dgrad epilogues): the same count, and every chunk of
-        # the reduce pass in a replica of its own when there are few (MDA_BN_PNREP overrides)
-        pfixed = int(os.environ.get("MDA_BN_PNREP", "0"))
-        self.pnrep = pfixed or max(self.nrep, min(NREP, 1 << max(0, math.ceil(math.log2(max(1, self.nchunk))))))
+        # the reduce pass in a replica of its own when there are few
+        self.pnrep = max(self.nrep, min(NREP, 1 << max(0, math.ceil(math.log2(max(1, self.nchunk))))))
         self.arena = arena
         self.dzbuf = None
 
@@ -386,8 +383,8 @@ class ConvLayer:
     # convs batched into one launch (csrc/conv.hip conv_wgrad_batched_kernel) the grid no longer has to
     # be filled by one conv's splits, and each extra split costs a full Npad x Kpad slab read in the
     # finalize (Model C: ~0.9 GB/step of slab traffic with grid-filling splits)
-    # (MDA_MIN_SPLIT_PX: 512 / 2048 / 4096 measured within noise on A, C 7.10k at 1024 vs 6.83k at 2048)
-    MIN_SPLIT_PX = int(__import__("os").environ.get("MDA_MIN_SPLIT_PX", "1024"))
+    # (512 / 2048 / 4096 measured within noise on A, C 7.10k at 1024 vs 6.83k at 2048)
+    MIN_SPLIT_PX = 1024
 
     def wgrad_valid(self, cfg: int) -> bool:
         """The K tiles of ``cfg`` cover this conv's padded reduction exactly (patch configs: a 3x3 / s1 /
@@ -399,10 +396,8 @@ class ConvLayer:
         return self.Kpad_w % WGRAD_TILES[cfg][1] == 0
 
     def wgrad_plan(self, cfg: int):
-        if cfg in WGRAD_PATCH:
-            import os
-            return patch_plan(cfg, self.B, self.Ho, self.Npad, self.Cs, self.G,
-                              int(os.environ.get("MDA_PATCH_TARGET", "128")))
+        if cfg in WGRAD_PATCH:  # splits sized for ~128 blocks per job (32 / 64 / 256 measured slower)
+            return patch_plan(cfg, self.B, self.Ho, self.Npad, self.Cs, self.G, 128)
         TN, TK, MCH = WGRAD_TILES[cfg]
         tiles = math.ceil(self.Npad / TN) * (self.Kpad_w // TK) * self.G
         # whole-reduction tiles (TK >= 128) have one tile per channel block: shorter per-block pixel
@@ -439,17 +434,6 @@ class ConvLayer:
             segs.append(dict(common, kind=1, n=self.Npad * self.Kpad, wf=P(self.wf, g * self.Npad * self.Kpad)))
             segs.append(dict(common, kind=2, n=self.Npad_d * self.Kpad_d,
                              wd=P(self.wd, g * self.Npad_d * self.Kpad_d)))
-        return segs
-
-    def fused_segments(self) -> List[dict]:
-        """Fused Adam + pack tiles (csrc/optim.hip adam_pack_fused_kernel): one kind-2 segment per group
-        member that updates the masters and writes both bf16 images."""
-        segs = []
-        for g, m in enumerate(self.mods):
-            segs.append({"off": self.flat.off(m.weight), "Co": self.Co, "Ci": self.Ci, "KH": self.KH, "KW": self.KW,
-                         "Cs": self.Cs, "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d, "kind": 2,
-                         "n": self.Co * self.Ci * self.KH * self.KW,
-                         "wf": P(self.wf, g * self.Npad * self.Kpad), "wd": P(self.wd, g * self.Npad_d * self.Kpad_d)})
         return segs
 
     def finalize_desc(self) -> dict:
@@ -492,19 +476,16 @@ class ConvLayer:
 # ------------------------------------------------------------------------------------------------
 # descriptor tables (uploaded once; read by wgrad_finalize / adam_pack)
 def finalize_lanes(splits: int) -> int:
-    """Threads per weight in wgrad_finalize: about 8 splits per thread, a power of two <= 16
-    (MDA_FIN_LANES caps it; 1 = one thread per weight)."""
-    import os
-    cap = int(os.environ.get("MDA_FIN_LANES", "16"))
+    """Threads per weight in wgrad_finalize: about 8 splits per thread, a power of two <= 16."""
     lanes = 1
-    while lanes < cap and splits > 8 * lanes:
+    while lanes < 16 and splits > 8 * lanes:
         lanes *= 2
     return lanes
 
 
 # convs with at most this many wgrad splits are finalized in output order (contiguous gradient stores);
-# more splits: slab order with several lanes per weight (coalesced split reads)
-FIN_OUT_MAX_SPLITS = int(__import__("os").environ.get("MDA_FIN_OUT_MAX", "2"))
+# more splits: slab order with several lanes per weight (coalesced split reads); 0 / 2 / 8 swept (docs/PERF.md)
+FIN_OUT_MAX_SPLITS = 2
 
 
 def build_wgfin_table(descs: List[dict], device) -> tuple:
@@ -534,18 +515,6 @@ def build_wgfin_table(descs: List[dict], device) -> tuple:
 
 PACK_ROWS = 72  # csrc/kernels.h
 PACK_FWD_FLOATS = 4096  # csrc/kernels.h
-
-
-def plain_ranges(numel: int, covered: List[tuple]) -> List[dict]:
-    """Kind-0 optimizer segments: the parts of [0, numel) not covered by the (off, n) conv-weight ranges."""
-    out, pos = [], 0
-    for off, n in sorted(covered):
-        if off > pos:
-            out.append({"kind": 0, "off": pos, "n": off - pos})
-        pos = max(pos, off + n)
-    if pos < numel:
-        out.append({"kind": 0, "off": pos, "n": numel - pos})
-    return out
 
 
 def build_optseg_table(segs: List[dict], device) -> tuple:

@@ -97,10 +97,8 @@ class Pool:
             raise ValueError("pool output shape mismatch")
         self.dx = new_act(prog.arena, 1, prog.B, s.H, s.W, s.C, torch.float32) if src.needs_grad else None
         # max pool: the training forward stores each output's window argmax (1 byte) for the backward
-        # (MDA_POOL_ARGMAX=0: the backward re-reads the 3x3 windows instead)
-        import os
         self.am = None
-        if is_max and self.dx is not None and os.environ.get("MDA_POOL_ARGMAX", "1") == "1":
+        if is_max and self.dx is not None:
             self.am = prog.arena.zeros((prog.B * Ho * Wo * s.C,), torch.uint8)
 
     def _geom(self, B):
@@ -317,7 +315,7 @@ class InceptionProgram(LoweredProgram):
         self.seed.fill_(stream << 32)
 
     # the stem's 47x122 and 21x58 convs keep their BN+ReLU tails (C at bs 32: 7.55k -> 7.66k samples/s,
-    # three runs each of MDA_NOL_MAX_PX = all / 1e5 / 3e4)
+    # three runs each of a limit of all / 1e5 / 3e4 output pixels)
     NOL_MAX_PX = 30000
 
     def _plan_nol(self):
@@ -327,7 +325,7 @@ class InceptionProgram(LoweredProgram):
         self.n_nol = 0
         if not self.nol_enabled():
             return
-        max_px = self.nol_max_px()
+        max_px = self.NOL_MAX_PX
         consumers = {}
         for op in self.ops:
             consumers[id(op.src)] = consumers.get(id(op.src), 0) + 1
@@ -358,7 +356,6 @@ class InceptionProgram(LoweredProgram):
         self.fwd_eval = self._emit_forward(False)
         self.bwd = self._emit_backward()
         self.fuse_dgrad_bn_stats()
-        self.apply_on_load()
         self.opt = self._emit_optimizer()
 
     def _emit_streamed(self, ph: Phase, order, run) -> List[str]:

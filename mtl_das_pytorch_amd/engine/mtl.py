@@ -174,7 +174,6 @@ class MTLProgram(LoweredProgram):
         self.fwd_eval = self._emit_forward(False)
         self.bwd = self._emit_backward()
         self.fuse_dgrad_bn_stats()
-        self.apply_on_load()
         self.opt = self._emit_optimizer()
 
     def _emit_forward(self, training: bool) -> Phase:
@@ -183,31 +182,16 @@ class MTLProgram(LoweredProgram):
         self._conv_fwd(ph, self.conv1, src_dict(self.xin), self.y0, self.bn1, training)
         self._tail(ph, ACT_RELU, 1, self.y0, self.bn1, self.f0, training)
         ph.cur_stream = 0
-        rol = self.nol and self.rol_enabled()
         for ri, L in enumerate(self.rbs):
             s = src_dict(L["in"])
-            nol_in = None
-            if rol and ri > 0:
-                # residual-on-load: this block's convs compute their input F_ri = relu(BN(yb) + r') from the
-                # previous block's yb and residual, so the previous block's ADD_RELU tail runs on stream 2,
-                # off the backbone chain; an identity residual r' = F_{ri-1} comes from stream 2 too
-                P_ = self.rbs[ri - 1]
-                s = src_dict(P_["yb"])
-                nol_in = (P_["bnb"], ADD_RELU, P_["ys"] if P_["proj"] else P_["in"], P_["bns"] if P_["proj"] else None)
-                if not P_["proj"] and ri >= 2:
-                    ph.pending_waits.append(f"F{ri - 1}")
-            self._conv_fwd(ph, L["ca"], s, L["ya"], L["bna"], training, nol=nol_in)
+            self._conv_fwd(ph, L["ca"], s, L["ya"], L["bna"], training)
             if self.nol_for(L["cb"]):  # conv b normalises ya on load: no BN+ReLU tail, ha never materialised
                 self._conv_fwd(ph, L["cb"], src_dict(L["ya"]), L["yb"], L["bnb"], training, nol=(L["bna"], ACT_RELU))
             else:
                 self._tail(ph, ACT_RELU, 1, L["ya"], L["bna"], L["ha"], training)
                 self._conv_fwd(ph, L["cb"], src_dict(L["ha"]), L["yb"], L["bnb"], training)
             if L["proj"]:
-                self._conv_fwd(ph, L["cs"], s, L["ys"], L["bns"], training, nol=nol_in)
-            if rol:
-                ph.mark(f"yb{ri + 1}")
-                ph.cur_stream = 2
-                ph.pending_waits.append(f"yb{ri + 1}")
+                self._conv_fwd(ph, L["cs"], s, L["ys"], L["bns"], training)
             if L["proj"]:
                 self._tail(ph, ADD_RELU, 1, L["yb"], L["bnb"], L["out"], training, r=L["ys"], bn2=L["bns"])
             else:
@@ -245,47 +229,6 @@ class MTLProgram(LoweredProgram):
             hd["lab_off"] = 0
         ph.add("mtl_head", k_head, hd)
         return ph
-
-    @staticmethod
-    def rol_enabled() -> bool:
-        """Residual-on-load in the forward (MDA_ROL=1, opt-in): the first convs of residual block k + 1
-        read block k's pre-BN yb and residual and apply relu(BN(yb) + r') on load (csrc/conv.hip
-        MODE_FWD_ROL, bitwise the tail's output: tests/test_engine_gpu.py::test_residual_on_load_bitwise),
-        so the ADD_RELU tails that materialise F_k for the task branches, the next tail's residual and the
-        backward run on stream 2.  Measured slower on MI355X (docs/PERF.md): forward 304 -> 600 us with the
-        side stream, 388 -> 437 us on one stream -- the ROL convs run 20-25 us instead of 12-15 (two BN
-        constant sets read from LDS in every K step's chain, a second operand load)."""
-        import os
-        return os.environ.get("MDA_ROL", "0") == "1"
-
-    @staticmethod
-    def msbns_enabled() -> bool:
-        """Multi-source BN-backward statistics (MDA_MSBNS=1, opt-in): the residual-block ADD_RELU tails and
-        conv1's tail have 2-4 gradient sources; instead of a reduce pass over their sum on the backbone's
-        critical stream, every producer accumulates its share of sum(dz), sum(dz xhat), sum(dz xhat2)
-        (statistics are linear in the gradient): the next block's data gradients in their epilogues, an
-        identity block's tail in its apply pass (its side output is the shortcut gradient), and a
-        reduce-only launch on stream 2 for the task-branch sources.  The tail then runs apply only.
-        Measured on MI355X (tools/phase_times.py): backward 663 -> 747 us, bench 31.9k -> 29.8k samples/s.
-        The apply-only tails are 3-13 us faster on the 5x11 / 9x21 maps but not on 33x83 (latency-bound
-        either way), and the reduce-only launches on stream 2 contend with the critical stream and put
-        their own latency in front of the first tail.  Off by default; tests keep it correct."""
-        import os
-        return os.environ.get("MDA_MSBNS", "0") == "1"
-
-    def _feed_tail_stats(self, j: int, stats: dict):
-        """Make residual block j (0-based) -- the consumer of the feature whose tail ``stats`` describes --
-        accumulate that tail's statistics over the gradients it produces for it: the data gradients of
-        its conv a (and projection shortcut) and, for an identity shortcut, its own tail's side output."""
-        if j >= len(self.rbs):
-            return
-        R = self.rbs[j]
-        for key in ("ca_dgrad", "cs_dgrad"):
-            if key in R:
-                R[key].args[3]["bnb"] = dict(stats)
-        if not R["proj"]:
-            prev = {k: v for k, v in stats.items() if k not in ("ygs", "rgs", "C")}
-            R["tail_bwd"].args[3]["prev"] = prev
 
     def bucket_cut_candidates(self) -> List[tuple]:
         """One cut: right before residual block 1's backward, every task-branch (level) gradient is
@@ -349,7 +292,6 @@ class MTLProgram(LoweredProgram):
                 else:
                     src.append((R["side"].p, 0, R["side"].ld))
             return src
-        msbns = self.msbns_enabled()
         for i in range(7, -1, -1):
             R = self.rbs[i]
             g = sources(i + 1)
@@ -358,37 +300,21 @@ class MTLProgram(LoweredProgram):
             # F_{i+1}'s task-branch gradients: for F_{2l+2} (i odd) the mask-target gradient dF, ready right
             # after the level's sigmoid-mask backward; for F_{2l+1} the concat gradient of the whole level
             task_tag = f"dF{i // 2}" if i % 2 == 1 else f"lvl{i // 2}"
-            r, bn2 = (R["ys"], R["bns"]) if R["proj"] else (R["in"], None)
-            if msbns:
-                # multi-source statistics: the task sources are reduced on stream 2 as soon as they exist,
-                # block i+2's data gradients (and identity tail) add theirs in their epilogues -> apply only
-                self._tail_partial(ph, ADD_RELU, R["yb"], R["bnb"], g[:T], r=r, bn2=bn2, stream=2, waits=(task_tag,),
-                                   record=f"pr{i}")
-                self._feed_tail_stats(i + 1, self._tail_stats_args(ADD_RELU, R["yb"], R["bnb"], r, bn2))
-                ph.pending_waits.append(f"pr{i}")
-            else:
-                ph.pending_waits.append(task_tag)
+            ph.pending_waits.append(task_tag)
             if R["proj"]:
-                self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["ys"], bn2=R["bns"], dy2=R["dys"],
-                               apply_only=msbns)
+                self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["ys"], bn2=R["bns"], dy2=R["dys"])
             else:
-                self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["in"], side=R["side"],
-                               apply_only=msbns)
-            R["tail_bwd"] = ph.launches[-1]
+                self._tail_bwd(ph, ADD_RELU, 1, R["yb"], R["bnb"], g, R["dyb"], r=R["in"], side=R["side"])
             if self.nol_for(R["cb"]):
                 self._conv_bwd(ph, R["cb"], src_dict(R["ya"]), R["dyb"], R["dha"], nol=(R["bna"], ACT_RELU))
             else:
                 self._conv_bwd(ph, R["cb"], src_dict(R["ha"]), R["dyb"], R["dha"])
             self._tail_bwd(ph, ACT_RELU, 1, R["ya"], R["bna"], [(R["dha"].p, 0, R["dha"].ld)], R["dya"])
             self._conv_bwd(ph, R["ca"], src_dict(R["in"]), R["dya"], R["dxa"])
-            R["ca_dgrad"] = next(l for l in reversed(ph.launches) if l.name == "conv_dgrad")
             if R["proj"]:
                 self._conv_bwd(ph, R["cs"], src_dict(R["in"]), R["dys"], R["dxs"])
-                R["cs_dgrad"] = next(l for l in reversed(ph.launches) if l.name == "conv_dgrad")
         self.dy0 = new_act(self.arena, 1, self.B, self.y0.H, self.y0.W, self.y0.C)
-        if msbns:  # conv1's BN+ReLU tail: sources dxa / side of RB1, both producers accumulate its statistics
-            self._feed_tail_stats(0, self._tail_stats_args(ACT_RELU, self.y0, self.bn1))
-        self._tail_bwd(ph, ACT_RELU, 1, self.y0, self.bn1, sources(0), self.dy0, apply_only=msbns)
+        self._tail_bwd(ph, ACT_RELU, 1, self.y0, self.bn1, sources(0), self.dy0)
         self._conv_bwd(ph, self.conv1, src_dict(self.xin), self.dy0, None)
         self._rb1_anchor = ph.launches[self._rb1_bwd_first]
         # weight-gradient slabs -> flat fp32 gradients (one launch for every conv), after all wgrads

@@ -25,7 +25,7 @@ from ..ops.hip import lib, stream
 # hipStreamEndCapture on ROCm 7.
 MULTI_STREAM = os.environ.get("MDA_STREAMS", "1") == "1"
 # streams used at most (ids above are folded onto the last one -- still a valid schedule)
-MAX_STREAMS = max(1, min(4, int(os.environ.get("MDA_MAX_STREAMS", "4"))))
+MAX_STREAMS = 4
 
 
 class Launch:

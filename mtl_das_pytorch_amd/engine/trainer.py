@@ -61,8 +61,20 @@ class ResidentSource:
         return len(self.X)
 
     def batches(self, index_batches):
-        for b in index_batches:
-            yield b.to(self.X.device), int(b.numel())
+        """Yield (device index batch, size).  The whole epoch's indices go to the device in ONE copy
+        (pinned host memory, non_blocking) and the batches are device slices: a per-batch pageable copy
+        would make the host wait for the previous step's graph before it could launch the next one."""
+        index_batches = list(index_batches)
+        if not index_batches:
+            return
+        sizes = [int(b.numel()) for b in index_batches]
+        flat = torch.cat([b.reshape(-1).to("cpu", torch.int64) for b in index_batches])
+        if self.X.device.type == "cuda":
+            flat = flat.pin_memory().to(self.X.device, non_blocking=True)
+        o = 0
+        for n in sizes:
+            yield flat[o:o + n], n
+            o += n
 
     def close(self):
         pass

@@ -37,8 +37,6 @@ def conv_signature(mode: int, G: int, d: dict) -> str:
     src = d["src"]
     sig = f"conv{mode}|G{G}|" + ",".join(str(d[k]) for k in keys) + f"|seg{int(src.get('C1', 0) > 0)}" + \
           f"|st{int(bool(d.get('stats')))}"
-    if (d.get("nol") or {}).get("r"):  # residual-on-load runs on the register-pipelined kernels only
-        sig += "|rol"
     return sig
 
 

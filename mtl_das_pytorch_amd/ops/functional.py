@@ -145,9 +145,6 @@ def prepare_conv2d(x, w, bias=None, stride=1, padding=0, stats=None, x2=None, cf
          "Npad": wf.shape[0], "Cs": Cs, "KH": KH, "KW": KW, "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": wf.shape[1]}
     if nol is not None:  # (bn dict of x's BN, kind): x is a pre-BN y, the operand is act(BN(x)) on load
         d["nol"] = {"bn": nol[0], "kind": nol[1]}
-        if len(nol) > 2:  # residual-on-load (kind 4): (bn, 4, r [B,H,W,C] bf16, bn2 dict or None)
-            r = nol[2]
-            d["nol"].update(r={"p": ptr(r), "gs": 0, "ld": r.shape[-1]}, bn2=nol[3])
     return ConvCall(0, _fwd_cfg(Co, B * Ho * Wo) if cfg is None else cfg, d, y, (x, x2, wf, bias, stats, nol))
 
 
@@ -161,16 +158,10 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return prepare_conv2d(x, w, bias, stride, padding, stats, x2, cfg, nol).run()
 
 
-def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg=None, bn_stats=None,
-                         aol=None) -> ConvCall:
+def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg=None, bn_stats=None) -> ConvCall:
     """``bn_stats`` (optional): ``(y, bn, part, kind)`` -- the dgrad output is the gradient of
     ``act(BN(y))`` and the epilogue accumulates that BN's backward sums sum(dz), sum(dz*xhat) into rows 0/1
-    of ``part`` ([NREP, 3, C] fp64, zero-initialised); see :func:`bn_tail_backward` ``stats_done``.
-    ``aol`` (optional): ``(g, y, bn, part, coef, dgamma, dbeta, kind)`` -- apply-on-load: ``dy`` is not
-    read; the operand is the BN-tail backward of ``act(BN(y))`` with upstream gradient ``g`` (fp32) and the
-    completed statistics ``part``, computed while loading.  Writes dgamma / dbeta and the [5, C]
-    coefficient table ``coef`` the matching :func:`conv2d_wgrad` ``aol`` reads.  ``dy`` only gives the
-    shape (pass ``y``)."""
+    of ``part`` ([NREP, 3, C] fp64, zero-initialised); see :func:`bn_tail_backward` ``stats_done``."""
     _check(dy, torch.bfloat16)
     B, Ho, Wo, Co = dy.shape
     _, Ci, KH, KW = w.shape
@@ -191,21 +182,13 @@ def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg
             raise ValueError("bn_stats: y must be the [B, H, W, C] bf16 BN input and part fp64 [NREP, 3, C]")
         d["bnb"] = {"y": ptr(y), "ldy": Cs, "bn": bn, "part": ptr(part), "kind": kind}
         keep = keep + (y, part)
-    if aol is not None:
-        g, y, bn, part, coef, dgamma, dbeta, kind = aol
-        _check(y, torch.bfloat16)
-        if g.dtype != torch.float32 or g.shape != dy.shape or y.shape != dy.shape or coef.numel() != 5 * Co:
-            raise ValueError("aol: g (fp32) and y (bf16) must have dy's shape, coef 5 * C floats")
-        d["aol"] = {"g": ptr(g), "ldg": Co, "y": ptr(y), "ldy": Co, "bn": bn, "part": ptr(part), "coef": ptr(coef),
-                    "dgamma": ptr(dgamma), "dbeta": ptr(dbeta), "kind": kind}
-        keep = keep + (g, y, part, coef, dgamma, dbeta)
     return ConvCall(1, _fwd_cfg(Cs, B * H * W) if cfg is None else cfg, d, dx, keep)
 
 
 def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw: Tuple[int, int], stride=1, padding=0,
-                 cin_stored: Optional[int] = None, cfg: Optional[int] = None, bn_stats=None, aol=None):
+                 cin_stored: Optional[int] = None, cfg: Optional[int] = None, bn_stats=None):
     """Gradient w.r.t. the NHWC input: fp32 ``[B, H, W, Cin_stored]``."""
-    return prepare_conv2d_dgrad(dy, w, in_hw, stride, padding, cin_stored, cfg, bn_stats, aol).run()
+    return prepare_conv2d_dgrad(dy, w, in_hw, stride, padding, cin_stored, cfg, bn_stats).run()
 
 
 WGRAD_TILES = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 64), 4: (16, 64, 128),
@@ -241,8 +224,7 @@ def wgrad_cfg(Co: int, Kpad: int) -> int:
     return 0 if Co <= 16 else ((1 if Kpad <= 64 else 2) if Co <= 32 else 3)
 
 
-def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=None, cfg=None, nol=None,
-                         aol=None) -> WgradCall:
+def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=None, cfg=None, nol=None) -> WgradCall:
     _check(x, torch.bfloat16)
     _check(dy, torch.bfloat16)
     Co, Ci, KH, KW = w_shape
@@ -280,23 +262,18 @@ def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=No
 
     if nol is not None:  # (consts [1, 4, Cs] fp32: scale, shift, mean, invstd; kind)
         d["nol"] = {"consts": ptr(nol[0]), "kind": nol[1]}
-    if aol is not None:  # (g fp32, y bf16, coef [5, Co] from the matching apply-on-load dgrad, kind)
-        if aol[0].shape != dy.shape or aol[1].shape != dy.shape:
-            raise ValueError("aol: g and y must have dy's shape")
-        d["aol"] = {"g": ptr(aol[0]), "ldg": Co, "y": ptr(aol[1]), "ldy": Co, "coef": ptr(aol[2]), "kind": aol[3]}
 
     def post(sl):
         dWp = sl.sum(dim=1)[0, :Co, :KH * KW * Cs].view(Co, KH, KW, Cs)[..., :Ci]
         return dWp.permute(0, 3, 1, 2).contiguous()
-    return WgradCall(cfg, d, slab, post, (x, x2, dy, nol, aol))
+    return WgradCall(cfg, d, slab, post, (x, x2, dy, nol))
 
 
 def conv2d_wgrad(x: torch.Tensor, dy: torch.Tensor, w_shape, stride=1, padding=0, x2: Optional[torch.Tensor] = None,
-                 splits: Optional[int] = None, cfg: Optional[int] = None, nol=None, aol=None):
+                 splits: Optional[int] = None, cfg: Optional[int] = None, nol=None):
     """Weight gradient in the reference layout ``[Co, Ci, KH, KW]`` (fp32).  ``nol`` ((consts, kind)): ``x``
-    is pre-BN and the operand is act(x * consts[0,0] + consts[0,1]), as in a normalise-on-load forward.
-    ``aol`` ((g, y, coef, kind)): dy is rebuilt on load as in an apply-on-load dgrad (which wrote coef)."""
-    return prepare_conv2d_wgrad(x, dy, w_shape, stride, padding, x2, splits, cfg, nol, aol).run()
+    is pre-BN and the operand is act(x * consts[0,0] + consts[0,1]), as in a normalise-on-load forward."""
+    return prepare_conv2d_wgrad(x, dy, w_shape, stride, padding, x2, splits, cfg, nol).run()
 
 
 # ---------------------------------------------------------------------------------------------------

@@ -37,7 +37,15 @@ class DistContext:
 
     @property
     def enabled(self) -> bool:
-        return self.world > 1
+        """A process group exists: collectives run (a 1-rank RCCL group included -- MDA_DIST_BACKEND=nccl with
+        WORLD_SIZE=1 executes the whole RCCL code path on one GPU)."""
+        return self.backend is not None
+
+    @property
+    def capturable_collectives(self) -> bool:
+        """Collectives can be captured into a HIP graph (RCCL: stream-ordered device collectives); gloo's
+        host round trip cannot, so a step with in-step collectives (SyncBN) then runs eagerly."""
+        return self.backend == "nccl"
 
     @property
     def is_main(self) -> bool:
@@ -102,11 +110,23 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[int] = N
     device = torch.device(f"cuda:{dev_index}") if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
+    backend = backend or os.environ.get("MDA_DIST_BACKEND")
     if world <= 1:
-        return DistContext(0, 1, 0, device, None)
+        if not backend:
+            return DistContext(0, 1, 0, device, None)
+        # a real 1-rank process group (MDA_DIST_BACKEND=nccl: a 1-rank RCCL communicator on this GPU), so
+        # the collective code path -- async bucket all-reduces, stream-ordered SyncBN sums, barriers,
+        # metric reduction -- executes on a one-GPU machine; rendezvous through an in-process store
+        if not dist.is_initialized():
+            kw = dict(backend=backend, store=dist.HashStore(), rank=0, world_size=1,
+                      timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kw["device_id"] = device
+            dist.init_process_group(**kw)
+        return DistContext(0, 1, 0, device, backend)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
-    backend = backend or os.environ.get("MDA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+    backend = backend or ("nccl" if use_gpu else "gloo")
     if backend == "gloo" and os.environ["MASTER_ADDR"] in ("127.0.0.1", "localhost"):
         # single-node gloo over loopback: the host name may not resolve (containers), and gloo's
         # interface guess then makes a restarted group's full-mesh connect fail intermittently

@@ -118,3 +118,30 @@ def test_dp_trainer_ranks_stay_in_sync(tmp_path):
     assert len(dirs) == 1  # only rank 0 writes, one run directory
     files = os.listdir(os.path.join(tmp_path, dirs[0]))
     assert "console output.log" in files and any(f.endswith(".pth") for f in files)
+
+
+def _worker_one_rank(q):
+    os.environ.pop("WORLD_SIZE", None)
+    os.environ["MDA_DIST_BACKEND"] = "gloo"
+    from mtl_das_pytorch_amd.parallel.dist import FlatGradAllReducer, init_distributed, shutdown
+    ctx = init_distributed()
+    t = torch.arange(8, dtype=torch.float32)
+    red = FlatGradAllReducer(ctx)
+    red.start(t[:4])
+    red.start(t[4:])
+    red.finish()
+    ctx.barrier()
+    q.put((ctx.enabled, ctx.world, dist.is_initialized(), dist.get_world_size(), t.tolist()))
+    shutdown(ctx)
+
+
+def test_one_rank_process_group():
+    """MDA_DIST_BACKEND with WORLD_SIZE=1 builds a real 1-rank process group (in-process store): the
+    collective code path runs and a 1-rank sum is the identity (the GPU test does the same over RCCL)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_one_rank, args=(q,))
+    p.start()
+    res = q.get(timeout=120)
+    p.join(60)
+    assert res == (True, 1, True, 1, [float(i) for i in range(8)])

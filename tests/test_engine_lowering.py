@@ -7,8 +7,7 @@ from mtl_das_pytorch_amd.engine.mtl import MTLProgram
 from mtl_das_pytorch_amd.models import MTL_Net, Single_Task_Net
 
 
-def test_mtl_program_structure(monkeypatch):
-    monkeypatch.setenv("MDA_MSBNS", "1")  # opt-in multi-source BN statistics (checked below)
+def test_mtl_program_structure():
     m = MTL_Net()
     sd_before = {k: v.clone() for k, v in m.state_dict().items()}
     p = MTLProgram(m, 32, "cpu")
@@ -18,16 +17,10 @@ def test_mtl_program_structure(monkeypatch):
     assert p.flat.numel >= sum(x.numel() for x in m.parameters())
     n = p.num_launches()
     # forward: 12 BN+ReLU tails are folded into their consumer conv (normalise-on-load)
-    assert n["forward_train"] == 48 and n["backward"] == 98
-    # multi-source BN statistics (MDA_MSBNS): one reduce-only launch per residual tail on stream 2, every
-    # residual tail and conv1's tail apply-only, their producers carry the statistics descriptors
-    parts = [l for l in p.bwd.launches if l.name.startswith("tailpart")]
-    assert len(parts) == 8 and all(l.stream == 2 and l.args[3]["fused"] == 3 for l in parts)
+    assert n["forward_train"] == 48 and n["backward"] == 90
+    # the residual tails have 2-4 gradient sources: reduce + apply (or single launch) over their sum
     tails = [l for l in p.bwd.launches if l.name == "tailbwd4"]
-    assert len(tails) == 8 and all(l.args[3]["fused"] == 2 and "dzbuf" not in l.args[3] for l in tails)
-    assert [R["ca_dgrad"].args[3]["bnb"]["kind"] for R in p.rbs] == [1] + [4] * 7
-    assert [("prev" in R["tail_bwd"].args[3]) for R in p.rbs] == [not R["proj"] for R in p.rbs]
-    assert all("bn2" in R["ca_dgrad"].args[3]["bnb"] for j, R in enumerate(p.rbs) if j and p.rbs[j - 1]["proj"])
+    assert len(tails) == 8 and all(l.args[3].get("fused", 0) != 2 for l in tails)
     # both task branches of a level are ONE grouped launch with an even parameter stride
     L = p.levels[1]
     assert L["c0"].G == 2 and L["c0"].wstride > 0
@@ -83,106 +76,25 @@ def test_inception_program_structure():
 
 
 def test_wgrad_batching_structure():
-    """All per-conv weight-gradient launches collapse into one launch per tile config; every conv appears
-    in exactly one job table.  With MDA_FIN_SPLIT=1 (opt-in) each stream finalizes its own convs right after
-    its batches, so the main stream's tail finalize covers the main stream's convs only; with the split off,
-    one finalize waits for every stream's last batch."""
-    for split in ("1", "0"):
-        import os
-        os.environ["MDA_FIN_SPLIT"] = split
-        os.environ["MDA_EARLY_OPT"] = "0"
-        try:
-            p = MTLProgram(MTL_Net(), 32, "cpu")
-            n_wg = sum(1 for l in p.bwd.launches if l.name == "conv_wgrad")
-            st_of = {id(l.owner): l.stream for l in p.bwd.launches if l.name == "conv_wgrad"}
-            p.batch_wgrads()
-        finally:
-            del os.environ["MDA_FIN_SPLIT"]
-            del os.environ["MDA_EARLY_OPT"]
-        b = [l for l in p.bwd.launches if l.name == "wgrad_batched"]
-        assert sum(l.args[2] for l in b) == n_wg
-        fin = p.bwd.launches[-1]
-        assert fin.name == "wgrad_finalize" and fin.stream == 0
-        fins = [l for l in p.bwd.launches if l.name == "wgrad_finalize"]
-        if split == "1":
-            assert fin.waits == () and len(fins) == len({l.stream for l in b})
-            assert sum(f.args[1] for f in fins) == len(p.convs) == len(st_of)
-            for f in fins[:-1]:  # a side stream's finalize follows that stream's last batch
-                assert f.stream != 0 and f.record == f"wgrads_s{f.stream}"
-                last = max(i for i, l in enumerate(p.bwd.launches) if l.name == "wgrad_batched" and l.stream == f.stream)
-                assert p.bwd.launches.index(f) > last
-        else:
-            assert len(fins) == 1 and set(fin.waits) == {f"wgrads_s{s}" for s in {l.stream for l in b}}
-        _check_event_order(p.bwd)
-
-
-@pytest.mark.parametrize("mode", ["join", "join2"])
-def test_wgrad_join_stage_structure(monkeypatch, mode):
-    """Model C (MDA_WGRAD_STAGE=join / join2): the main stream's weight gradients of the Inception blocks move to
-    stream 2, batched right after the first main-stream launch that follows stream 2's last backward launch
-    (waiting on its event); the stem's weight gradients stay at the main stream's tail; every conv is in
-    exactly one batch and the finalize waits for every stream's last batch.  join2 also moves the first half
-    of the stem's weight gradients to stream 1, after their last dy producer."""
-    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
-    from mtl_das_pytorch_amd.models import Multi_Classifier
-    monkeypatch.setenv("MDA_WGRAD_STAGE", mode)
-    monkeypatch.setenv("MDA_EARLY_OPT", "0")
-    p = InceptionProgram(Multi_Classifier(), 4, "cpu")
-    ls = p.bwd.launches
-    n_wg = sum(1 for l in ls if l.name == "conv_wgrad")
-    last2 = max(i for i, l in enumerate(ls) if l.stream == 2 and l.name != "conv_wgrad")
-    ai = next(i for i in range(last2 + 1, len(ls)) if ls[i].stream == 0 and ls[i].name != "conv_wgrad")
-    anchor, last2_l = ls[ai], ls[last2]
-    moved = {id(l.owner) for l in ls[:ai] if l.name == "conv_wgrad" and l.stream == 0}
-    tail = {id(l.owner) for l in ls[ai:] if l.name == "conv_wgrad" and l.stream == 0}
-    assert moved and tail
-    p.batch_wgrads()
-    ls = p.bwd.launches
-    b = [l for l in ls if l.name == "wgrad_batched"]
-    assert sum(l.args[2] for l in b) == n_wg
-    s2 = [l for l in b if l.stream == 2]
-    assert s2[0].waits == ("wgstage",) and ls.index(s2[0]) == ls.index(anchor) + 1
-    assert all(ls.index(l) > ls.index(last2_l) for l in s2)
-    if mode == "join2":
-        s1 = [l for l in b if l.stream == 1]
-        assert s1[0].waits == ("wgstage1",) and ls.index(s1[0]) > ls.index(anchor)
-        assert sum(l.args[2] for l in b if l.stream == 0) == len(tail) - len(tail) // 2
-    fin = ls[-1]
-    assert fin.name == "wgrad_finalize" and set(fin.waits) == {f"wgrads_s{s}" for s in {l.stream for l in b}}
-    _check_event_order(p.bwd)
-
-
-def test_wgrad_fanout_structure(monkeypatch):
-    """Opt-in (MDA_WGRAD_FANOUT=1): the main stream's batches are fanned out over the side streams from
-    one fork point."""
-    monkeypatch.setenv("MDA_WGRAD_FANOUT", "1")
+    """All per-conv weight-gradient launches collapse into one launch per (stream, tile config); every conv
+    appears in exactly one job table and one finalize waits for every stream's last batch."""
     p = MTLProgram(MTL_Net(), 32, "cpu")
     n_wg = sum(1 for l in p.bwd.launches if l.name == "conv_wgrad")
-    cfgs = {l.args[0] for l in p.bwd.launches if l.name == "conv_wgrad"}
     p.batch_wgrads()
-    names = [l.name for l in p.bwd.launches]
-    assert "conv_wgrad" not in names
     b = [l for l in p.bwd.launches if l.name == "wgrad_batched"]
-    assert len(b) >= len(cfgs) and sum(l.args[2] for l in b) == n_wg
+    assert sum(l.args[2] for l in b) == n_wg
     fin = p.bwd.launches[-1]
-    assert fin.name == "wgrad_finalize"
-    # one batch per (stream, config); the finalize waits for every stream's last batch.  The main stream's
-    # batches (the step's tail) are fanned out over the streams from one fork point.
-    assert set(fin.waits) == {l.record for l in b if l.record}
-    assert len(fin.waits) == len({(l.stream, l.record.startswith("wgrads_s0_")) for l in b if l.record})
-    main_tail = [l for l in b if l.record and l.record.startswith("wgrads_s0_")]
-    assert len(main_tail) > 1
-    assert all(l.waits == ("wgfork",) for l in b if l.stream != 0 and l.waits)
+    assert fin.name == "wgrad_finalize" and fin.stream == 0
+    fins = [l for l in p.bwd.launches if l.name == "wgrad_finalize"]
+    assert len(fins) == 1 and set(fin.waits) == {f"wgrads_s{s}" for s in {l.stream for l in b}}
     _check_event_order(p.bwd)
 
 
-def test_dgrad_fused_bn_stats_wiring(monkeypatch):
+def test_dgrad_fused_bn_stats_wiring():
     """Single-source elementwise BN tails take their backward sums from the producing dgrad's epilogue
     (Model A: 8 residual-block inner BNs + 4 grouped attention-generator BNs)."""
     from mtl_das_pytorch_amd.engine.inception import InceptionProgram
     from mtl_das_pytorch_amd.models import Multi_Classifier
-    monkeypatch.setenv("MDA_AOL", "0")  # keep the apply-only tails in the program
-    monkeypatch.setenv("MDA_MSBNS", "0")  # single-source tails only (multi-source: test_mtl_program_structure)
     p = MTLProgram(MTL_Net(), 8, "cpu")
     assert p.n_dgrad_bnstats == 12
     fused = [l for l in p.bwd.launches if l.name.startswith("tailbwd") and l.args[3].get("fused") == 2]
@@ -195,38 +107,6 @@ def test_dgrad_fused_bn_stats_wiring(monkeypatch):
         assert p.bwd.launches.index(prod[0]) < p.bwd.launches.index(l)
     c = InceptionProgram(Multi_Classifier(), 4, "cpu")
     assert c.n_dgrad_bnstats >= 40
-
-
-def test_apply_on_load_wiring(monkeypatch):
-    """Apply-only BN tails disappear: their conv's dgrad and wgrad read the tail's g / y (same pointers,
-    strides and groups), the dgrad before the wgrad on one stream, sharing one coefficient table; the
-    dgrad also takes over d(gamma) / d(beta).  Event tags the program uses stay recorded."""
-    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
-    from mtl_das_pytorch_amd.models import Multi_Classifier
-    monkeypatch.setenv("MDA_AOL", "1")  # opt-in
-    monkeypatch.setenv("MDA_MSBNS", "1")
-    for p in (MTLProgram(MTL_Net(), 8, "cpu"), InceptionProgram(Multi_Classifier(), 4, "cpu")):
-        ls = p.bwd.launches
-        assert p.n_aol > 0 and p.n_aol <= p.n_dgrad_bnstats
-        dg = [l for l in ls if l.name == "conv_dgrad" and "aol" in l.args[3]]
-        wg = [l for l in ls if l.name == "conv_wgrad" and "aol" in l.args[2]]
-        assert len(dg) == len(wg) == p.n_aol
-        for d in dg:
-            a = d.args[3]["aol"]
-            w = [x for x in wg if x.args[2]["aol"]["coef"] == a["coef"]]
-            assert len(w) == 1 and w[0].stream == d.stream and ls.index(w[0]) > ls.index(d)
-            assert w[0].args[2]["aol"]["g"] == a["g"] and w[0].args[2]["aol"]["y"] == a["y"]
-            assert a["dgamma"] and a["dbeta"] and a["part"]
-        _check_event_order(p.bwd)
-    p = MTLProgram(MTL_Net(), 8, "cpu")
-    # every single-source apply-only tail is folded; the multi-source ones (MDA_MSBNS) stay
-    assert p.n_aol == 12 and not any(l.name.startswith("tailbwd") and l.args[3].get("fused") == 2
-                                     and len(l.args[3]["g"]) == 1 for l in p.bwd.launches)
-    assert p.num_launches()["backward"] == 98 - 12
-    monkeypatch.setenv("MDA_AOL", "pw")
-    c = InceptionProgram(Multi_Classifier(), 4, "cpu")
-    assert 0 < c.n_aol < 43 and all(l.args[3]["KH"] * l.args[3]["KW"] == 1 for l in c.bwd.launches
-                                    if l.name == "conv_dgrad" and "aol" in l.args[3])
 
 
 def test_stem_tap_packing_geometry():
@@ -276,7 +156,7 @@ def test_stream_events_are_recorded_before_they_are_awaited():
 
 def test_merge_wgrad_cfgs_caps_batches_per_stream():
     """After tuning, small weight-gradient config groups are folded into a valid config of the same
-    stream so that each stream's tail holds at most MDA_WGRAD_MAXB batched launches."""
+    stream so that each stream's tail holds at most WGRAD_MAX_BATCHES batched launches."""
     from mtl_das_pytorch_amd.ops.functional import WGRAD_PATCH, WGRAD_TILES
     p = MTLProgram(MTL_Net(), 32, "cpu")
     wg = [l for l in p.bwd.launches if l.name == "conv_wgrad"]
@@ -310,49 +190,3 @@ def test_inception_aux_logits_shape_error():
         m(torch.randn(2, 1, 100, 250))
     with pytest.raises(ValueError, match="4 x 13"):
         InceptionProgram(m, 2, "cpu")
-
-
-@pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
-def test_early_optimizer_partition(model):
-    """Early optimizer (single GPU, MDA_EARLY_OPT=1): every side stream finalizes its convs and then runs Adam + re-pack on the
-    parameters only it produces gradients for; the optimizer phase after the backward covers the rest.
-    Together the segments cover the flat buffer exactly once, conv weights as pack tiles, and an early
-    parameter's gradient is written by no other stream and not in the forward."""
-    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
-    from mtl_das_pytorch_amd.engine.lowering import _grad_offsets
-    from mtl_das_pytorch_amd.engine.core import P
-    from mtl_das_pytorch_amd.models import build_model
-    import os
-    torch.manual_seed(0)
-    m = build_model(model)
-    p = InceptionProgram(m, 8, "cpu") if model == "multi_classifier" else MTLProgram(m, 8, "cpu")
-    os.environ["MDA_EARLY_OPT"] = "1"
-    try:
-        p.batch_wgrads()
-    finally:
-        del os.environ["MDA_EARLY_OPT"]
-    ls = p.bwd.launches
-    early = [l for l in ls if l.name == "adam_early"]
-    assert early and all(l.stream != 0 for l in early)
-    for l in early:  # right after its stream's finalize, carrying the stream's end event
-        i = ls.index(l)
-        assert ls[i - 1].name == "wgrad_finalize" and ls[i - 1].stream == l.stream
-        assert l.record == f"wgrads_s{l.stream}" and l.args[0]["fused"] == 1 and l.args[0]["ticket"] == 0
-    n = p.flat.numel
-    cover = torch.zeros(n, dtype=torch.int32)
-    segs = [sg for st in p.early_segs.values() for sg in st] + p.late_segs
-    for sg in segs:
-        cover[sg["off"]:sg["off"] + sg["n"]] += 1
-    assert torch.all(cover == 1)
-    conv_w = {p.flat.off(mm.weight) for c in p.convs for mm in c.mods}
-    assert {sg["off"] for sg in segs if sg["kind"] == 2} == conv_w
-    gbase = P(p.flat.grads)
-    for st, ss in p.early_segs.items():
-        for sg in ss:
-            if sg["kind"] != 0:
-                continue
-            for l in ls + p.fwd_train.launches:
-                if l.fn is not None and sg["off"] in _grad_offsets(l, gbase, n):
-                    assert l in ls and l.stream == st, (l.name, l.stream, st)
-    late = p.opt["adam"].launches
-    assert len(late) == 1 and late[0].args[0]["ticket"] != 0  # the late launch advances the step counter

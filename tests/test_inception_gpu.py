@@ -16,15 +16,15 @@ def rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
 
-def _setup(B=8, seed=0, p_drop=0.0):
+def _setup(B=8, seed=0, p_drop=0.0, in_channels=1):
     from mtl_das_pytorch_amd.data.synthetic import generate
     from mtl_das_pytorch_amd.engine.inception import InceptionProgram
     from mtl_das_pytorch_amd.models import Multi_Classifier, encode_joint
     torch.manual_seed(seed)
-    model = Multi_Classifier()
+    model = Multi_Classifier(in_channels=in_channels)
     ref = copy.deepcopy(model).cuda()
     prog = InceptionProgram(model, B, "cuda", p_drop=p_drop)
-    X, d, e = generate(2 * B, seed=seed + 1, device="cuda")
+    X, d, e = generate(2 * B, seed=seed + 1, device="cuda", in_channels=in_channels)
     return model, ref, prog, X, encode_joint(d, e)
 
 
@@ -145,27 +145,21 @@ def _nchw(a):
     return t[idx].float().view(a.B, a.H, a.W, a.C).permute(0, 3, 1, 2)
 
 
-@pytest.mark.parametrize("aol", ["0", "1"])
-def test_inception_backward_layer_local(monkeypatch, aol):
+@pytest.mark.parametrize("cin", [1, 2])
+def test_inception_backward_layer_local(cin):
     """Every op's backward against autograd of that single op, fed with the ENGINE's own input activation
     and incoming gradient (the sum of its gradient sources).  This checks the whole backward wiring (the
     concat-slice gradient routing, multi-consumer source lists, pool backward) and every kernel at
-    bf16-rounding precision, independent of the network's error amplification."""
+    bf16-rounding precision, independent of the network's error amplification.  ``cin`` = 2: the 2-channel
+    input of BASELINE's north star (unpacked 3x3/s2 stem over 8 stored channels)."""
     from mtl_das_pytorch_amd.engine.inception import CBR
-    monkeypatch.setenv("MDA_AOL", aol)  # apply-on-load (opt-in) folds the apply-only tails into the convs
-    model, ref, prog, X, labels = _setup(p_drop=0.5)
-    assert (prog.n_aol > 0) == (aol == "1")
+    model, ref, prog, X, labels = _setup(p_drop=0.5, in_channels=cin)
+    assert (prog.stem_pack[0] > 0) == (cin == 1)
     idx = torch.arange(prog.B, device="cuda")
     _engine_step(prog, X, labels, idx)
     prog.flat.sync_module_grads()
     q = lambda t: t.bfloat16().float()
     worst = {}
-    # apply-on-load: dy of these convs is never materialised -- rebuild it from the engine's own
-    # coefficient table exactly as the dgrad / wgrad operand loaders do
-    from mtl_das_pytorch_amd.engine.core import P
-    coefs = {c.data_ptr(): c for c in getattr(prog, "aol_coefs", [])}
-    aol = {l.args[3]["aol"]["y"]: l.args[3]["aol"] for l in prog.bwd.launches
-           if l.name == "conv_dgrad" and "aol" in l.args[3]}
     for op in prog.ops:
         g = sum(_nchw(a) for a in op.out.grad_sources())
         if getattr(op, "nol_from", None) is not None:
@@ -193,12 +187,6 @@ def test_inception_backward_layer_local(monkeypatch, aol):
             dyq = gam.view(1, -1, 1, 1) * inv * (dz - dz.mean((0, 2, 3), keepdim=True)
                                                  - xh * (dz * xh).mean((0, 2, 3), keepdim=True))
             dye = _nchw(op.dy)
-            a = aol.get(P(op.y.t, op.y.off))
-            if a is not None:
-                k = coefs[a["coef"]].view(5, -1, 1, 1)
-                yv = _nchw(op.y)
-                dze = g * ((yv * k[3] + k[4]) > 0)
-                dye = q(k[0] * dze + k[1] * yv + k[2])
             y.backward(dye)  # the conv backward kernels are checked on the engine's own dy
             checks = {"dy": (dye, dyq), "dW": (conv.weight.grad, w.grad),
                       "dgamma": (bn.weight.grad, dgam), "dbeta": (bn.bias.grad, dbet)}

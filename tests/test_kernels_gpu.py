@@ -345,40 +345,6 @@ def test_dgrad_fused_bn_backward_stats(fn, kind, case, cfg):
     assert rel(dy, dy2) < 1e-4 and rel(dg, dg2) < 1e-5 and rel(db, db2) < 1e-5
 
 
-@pytest.mark.parametrize("kind", [0, 1])
-@pytest.mark.parametrize("case", [(4, 17, 42, 16, 16, 3, 1, 1, 8), (2, 9, 21, 48, 32, 3, 2, 1, 11)])
-def test_conv_apply_on_load(fn, kind, case):
-    """Apply-on-load: conv P (input x, output y) -> act(BN(y)) -> conv Q.  Q's dgrad accumulates the BN sums;
-    P's dgrad and wgrad then rebuild dy = BN-tail-backward(g, y) while loading instead of reading the
-    apply-only tail's output.  Against the tail + plain dgrad / wgrad path on the same inputs (the
-    coefficients are summed in fp64 instead of fp32 -> bf16 dy can differ in the last bit)."""
-    B, H, W, C, Cx, k, s, p, wcfg = case
-    g = torch.Generator().manual_seed(40 + kind)
-    Hx, Wx = (H - 1) * s + k - 2 * p, (W - 1) * s + k - 2 * p
-    x = torch.randn(B, Hx, Wx, Cx, generator=g).bfloat16().cuda()
-    y = (torch.randn(B, C, H, W, generator=g) * 2 + 0.3).bfloat16().float().cuda()
-    bn, gamma, beta, *_ = _bn_setup(fn, y, C, seed=kind + 3)
-    wq = (torch.randn(24, C, 3, 3, generator=g) / math.sqrt(9 * C)).bfloat16().float().cuda()
-    wp = (torch.randn(C, Cx, k, k, generator=g) / math.sqrt(Cx * k * k)).bfloat16().float().cuda()
-    go = torch.randn(B, H, W, 24, generator=g).bfloat16().cuda()
-    yb = nhwc(y).bfloat16()
-    part = torch.zeros(NREP, 3, C, device="cuda", dtype=torch.float64)
-    gx = fn.conv2d_dgrad(go, wq, (H, W), stride=1, padding=1, bn_stats=(yb, bn, part, kind))
-    dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
-    dy, _, _ = fn.bn_tail_backward(kind, yb, bn, [gx], dg, db, part=part)
-    ref_dx = fn.conv2d_dgrad(dy, wp, (Hx, Wx), stride=s, padding=p)
-    ref_dw = fn.conv2d_wgrad(x, dy, wp.shape, stride=s, padding=p)
-    coef = torch.full((5, C), float("nan"), device="cuda")
-    dg2, db2 = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
-    dx = fn.conv2d_dgrad(yb, wp, (Hx, Wx), stride=s, padding=p, aol=(gx, yb, bn, part, coef, dg2, db2, kind))
-    assert torch.isfinite(coef).all()
-    assert rel(dx, ref_dx) < 2e-3
-    assert rel(dg2, dg) < 1e-5 and rel(db2, db) < 1e-5
-    for cfg in (None, wcfg):
-        dw = fn.conv2d_wgrad(x, yb, wp.shape, stride=s, padding=p, cfg=cfg, aol=(gx, yb, coef, kind))
-        assert rel(dw, ref_dw) < 2e-3, cfg
-
-
 @pytest.mark.parametrize("fused", [False, True])
 def test_bn_residual_projection(fn, fused):
     g = torch.Generator().manual_seed(20)

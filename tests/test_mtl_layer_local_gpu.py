@@ -8,6 +8,10 @@ its gradient sources -- and compared per tensor with fp32 PyTorch math at tolera
 rounding, independent of the network's error amplification at init.  The program runs at the bench's
 batch (32) with the tuned kernel configs the bench uses (LDS-staged convs, split-K, fused statistics,
 normalise-on-load).  Reference: model/modelA_MTL.py:7-174.
+
+Parametrized over the input channels: 1 (the reference; the stem runs as a 1 x 7 conv over 7 packed taps)
+and 2 (BASELINE's 2-channel north star, ``--in_channels 2``: gather of two channels into the 8-channel
+stored input, the unpacked 7x7 stem at K = 392 padded to 416 and its weight gradient / finalize).
 """
 import pytest
 import torch
@@ -50,8 +54,8 @@ def bn_backward(dz, y, bn, z=0):
     return dy, (dz * xh).sum((0, 2, 3)), dz.sum((0, 2, 3))
 
 
-@pytest.fixture(scope="module")
-def engine_step():
+@pytest.fixture(scope="module", params=[1, 2], ids=["cin1", "cin2"])
+def engine_step(request):
     from mtl_das_pytorch_amd.data.synthetic import generate
     from mtl_das_pytorch_amd.engine.mtl import MTLProgram
     from mtl_das_pytorch_amd.engine.tune import autotune_program
@@ -64,10 +68,12 @@ def engine_step():
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.manual_seed(0)
     B = 32
-    model = MTL_Net()
+    cin = request.param
+    model = MTL_Net(in_channels=cin)
     prog = MTLProgram(model, B, "cuda")
+    assert (prog.stem_pack[0] > 0) == (cin == 1)
     autotune_program(prog, measure=False)  # the bench's tuned kernel configs
-    X, d, e = generate(B, seed=11, device="cuda")
+    X, d, e = generate(B, seed=11, device="cuda", in_channels=cin)
     labels = torch.stack([d, e], 1)
     idx = torch.arange(B, device="cuda")
     prog.opt["pack"].run()
@@ -213,6 +219,9 @@ def test_mtl_backward_layer_local(engine_step):
     dy0, dgam, dbet = bn_backward(sources(0) * ((y0 * sc + sh) > 0), y0, prog.bn1)
     chk("dy", "conv1 tail dy", nchw(prog.dy0), dy0)
     bn_grads_check(chk, "conv1.1", prog.bn1, 0, dgam, dbet)
+    if not prog.stem_pack[0]:  # the gathered NHWC input: the dataset rows, bf16, channels padded to 8 with 0
+        xin = prog.x.float()
+        assert torch.equal(xin[..., :X.shape[1]], q(X).permute(0, 2, 3, 1)) and not xin[..., X.shape[1]:].any()
     conv_check(chk, "conv1.0", prog.conv1, 0, q(X), nchw(prog.dy0))
 
     # ---- head: d loss / d A4 = w_t (softmax - onehot) / (B * group size * HW), broadcast per channel group

@@ -1,0 +1,45 @@
+"""The RCCL collective path executed on one MI355X: a 1-rank RCCL process group
+(MDA_DIST_BACKEND=nccl, WORLD_SIZE=1) carries bench.py's DP step -- per-bucket backward graphs with
+asynchronous RCCL all-reduces -- and graph-captured SyncBN.  Multi-rank correctness is covered by the gloo
+tests (tests/test_dp_engine_gpu.py, tests/test_dist.py); this one proves the RCCL-specific code: the
+communicator, stream-ordered collectives, Work.wait stream semantics, barrier(device_ids) and collective
+capture inside a HIP graph."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _worker(model):
+    env = dict(os.environ, MDA_DIST_BACKEND="nccl", OMP_NUM_THREADS="4")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MDA_SINGLE_DEVICE"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_worker.py"), model], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    res = json.loads(line)
+    print(json.dumps(res, indent=1))
+    return res
+
+
+@pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
+def test_rccl_one_rank_dp_and_syncbn(model):
+    res = _worker(model)
+    assert res["enabled"] and res["backend"] == "nccl" and res["world"] == 1
+    nbk = 4 if model == "multi_classifier" else 2
+    for b in (1, nbk):
+        r = res[f"dp{b}"]
+        assert r["buckets"] == b
+        assert all(r["bitwise"].values()), r  # 1-rank RCCL sums are exact: same bits as no collective
+    s = res["syncbn"]
+    assert s["collectives_per_step"] > 40  # one per BN forward + one per BN backward
+    assert "train_full" in s["graphs"]  # SyncBN stays on the single-graph step: collectives captured
+    assert all(s["graph_eq_eager"].values()), s
+    assert s["rel_vs_plain"]["bn_mean"] < 1e-3 and s["rel_vs_plain"]["params"] < 1e-3, s
+    assert res["misc"]["metrics_ok"] and res["misc"]["average_ok"]

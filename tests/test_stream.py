@@ -155,3 +155,29 @@ def test_disk_stream_peak_rss_below_dataset_size(tmp_path):
     print({k: v / 2 ** 20 for k, v in growth.items()}, "dataset MB", ds_bytes / 2 ** 20)
     assert growth[False] < ds_bytes / 2, growth  # ring + activations only
     assert growth[True] - growth[False] > ds_bytes * 0.8, growth
+
+
+def test_native_loader_rejects_transposed_and_non_regular_files(tmp_path):
+    """A variable with the right numel but other dims (250 x 100 for a 100 x 250 slot) is rejected by the
+    native batch loader -- it would land transposed -- and a directory entry returns an error status instead
+    of crashing a worker thread; the streaming dataset then raises on the scipy fallback's shape check."""
+    import scipy.io as sio
+    from mtl_das_pytorch_amd.data.mat_dataset import DatasetDisk
+    from mtl_das_pytorch_amd.data.stream import DiskBatchStream
+    L = _lib()
+    rng = np.random.default_rng(5)
+    good, bad = str(tmp_path / "good.mat"), str(tmp_path / "bad.mat")
+    sio.savemat(good, {"data": rng.standard_normal((100, 250))})
+    sio.savemat(bad, {"data": rng.standard_normal((250, 100))})
+    (tmp_path / "adir").mkdir()
+    ld = L.MatBatchLoader([good, bad, str(tmp_path / "adir")], "data", [100, 250], 2)
+    out = torch.empty(3, 100 * 250)
+    st = ld.load([0, 1, 2], out.data_ptr())
+    assert st[0] == 0 and st[1] != 0 and st[2] != 0
+    assert L.mat_read(str(tmp_path / "adir"), "data", out.data_ptr(), 100 * 250) != 0
+    ds = DatasetDisk([good, bad], [[0, 0], [1, 1]])
+    s = DiskBatchStream(ds, batch=2, device="cpu", ring=2)
+    with pytest.raises(ValueError, match="shape"):
+        for _ in s.batches([[0, 1]]):
+            pass
+    s.close()
