@@ -51,6 +51,167 @@ constexpr int LDS_WAM[8] = {2, 2, 2, 2, 2, 2, 2, 4};
 // index would copy the argument struct to scratch memory).
 #define PSEL(f) (p == 0 ? pl.ph[0].f : p == 1 ? pl.ph[1].f : p == 2 ? pl.ph[2].f : pl.ph[3].f)
 
+// Cross-block split-K reduction and epilogue of one output tile, shared by the register-staged kernel
+// (conv_lds_kernel) and the LDS-DMA kernel (conv_glds_kernel).  Lane: pixel l16 of each fragment,
+// channels 4*kgl .. +3 of each 16-channel fragment.
+struct TileCtx {
+  int tid, lane, wid, wn, wm, l16, kgl, S, split, nt, ntn, z, mbase, nbase, Mq, HWq, Wq, oy0, ox0, bN;
+};
+
+template <bool FWD, bool BNS, int BM, int BN, int WAM, int WM, int WN, int FN, int FM>
+DEV void tile_epilogue(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f32x4 (&acc)[FN][FM], float* s_st,
+                       const float* s_k, int* s_flag) {
+  // ---- cross-block split of K: deterministic last-arriver reduction
+  if (t.S > 1) {
+    const int64_t tile = ((int64_t)t.z * gridDim.x + blockIdx.x) * t.ntn + t.nt;
+    float4* slab = reinterpret_cast<float4*>(a.ws) + tile * t.S * (BM * BN / 4);
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+        slab[(int64_t)t.split * (BM * BN / 4) + ((t.wid * FN + i) * FM + f) * 64 + t.lane] =
+            make_float4(acc[i][f][0], acc[i][f][1], acc[i][f][2], acc[i][f][3]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t.tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned tk = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_flag[0] = tk == (unsigned)(t.S - 1);
+    }
+    __syncthreads();
+    if (!s_flag[0]) return;
+    if (t.tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reusable next launch
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < t.S; ++s) {
+          const float4 u = slab[(int64_t)s * (BM * BN / 4) + ((t.wid * FN + i) * FM + f) * 64 + t.lane];
+          v[0] += u.x; v[1] += u.y; v[2] += u.z; v[3] += u.w;
+        }
+        acc[i][f] = v;
+      }
+  }
+
+  // ---- epilogue (lane: pixel l16 of each fragment, channels 4*kgl .. +3)
+  int orow[FM];
+  bool pv[FM];
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    const int m = t.mbase + t.wm * WM + f * 16 + t.l16;
+    pv[f] = m < t.Mq;
+    const int mm = pv[f] ? m : 0;
+    const int b = mm / t.HWq, r = mm - b * t.HWq;
+    const int i = r / t.Wq, jj = r - i * t.Wq;
+    orow[f] = (b * a.Ho + t.oy0 + i * pl.qy) * a.Wo + t.ox0 + jj * pl.qx;
+  }
+  const bool want_stats = FWD && a.stats != nullptr;
+  const bool want_red = want_stats || BNS;
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int n0 = t.nbase + t.wn * WN + i * 16 + 4 * t.kgl;
+    const int cl = t.wn * WN + i * 16 + 4 * t.kgl;
+    const bool nok = n0 < a.N;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (FWD && a.bias && nok) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[r] = a.bias[a.bgs * t.z + n0 + r];
+    }
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < FM; ++f) {
+      if (!(nok && pv[f])) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] + bias[r];
+      if (FWD) {
+        bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + a.ogs * t.z + (int64_t)orow[f] * a.ldo + n0;
+        uint2 w;
+        w.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        w.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(o) = w;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { s[r] += v[r]; ss[r] += v[r] * v[r]; }
+      } else {
+        float* o = reinterpret_cast<float*>(a.out) + a.ogs * t.z + (int64_t)orow[f] * a.ldo + n0;
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        if (BNS && n0 < t.bN) {  // dz of the BN tail this gradient feeds, and its statistics
+          const uint2 u = *reinterpret_cast<const uint2*>(a.by + a.bygs * t.z + (int64_t)orow[f] * a.ldby + n0);
+          const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                               __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+          uint2 q = make_uint2(0, 0);
+          if (a.bkind == ADD_RELU) q = *reinterpret_cast<const uint2*>(a.br + a.brgs * t.z + (int64_t)orow[f] * a.ldbr + n0);
+          const float rv[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                               __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float tv = yv[r] * s_k[cl + r] + s_k[BN + cl + r];
+            float dz = v[r], xh2 = 0.f;
+            if (a.bkind == ACT_RELU) {
+              dz = tv > 0.f ? dz : 0.f;
+            } else if (a.bkind == ACT_SIGMOID) {
+              const float sg = sigmoidf_(tv);
+              dz *= sg * (1.f - sg);
+            } else if (a.bkind == ADD_RELU) {
+              float rr = rv[r];
+              if (a.br_bn) {
+                xh2 = (rr - s_k[6 * BN + cl + r]) * s_k[7 * BN + cl + r];
+                rr = rr * s_k[4 * BN + cl + r] + s_k[5 * BN + cl + r];
+              }
+              dz = (tv + rr) > 0.f ? dz : 0.f;
+            }
+            const float xh = (yv[r] - s_k[2 * BN + cl + r]) * s_k[3 * BN + cl + r];
+            s[r] += dz;
+            ss[r] += dz * xh;
+            s2[r] += dz * xh2;
+          }
+        }
+      }
+    }
+    if (want_red) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // the 16 pixels of a lane row -> lane 15 (DPP, common.h)
+        s[r] = row16_sum(s[r]);
+        ss[r] = row16_sum(ss[r]);
+        if (BNS) s2[r] = row16_sum(s2[r]);
+      }
+      if (t.l16 == 15) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s_st[(t.wm * BN + cl + r) * 3 + 0] = s[r];
+          s_st[(t.wm * BN + cl + r) * 3 + 1] = ss[r];
+          s_st[(t.wm * BN + cl + r) * 3 + 2] = s2[r];
+        }
+      }
+    }
+  }
+  if (want_red) {
+    __syncthreads();
+    const int rep = blockIdx.x % (BNS ? a.bbn.pnrep : a.stats_nrep);
+    double* dst = BNS ? a.bpart : a.stats;
+    const int rows = BNS ? 3 : 2, nrow = BNS && a.br_bn ? 3 : 2, nlim = BNS ? t.bN : a.N;
+    const int64_t gb = BNS ? (a.bpgs < 0 ? (int64_t)t.z * NREP * 3 * t.bN : (int64_t)t.z * a.bpgs)
+                           : (int64_t)t.z * NREP * 2 * a.N;
+    for (int q = t.tid; q < BN * 3; q += 256) {
+      const int c = q / 3, which = q - c * 3;
+      const int n = t.nbase + c;
+      if (n < nlim && which < nrow) {
+        float v = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < WAM; ++w2) v += s_st[(w2 * BN + c) * 3 + which];
+        atomicAdd(dst + gb + ((int64_t)rep * rows + which) * nlim + n, (double)v);
+      }
+    }
+  }
+}
+
 template <int MODE, int BM, int BN, int WAM, int KC>
 __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
   constexpr int WAN = 4 / WAM;
@@ -252,155 +413,8 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
     __syncthreads();
   }
 
-  // ---- cross-block split of K: deterministic last-arriver reduction
-  if (S > 1) {
-    const int64_t tile = ((int64_t)z * gridDim.x + blockIdx.x) * ntn + nt;
-    float4* slab = reinterpret_cast<float4*>(a.ws) + tile * S * (BM * BN / 4);
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int f = 0; f < FM; ++f)
-        slab[(int64_t)split * (BM * BN / 4) + ((wid * FN + i) * FM + f) * 64 + lane] =
-            make_float4(acc[i][f][0], acc[i][f][1], acc[i][f][2], acc[i][f][3]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned t = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_flag[0] = t == (unsigned)(S - 1);
-    }
-    __syncthreads();
-    if (!s_flag[0]) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reusable next launch
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int f = 0; f < FM; ++f) {
-        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < S; ++s) {
-          const float4 t = slab[(int64_t)s * (BM * BN / 4) + ((wid * FN + i) * FM + f) * 64 + lane];
-          v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
-        }
-        acc[i][f] = v;
-      }
-  }
-
-  // ---- epilogue (lane: pixel l16 of each fragment, channels 4*kgl .. +3)
-  int orow[FM];
-  bool pv[FM];
-#pragma unroll
-  for (int f = 0; f < FM; ++f) {
-    const int m = mbase + wm * WM + f * 16 + l16;
-    pv[f] = m < Mq;
-    const int mm = pv[f] ? m : 0;
-    const int b = mm / HWq, r = mm - b * HWq;
-    const int i = r / Wq, jj = r - i * Wq;
-    orow[f] = (b * a.Ho + oy0 + i * pl.qy) * a.Wo + ox0 + jj * pl.qx;
-  }
-  const bool want_stats = FWD && a.stats != nullptr;
-  const bool want_red = want_stats || BNS;
-#pragma unroll
-  for (int i = 0; i < FN; ++i) {
-    const int n0 = nbase + wn * WN + i * 16 + 4 * kgl;
-    const int cl = wn * WN + i * 16 + 4 * kgl;
-    const bool nok = n0 < a.N;
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    if (FWD && a.bias && nok) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bias[r] = a.bias[a.bgs * z + n0 + r];
-    }
-    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int f = 0; f < FM; ++f) {
-      if (!(nok && pv[f])) continue;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][f][r] + bias[r];
-      if (FWD) {
-        bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + a.ogs * z + (int64_t)orow[f] * a.ldo + n0;
-        uint2 w;
-        w.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        w.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(o) = w;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { s[r] += v[r]; ss[r] += v[r] * v[r]; }
-      } else {
-        float* o = reinterpret_cast<float*>(a.out) + a.ogs * z + (int64_t)orow[f] * a.ldo + n0;
-        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-        if (BNS && n0 < bN) {  // dz of the BN tail this gradient feeds, and its statistics
-          const uint2 u = *reinterpret_cast<const uint2*>(a.by + a.bygs * z + (int64_t)orow[f] * a.ldby + n0);
-          const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                               __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
-          uint2 q = make_uint2(0, 0);
-          if (a.bkind == ADD_RELU) q = *reinterpret_cast<const uint2*>(a.br + a.brgs * z + (int64_t)orow[f] * a.ldbr + n0);
-          const float rv[4] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
-                               __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u)};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float t = yv[r] * s_k[cl + r] + s_k[BN + cl + r];
-            float dz = v[r], xh2 = 0.f;
-            if (a.bkind == ACT_RELU) {
-              dz = t > 0.f ? dz : 0.f;
-            } else if (a.bkind == ACT_SIGMOID) {
-              const float sg = sigmoidf_(t);
-              dz *= sg * (1.f - sg);
-            } else if (a.bkind == ADD_RELU) {
-              float rr = rv[r];
-              if (a.br_bn) {
-                xh2 = (rr - s_k[6 * BN + cl + r]) * s_k[7 * BN + cl + r];
-                rr = rr * s_k[4 * BN + cl + r] + s_k[5 * BN + cl + r];
-              }
-              dz = (t + rr) > 0.f ? dz : 0.f;
-            }
-            const float xh = (yv[r] - s_k[2 * BN + cl + r]) * s_k[3 * BN + cl + r];
-            s[r] += dz;
-            ss[r] += dz * xh;
-            s2[r] += dz * xh2;
-          }
-        }
-      }
-    }
-    if (want_red) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {  // the 16 pixels of a lane row -> lane 15 (DPP, common.h)
-        s[r] = row16_sum(s[r]);
-        ss[r] = row16_sum(ss[r]);
-        if (BNS) s2[r] = row16_sum(s2[r]);
-      }
-      if (l16 == 15) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s_st[(wm * BN + cl + r) * 3 + 0] = s[r];
-          s_st[(wm * BN + cl + r) * 3 + 1] = ss[r];
-          s_st[(wm * BN + cl + r) * 3 + 2] = s2[r];
-        }
-      }
-    }
-  }
-  if (want_red) {
-    __syncthreads();
-    const int rep = blockIdx.x % (BNS ? a.bbn.pnrep : a.stats_nrep);
-    double* dst = BNS ? a.bpart : a.stats;
-    const int rows = BNS ? 3 : 2, nrow = BNS && a.br_bn ? 3 : 2, nlim = BNS ? bN : a.N;
-    const int64_t gb = BNS ? (a.bpgs < 0 ? (int64_t)z * NREP * 3 * bN : (int64_t)z * a.bpgs)
-                           : (int64_t)z * NREP * 2 * a.N;
-    for (int q = tid; q < BN * 3; q += 256) {
-      const int c = q / 3, which = q - c * 3;
-      const int n = nbase + c;
-      if (n < nlim && which < nrow) {
-        float v = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < WAM; ++w2) v += s_st[(w2 * BN + c) * 3 + which];
-        atomicAdd(dst + gb + ((int64_t)rep * rows + which) * nlim + n, (double)v);
-      }
-    }
-  }
+  const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, S, split, nt, ntn, z, mbase, nbase, Mq, HWq, Wq, oy0, ox0, bN};
+  tile_epilogue<FWD, BNS, BM, BN, WAM, WM, WN, FN, FM>(a, pl, tc, acc, s_st, s_k, s_flag);
 }
 
 #undef PSEL

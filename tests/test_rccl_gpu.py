@@ -41,5 +41,8 @@ def test_rccl_one_rank_dp_and_syncbn(model):
     assert s["collectives_per_step"] > 40  # one per BN forward + one per BN backward
     assert "train_full" in s["graphs"]  # SyncBN stays on the single-graph step: collectives captured
     assert all(s["graph_eq_eager"].values()), s
-    assert s["rel_vs_plain"]["bn_mean"] < 1e-3 and s["rel_vs_plain"]["params"] < 1e-3, s
+    # one step vs plain BN: forward bitwise (BN statistics); backward summation order amplified by the chaotic
+    # network at init (measured: A 0 everywhere, C grads 1.1e-2)
+    r = s["rel_vs_plain"]
+    assert r["bn_mean"] == 0.0 and r["bn_var"] == 0.0 and r["grads"] < 5e-2 and r["params"] < 1e-3, s
     assert res["misc"]["metrics_ok"] and res["misc"]["average_ok"]
