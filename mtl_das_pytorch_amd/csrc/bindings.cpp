@@ -100,7 +100,7 @@ py::tuple conv_workspace(int mode, int cfg, int G, py::dict d) {
   ConvArgs a = parse_conv(mode, d);
   int64_t ws = 0, nt = 0;
   int rc = 0;
-  if (cfg >= CONV_DEEP_CFG0) rc = cfg < CONV_DEEP_CFG0 + CONV_DEEP_NCFG ? 0 : -1;
+  if (cfg >= CONV_DEEP_CFG0 && cfg < CONV_DEEP_CFG0 + CONV_DEEP_NCFG) rc = 0;
   else if (cfg >= CONV_LDS_CFG0) rc = conv_lds_workspace(mode, a, G, cfg, ws, nt);
   return py::make_tuple(rc, ws, nt);
 }
@@ -339,6 +339,8 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.attr("CONV_LDS_NCFG") = CONV_LDS_NCFG;
   m.attr("CONV_DEEP_CFG0") = CONV_DEEP_CFG0;
   m.attr("CONV_DEEP_NCFG") = CONV_DEEP_NCFG;
+  m.attr("CONV_GLDS_CFG0") = CONV_GLDS_CFG0;
+  m.attr("CONV_GLDS_NCFG") = CONV_GLDS_NCFG;
   m.def("wgrad", &wgrad);
   m.def("wgrad_finalize", &wgrad_finalize);
   m.def("tail_fwd", &tail_fwd);

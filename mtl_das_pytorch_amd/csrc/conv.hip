@@ -596,18 +596,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob*
 }
 
 // ------------------------------------------------------------------------------------------------
-// Patch weight gradient for 3x3 / stride 1 / pad 1 convolutions (tile configs 12-15).  The im2col operand
-// of a 3x3 conv re-reads every input pixel 9 times; here a block stages a strip of PR output rows' INPUT
-// rows (PR + 2 rows with halo, CB channels) once in LDS and forms all 9 taps' MFMA operands from it with
+// Patch weight gradient for 3x3 / stride 1 convolutions, padding 1 ("same") or 0 ("valid") (tile configs
+// 12-19).  The im2col operand of a 3x3 conv re-reads every input pixel 9 times; here a block stages a strip
+// of R output rows' INPUT rows (R + 2 rows with halo, CB channels) once in LDS and forms all 9 taps' MFMA operands from it with
 // shifted transposed reads -- the input is read once per (strip, channel slice) instead of once per
 // (tap, K tile).  Output rows are padded to a multiple of 8 pixels (Wo8) so that each 8-pixel MFMA row
 // group stays inside one image row; the pad pixels carry dy = 0.  Work unit = (image, strip); split s of
 // a job covers units [s * m_per_split, ...).  Tile = (TN output channels) x (all 9 taps x CB input
 // channels), written to the same [split][Npad][Kpad] slab layout as the im2col kernel (k = tap*Cs + ci).
-constexpr int PATCH_R = 4;  // output rows per strip
-template <int TN, int CB, int W8>
+// R = 2 strips for the wide (W8 = 128) stem maps keep the staging registers and LDS within 2 blocks per CU.
+template <int TN, int CB, int W8, int R>
 DEV void wgrad_patch_block(const WgradArgs& a, const int tile, const int split, const int z) {
-  constexpr int R = PATCH_R, TAPS = 9;
+  constexpr int TAPS = 9;
   constexpr int CBP = CB + 8, LDY = TN + 8, WP = W8 + 2;
   constexpr int FN = TN / 16, FC = CB / 16, NFR = FN * TAPS * FC, FPW = (NFR + 3) / 4;
   constexpr int NPI = (R + 2) * WP * (CB / 8), NDI = R * W8 * (TN / 8);
@@ -620,7 +620,7 @@ DEV void wgrad_patch_block(const WgradArgs& a, const int tile, const int split, 
   const int tn = tile / ncs, tcs = tile - tn * ncs;
   const int n0 = tn * TN, c0 = tcs * CB;
   const int Wo8 = (a.Wo + 7) & ~7;
-  const int wpr = Wo8 + 2;  // staged input columns: iw = -1 .. Wo8
+  const int wpr = Wo8 + 2;  // staged input columns: iw = -pw .. Wo8 + 1 - pw
   const int nstrip = (a.Ho + R - 1) / R;
   const int U = a.B * nstrip;
   const int ubeg = split * a.m_per_split, uend = min(U, ubeg + a.m_per_split);
@@ -650,7 +650,7 @@ DEV void wgrad_patch_block(const WgradArgs& a, const int tile, const int split, 
       if (v < npi) {
         const int cg = v % (CB / 8), q = v / (CB / 8);
         const int j = q / wpr, c = q - j * wpr;
-        const int ih = oh0 - 1 + j, iw = c - 1;
+        const int ih = oh0 - a.ph + j, iw = c - a.pw;
         if (ih >= 0 && ih < a.Hi && iw >= 0 && iw < a.Wi) {
           rp[i] = *reinterpret_cast<const uint4*>(xz + ((int64_t)(b * a.Hi + ih) * a.Wi + iw) * ldx + cg * 8);
           pok |= 1u << i;
@@ -744,12 +744,12 @@ DEV void wgrad_patch_block(const WgradArgs& a, const int tile, const int split, 
   }
 }
 
-template <int TN, int CB, int W8>
+template <int TN, int CB, int W8, int R>
 __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(WgradArgs a) {
-  wgrad_patch_block<TN, CB, W8>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  wgrad_patch_block<TN, CB, W8, R>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
-template <int TN, int CB, int W8>
+template <int TN, int CB, int W8, int R>
 __global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const WgradJob* __restrict__ jobs, int nj) {
   int lo = 0, hi = nj - 1;
   while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
@@ -757,7 +757,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const Wgr
   const int local = (int)((int64_t)blockIdx.x - J.block0);
   const int per_z = J.ntiles * J.a.splits;
   const int z = local / per_z, r = local - z * per_z;
-  wgrad_patch_block<TN, CB, W8>(J.a, r % J.ntiles, r / J.ntiles, z);
+  wgrad_patch_block<TN, CB, W8, R>(J.a, r % J.ntiles, r / J.ntiles, z);
 }
 
 // Sums the split-M partial slabs of many convolutions into the flat fp32 gradient buffer (deterministic,
@@ -906,7 +906,7 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
 }
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
-  if (cfg >= CONV_LDS_CFG0 && cfg < CONV_DEEP_CFG0) {  // LDS-staged kernels (conv_lds.hip)
+  if ((cfg >= CONV_LDS_CFG0 && cfg < CONV_DEEP_CFG0) || cfg >= CONV_GLDS_CFG0) {  // LDS-staged kernels (conv_lds.hip)
     const int m = mode == MODE_FWD ? (a.nol ? MODE_FWD_NOL : MODE_FWD) : (a.bpart ? MODE_DGRAD_BNS : MODE_DGRAD);
     return launch_conv_lds(m, a, G, cfg, st);
   }
@@ -925,23 +925,29 @@ int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
   case 4: X(16, 64, 128) case 5: X(16, 32, 256) case 6: X(32, 32, 256) case 7: X(64, 32, 64)        \
   case 8: X(16, 192, 64) case 9: X(16, 128, 64) case 10: X(32, 192, 64) case 11: X(32, 320, 32)
 
-// Patch configs 12-15 (TN, CB, max padded output width); keep in sync with ops/functional.py WGRAD_PATCH.
-#define WGRAD_PATCH_CASES(X) case 12: X(16, 16, 88) case 13: X(32, 16, 88) case 14: X(32, 32, 48) case 15: X(64, 32, 24)
+// Patch configs 12-19 (TN, CB, max padded output width, strip rows); keep in sync with ops/functional.py
+// WGRAD_PATCH.
+#define WGRAD_PATCH_CASES(X)                                                                       \
+  case 12: X(16, 16, 88, 4) case 13: X(32, 16, 88, 4) case 14: X(32, 32, 48, 4) case 15: X(64, 32, 24, 4) \
+  case 16: X(32, 32, 128, 2) case 17: X(64, 32, 128, 2) case 18: X(64, 16, 128, 2) case 19: X(32, 16, 128, 2)
 
-int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8) {
-  static const int tn[] = {16, 32, 32, 64}, cb[] = {16, 16, 32, 32}, w8[] = {88, 88, 48, 24};
-  if (cfg < WGRAD_PATCH_CFG0 || cfg >= WGRAD_PATCH_CFG0 + 4) return -1;
-  TN = tn[cfg - WGRAD_PATCH_CFG0]; CB = cb[cfg - WGRAD_PATCH_CFG0]; W8 = w8[cfg - WGRAD_PATCH_CFG0];
+int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8, int& R) {
+  static const int tn[] = {16, 32, 32, 64, 32, 64, 64, 32}, cb[] = {16, 16, 32, 32, 32, 32, 16, 16};
+  static const int w8[] = {88, 88, 48, 24, 128, 128, 128, 128}, rr[] = {4, 4, 4, 4, 2, 2, 2, 2};
+  if (cfg < WGRAD_PATCH_CFG0 || cfg >= WGRAD_PATCH_CFG0 + WGRAD_PATCH_NCFG) return -1;
+  const int k = cfg - WGRAD_PATCH_CFG0;
+  TN = tn[k]; CB = cb[k]; W8 = w8[k]; R = rr[k];
   return 0;
 }
 
 int wgrad_ntiles(int cfg, const WgradArgs& a) {
-  int TN, TK, CB, W8;
-  if (!wgrad_patch_shape(cfg, TN, CB, W8)) {
+  int TN, TK, CB, W8, R;
+  if (!wgrad_patch_shape(cfg, TN, CB, W8, R)) {
     const int Wo8 = (a.Wo + 7) & ~7;
     const bool seg_ok = a.src.C1 == 0 || a.src.C0 % CB == 0;
-    if (a.KH != 3 || a.KW != 3 || a.sh != 1 || a.sw != 1 || a.ph != 1 || a.pw != 1 || a.Hi != a.Ho ||
-        a.Wi != a.Wo || a.Cs % CB || Wo8 > W8 || !seg_ok || a.Kpad < 9 * a.Cs)
+    if (a.KH != 3 || a.KW != 3 || a.sh != 1 || a.sw != 1 || a.ph > 1 || a.pw > 1 || a.ph < 0 || a.pw < 0 ||
+        a.Ho != a.Hi + 2 * a.ph - 2 || a.Wo != a.Wi + 2 * a.pw - 2 || a.Cs % CB || Wo8 > W8 || (R * Wo8) % 32 ||
+        !seg_ok || a.Kpad < 9 * a.Cs)
       return -2;
     return ((a.Npad + TN - 1) / TN) * (a.Cs / CB);
   }
@@ -953,8 +959,8 @@ int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st) {
   if (cfg >= WGRAD_PATCH_CFG0) {
     const int nt = wgrad_ntiles(cfg, a);
     if (nt < 0) return nt;
-#define LAUNCH_WGP(TN, CB, W8)                                                                      \
-  hipLaunchKernelGGL((conv_wgrad_patch_kernel<TN, CB, W8>), dim3(nt, a.splits, G), dim3(256), 0, st, a); \
+#define LAUNCH_WGP(TN, CB, W8, R)                                                                      \
+  hipLaunchKernelGGL((conv_wgrad_patch_kernel<TN, CB, W8, R>), dim3(nt, a.splits, G), dim3(256), 0, st, a); \
   break;
     switch (cfg) {
       WGRAD_PATCH_CASES(LAUNCH_WGP)
@@ -991,8 +997,8 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
   if (nblocks <= 0) return 0;
   dim3 grid((unsigned)nblocks);
   if (cfg >= WGRAD_PATCH_CFG0) {
-#define LAUNCH_WGPB(TN, CB, W8)                                                                                 \
-  hipLaunchKernelGGL((conv_wgrad_patch_batched_kernel<TN, CB, W8>), grid, dim3(256), 0, st, d_jobs, nj); \
+#define LAUNCH_WGPB(TN, CB, W8, R)                                                                              \
+  hipLaunchKernelGGL((conv_wgrad_patch_batched_kernel<TN, CB, W8, R>), grid, dim3(256), 0, st, d_jobs, nj); \
   break;
     switch (cfg) {
       WGRAD_PATCH_CASES(LAUNCH_WGPB)

@@ -417,14 +417,228 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
   tile_epilogue<FWD, BNS, BM, BN, WAM, WM, WN, FN, FM>(a, pl, tc, acc, s_st, s_k, s_flag);
 }
 
+// ================================================================================================
+// LDS-DMA variant (cfg >= CONV_GLDS_CFG0): the operand tiles go global -> LDS with
+// global_load_lds_dwordx4 (no register hop, no ds_write pass), through a 3-stage ring of LDS buffers with
+// one raw s_barrier per K chunk and a counted vmcnt that keeps the next chunk's DMAs in flight ACROSS the
+// barrier (a __syncthreads() would emit vmcnt(0) and drain them).
+//
+// LDS image of an operand chunk (KC = 64): [row][8 k-groups] with 128-byte rows; k-group g of row r sits
+// in 16-byte slot g ^ ((r >> 1) & 7).  An LDS-DMA instruction writes 64 lanes x 16 B contiguously (8 rows),
+// so the swizzle is applied on the per-lane SOURCE address (lane l of the instruction fetches k-group
+// (l & 7) ^ ((row >> 1) & 7) of row 8i + (l >> 3)) and again on the fragment read; with it the four 16-lane
+// groups of every ds_read_b128 of a 16x16x32 MFMA fragment (16 rows, one k-group each) hit 16 distinct
+// 16-byte slots of the 256-byte bank row -- conflict-free.  Padding (zero rows / taps outside the image /
+// k beyond K) is a DMA from a 16-byte zero page, so every lane always issues its instruction.
+constexpr int GL_NT = 8;  // tile configs: BM pixels x BN channels, WAM waves along M
+constexpr int GL_BM[GL_NT] = {64, 128, 64, 128, 256, 128, 256, 64};
+constexpr int GL_BN[GL_NT] = {64, 64, 128, 128, 64, 32, 128, 32};
+constexpr int GL_WAM[GL_NT] = {2, 2, 2, 2, 4, 4, 2, 4};
+constexpr int GL_KC = 64, GL_STAGES = 3;
+
+__device__ uint4 g_zero16[4];  // never written: the source of every padding lane
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* glb_vptr;
+
+DEV int gl_swz(int r, int g) { return g ^ ((r >> 1) & 7); }
+
+template <int MODE, int BM, int BN, int WAM>
+__global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a, LdsPlan pl) {
+  constexpr int WAN = 4 / WAM;
+  constexpr int WM = BM / WAM, WN = BN / WAN, FM = WM / 16, FN = WN / 16;
+  static_assert(FM >= 1 && FN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
+  constexpr int KC = GL_KC, NG = KC / 8, NKS = KC / 32, ROWB = KC * 2;  // 128-byte rows
+  constexpr int IA = BN / 32, IB = BM / 32;  // DMA instructions per wave per chunk (8 rows each)
+  static_assert(IA >= 1 && IB >= 1, "tile too small for 4 waves x 8 rows");
+  constexpr int NPER = IA + IB;
+  constexpr int BUF = (BN + BM) * ROWB;  // bytes of one stage
+  constexpr bool BNS = MODE == MODE_DGRAD_BNS;
+  constexpr bool FWD = MODE == MODE_FWD;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* s_tx = reinterpret_cast<int*>(smem + GL_STAGES * BUF);  // input coordinates / channel per k-group
+  int* s_tw = s_tx + pl.ntab;                                  // weight column per k-group
+  float* s_st = reinterpret_cast<float*>(s_tw + pl.ntab);      // [WAM][BN][3] epilogue sums
+  float* s_k = s_st + WAM * BN * 3;                             // BNS: [8][BN] constants
+  int* s_flag = reinterpret_cast<int*>(s_k + (BNS ? 8 * BN : 0));
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, kgl = lane >> 4;
+  const int wn = wid % WAN, wm = wid / WAN;
+  int p = 0;
+#pragma unroll
+  for (int q = 1; q < 4; ++q)
+    if (q < pl.nph && (int)blockIdx.x >= pl.ph[q].m0) p = q;
+  const int oy0 = PSEL(oy0), ox0 = PSEL(ox0), Hq = PSEL(Hq), Wq = PSEL(Wq);
+  const int rh = PSEL(rh), nh = PSEL(nh), rw = PSEL(rw), nw = PSEL(nw), ay = PSEL(ay), ax = PSEL(ax);
+  const int Kp = PSEL(Kp), m0t = PSEL(m0);
+  const int S = pl.splits;
+  const int ntn = (a.N + BN - 1) / BN;
+  const int nt = blockIdx.y / S, split = blockIdx.y - nt * S;
+  const int z = blockIdx.z;
+  const int HWq = Hq * Wq;
+  const int Mq = a.B * HWq;
+  const int mbase = ((int)blockIdx.x - m0t) * BM, nbase = nt * BN;
+  const int nch = Kp / KC;
+  const int cps = (nch + S - 1) / S;
+  const int cb = min(nch, split * cps), ce = min(nch, cb + cps);
+
+  // ---- per-block k-group tables for this split's chunks (as conv_lds_kernel)
+  {
+    const int cs8 = a.Cs >> 3, ntap = nh * nw;
+    const int ng = (ce - cb) * NG;
+    for (int i = tid; i < ng; i += 256) {
+      const int gabs = cb * NG + i;
+      const int t = gabs / cs8;
+      const int c = (gabs - t * cs8) * 8;
+      int ex = 0, ew = -1;
+      if (t < ntap) {
+        const int u = t / nw, v = t - u * nw;
+        const int kh = rh + pl.th * u, kw = rw + pl.tw * v;
+        const int dyo = ay + pl.by * u, dxo = ax + pl.bx * v;
+        const int seg = (a.src.C1 > 0 && c >= a.src.C0) ? 1 : 0;
+        ex = (c - seg * a.src.C0) | ((dyo + 64) << 14) | ((dxo + 64) << 21) | (seg << 28) | (1 << 29);
+        ew = (kh * a.KW + kw) * a.Cs + c;
+      }
+      s_tx[i] = ex;
+      s_tw[i] = ew;
+    }
+  }
+  const int bN = a.bN > 0 ? a.bN : a.N;
+  const int zb = a.bpgs == 0 ? 0 : z;
+  if (BNS) {
+    for (int i = tid; i < BN; i += 256) {
+      const int n = nbase + i;
+      float k[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (n < bN) {
+        bn_channel_bwd(a.bbn, zb, n, k[0], k[1], k[2], k[3]);
+        if (a.br_bn) bn_channel_bwd(a.bbn2, zb, n, k[4], k[5], k[6], k[7]);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s_k[q * BN + i] = k[q];
+    }
+  }
+
+  // ---- per-lane DMA sources: instruction j of wave w covers rows 8 (4j + w) .. +7; this lane fetches
+  // k-group ga / gb (swizzled) of row 8 (4j + w) + (lane >> 3)
+  const bf16_t* wz = a.w + a.wgs * z;
+  const bf16_t* base0 = a.src.p[0] + a.src.gs[0] * z;
+  const bf16_t* base1 = a.src.p[1] ? a.src.p[1] + a.src.gs[1] * z : base0;
+  const int ld0 = a.src.ld[0], ld1 = a.src.ld[1];
+  const void* zero = &g_zero16[0];
+  int an[IA], ga[IA];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int row = 8 * (4 * j + wid) + (lane >> 3);
+    const int n = nbase + row;
+    an[j] = n < a.Npad ? n : -1;
+    ga[j] = gl_swz(row, lane & 7);
+  }
+  int pb[IB], pih[IB], piw[IB], gb[IB];
+#pragma unroll
+  for (int j = 0; j < IB; ++j) {
+    const int row = 8 * (4 * j + wid) + (lane >> 3);
+    const int m = mbase + row;
+    const bool ok = m < Mq;
+    const int mm = ok ? m : 0;
+    const int b = mm / HWq, r = mm - b * HWq;
+    const int i = r / Wq, jj = r - i * Wq;
+    pb[j] = ok ? b : -1;
+    pih[j] = i * pl.mh;
+    piw[j] = jj * pl.mw;
+    gb[j] = gl_swz(row, lane & 7);
+  }
+  auto issue = [&](int ch, int buf) {
+    char* A = smem + buf * BUF;
+    char* Bq = A + BN * ROWB;
+    const int t0 = (ch - cb) * NG;
+#pragma unroll
+    for (int j = 0; j < IA; ++j) {
+      const int e = s_tw[t0 + ga[j]];
+      const void* src = (an[j] >= 0 && e >= 0) ? (const void*)(wz + (int64_t)an[j] * a.Kpad + e) : zero;
+      __builtin_amdgcn_global_load_lds((glb_vptr)src, (lds_vptr)(A + (4 * j + wid) * 8 * ROWB), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      const int e = s_tx[t0 + gb[j]];
+      const int ih = pih[j] + ((e >> 14) & 127) - 64, iw = piw[j] + ((e >> 21) & 127) - 64;
+      const bool ok = ((e >> 29) & 1) && pb[j] >= 0 && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+      const void* src = zero;
+      if (ok) {
+        const int seg = (e >> 28) & 1;
+        src = (seg ? base1 : base0) + ((int64_t)(pb[j] * a.Hs + ih) * a.Ws + iw) * (seg ? ld1 : ld0) + (e & 16383);
+      }
+      __builtin_amdgcn_global_load_lds((glb_vptr)src, (lds_vptr)(Bq + (4 * j + wid) * 8 * ROWB), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int f = 0; f < FM; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  __syncthreads();  // tables and constants (no DMA in flight yet)
+  if (cb < ce) issue(cb, 0);
+  if (cb + 1 < ce) issue(cb + 1, 1);
+  for (int ch = cb; ch < ce; ++ch) {
+    const int k = ch - cb;
+    // this wave's DMAs of chunk ch have landed (chunk ch + 1's may still fly), then every wave's have,
+    // and every wave is done reading chunk ch - 1 (whose buffer chunk ch + 2 overwrites)
+    if (ch + 1 < ce) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (ch + 2 < ce) issue(ch + 2, (k + 2) % GL_STAGES);
+    const char* A = smem + (k % GL_STAGES) * BUF;
+    const char* Bq = A + BN * ROWB;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const int g = 4 * s + kgl;
+      bf16x8 afr[FN], bfr[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int row = wn * WN + i * 16 + l16;
+        afr[i] = *reinterpret_cast<const bf16x8*>(A + row * ROWB + gl_swz(row, g) * 16);
+      }
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        const int row = wm * WM + f * 16 + l16;
+        bfr[f] = *reinterpret_cast<const bf16x8*>(Bq + row * ROWB + gl_swz(row, g) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int f = 0; f < FM; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], bfr[f], acc[i][f], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // the stage buffers are dead; s_st / s_flag live past them
+  const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, S, split, nt, ntn, z, mbase, nbase, Mq, HWq, Wq, oy0, ox0, bN};
+  tile_epilogue<FWD, BNS, BM, BN, WAM, WM, WN, FN, FM>(a, pl, tc, acc, s_st, s_k, s_flag);
+}
+
 #undef PSEL
 
 // ---- host-side plan
 struct LdsCfg {
   int tile, BM, BN, WAM, KC, splits;
+  bool glds;  // LDS-DMA kernel (conv_glds_kernel)
 };
 
 int decode_cfg(int cfg, LdsCfg& c) {
+  c.glds = cfg >= CONV_GLDS_CFG0 && cfg < CONV_GLDS_CFG0 + CONV_GLDS_NCFG;
+  if (c.glds) {  // cfg = CONV_GLDS_CFG0 + 4 * tile + log2(splits)
+    const int k = cfg - CONV_GLDS_CFG0;
+    c.tile = k / 4;
+    c.KC = GL_KC;
+    c.splits = 1 << (k % 4);
+    c.BM = GL_BM[c.tile]; c.BN = GL_BN[c.tile]; c.WAM = GL_WAM[c.tile];
+    return 0;
+  }
   const int k = cfg - CONV_LDS_CFG0;
   if (k < 0 || k >= CONV_LDS_NCFG) return -1;
   c.tile = k / 8;
@@ -480,6 +694,31 @@ int make_plan(int mode, const ConvArgs& a, const LdsCfg& c, LdsPlan& pl, int& gx
   return 0;
 }
 
+size_t glds_lds_bytes(const LdsCfg& c, const LdsPlan& pl, bool bns) {
+  return (size_t)GL_STAGES * (c.BM + c.BN) * GL_KC * 2 + (size_t)2 * pl.ntab * 4 +
+         ((size_t)c.WAM * c.BN * 3 + (bns ? 8 * c.BN : 0)) * 4 + 16;
+}
+
+template <int MODE>
+int launch_glds(const ConvArgs& a, int G, const LdsCfg& c, const LdsPlan& pl, int gx, hipStream_t st) {
+  if constexpr (MODE == MODE_FWD_NOL) {
+    return -2;  // the DMA bypasses registers: no on-load transform (conv_lds_kernel / conv_igemm do it)
+  } else {
+    const int ntn = (a.N + c.BN - 1) / c.BN;
+    const size_t lds = glds_lds_bytes(c, pl, MODE == MODE_DGRAD_BNS);
+    if (lds > 160 * 1024) return -2;
+    dim3 grid(gx, ntn * c.splits, G);
+#define GL_LAUNCH(T)                                                                                      \
+  if (c.tile == T) {                                                                                      \
+    hipLaunchKernelGGL((conv_glds_kernel<MODE, GL_BM[T], GL_BN[T], GL_WAM[T]>), grid, dim3(256), lds, st, a, pl); \
+    return (int)hipGetLastError();                                                                        \
+  }
+    GL_LAUNCH(0) GL_LAUNCH(1) GL_LAUNCH(2) GL_LAUNCH(3) GL_LAUNCH(4) GL_LAUNCH(5) GL_LAUNCH(6) GL_LAUNCH(7)
+#undef GL_LAUNCH
+    return -1;
+  }
+}
+
 template <int MODE>
 int launch_mode(const ConvArgs& a, int G, const LdsCfg& c, hipStream_t st) {
   LdsPlan pl;
@@ -488,6 +727,7 @@ int launch_mode(const ConvArgs& a, int G, const LdsCfg& c, hipStream_t st) {
   if (rc) return rc;
   const int ntn = (a.N + c.BN - 1) / c.BN;
   if (c.splits > 1 && (!a.ws || !a.cnt)) return -3;
+  if (c.glds) return launch_glds<MODE>(a, G, c, pl, gx, st);
   const bool nol = MODE == MODE_FWD_NOL, bns = MODE == MODE_DGRAD_BNS;
   const size_t lds = (size_t)2 * (c.BM + c.BN) * c.KC * 2 + (size_t)2 * pl.ntab * 4 +
                      ((size_t)c.WAM * c.BN * 3 + (nol ? 2 * a.Cs : (bns ? 8 * c.BN : 0))) * 4 + 16;
@@ -508,6 +748,8 @@ int launch_mode(const ConvArgs& a, int G, const LdsCfg& c, hipStream_t st) {
 }  // namespace
 
 int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_floats, int64_t& ntickets) {
+  if (mode == MODE_FWD && a.nol) mode = MODE_FWD_NOL;  // the launch mode launch_conv will pick
+  if (mode == MODE_DGRAD && a.bpart) mode = MODE_DGRAD_BNS;
   LdsCfg c;
   int rc = decode_cfg(cfg, c);
   if (rc) return rc;
@@ -515,6 +757,7 @@ int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_
   int gx;
   rc = make_plan(mode, a, c, pl, gx);
   if (rc) return rc;
+  if (c.glds && (mode == MODE_FWD_NOL || glds_lds_bytes(c, pl, mode == MODE_DGRAD_BNS) > 160 * 1024)) return -2;
   const int64_t tiles = (int64_t)G * gx * ((a.N + c.BN - 1) / c.BN);
   ws_floats = c.splits > 1 ? tiles * c.splits * c.BM * c.BN : 0;
   ntickets = c.splits > 1 ? tiles : 0;

@@ -219,13 +219,15 @@ int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 constexpr int CONV_LDS_CFG0 = 16, CONV_LDS_NCFG = 64;
 // register-pipelined conv_igemm tiles 0-13 at pipeline depth 4 (conv.hip): cfg = CONV_DEEP_CFG0 + tile
 constexpr int CONV_DEEP_CFG0 = 128, CONV_DEEP_NCFG = 14;
+// LDS-DMA implicit GEMM (conv_lds.hip conv_glds_kernel): cfg = CONV_GLDS_CFG0 + 4 * tile + log2(splits)
+constexpr int CONV_GLDS_CFG0 = 160, CONV_GLDS_NCFG = 32;
 int launch_conv_lds(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 // fp32 workspace floats and ticket count a cfg needs (0 when it does not split K); < 0: cfg invalid for a
 int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_floats, int64_t& ntickets);
 int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st);
 int wgrad_tile_shape(int cfg, int& TN, int& TK);
-constexpr int WGRAD_PATCH_CFG0 = 12;  // wgrad cfgs 12-15: 3x3/s1 patch kernels (conv.hip wgrad_patch_block)
-int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8);
+constexpr int WGRAD_PATCH_CFG0 = 12, WGRAD_PATCH_NCFG = 8;  // wgrad cfgs 12-19: 3x3/s1 patch kernels (conv.hip)
+int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8, int& R);
 int wgrad_ntiles(int cfg, const WgradArgs& a);  // tiles per group of a wgrad launch, < 0: cfg invalid for a
 int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st);
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);

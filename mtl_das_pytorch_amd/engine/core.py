@@ -25,6 +25,7 @@ import torch.nn as nn
 
 from ..ops.functional import WGRAD_PATCH, WGRAD_TILES, bnb_plan, patch_plan, patch_valid, wgrad_cfg
 from ..ops.hip import lib, ptr
+from . import guard
 
 NREP = 32  # must match csrc/common.h
 BN_PX_PER_REP = 256  # forward BN-statistic replicas: about one per this many pixels
@@ -59,10 +60,10 @@ class FlatState:
             self.offsets[id(p)] = off
             off += pad_to(p.numel(), 4)  # 16-byte aligned slots
         self.numel = off
-        self.params = torch.zeros(off, device=self.device, dtype=torch.float32)
-        self.grads = torch.zeros_like(self.params)
-        self.exp_avg = torch.zeros_like(self.params)
-        self.exp_avg_sq = torch.zeros_like(self.params)
+        self.params = guard.alloc(off, torch.float32, self.device, zero=True, label="flat params")
+        self.grads = guard.alloc(off, torch.float32, self.device, zero=True, label="flat grads")
+        self.exp_avg = guard.alloc(off, torch.float32, self.device, zero=True, label="flat exp_avg")
+        self.exp_avg_sq = guard.alloc(off, torch.float32, self.device, zero=True, label="flat exp_avg_sq")
         self.order = order
         for p in order:
             o = self.offsets[id(p)]
@@ -86,9 +87,9 @@ class FlatState:
         for m in bns:
             self.bn_offsets[id(m)] = off
             off += pad_to(m.num_features, 4)
-        self.bn_mean = torch.zeros(off, device=self.device)
-        self.bn_var = torch.ones(off, device=self.device)
-        self.bn_nbt = torch.zeros(len(bns), device=self.device, dtype=torch.int64)
+        self.bn_mean = guard.alloc(off, torch.float32, self.device, zero=True, label="bn running mean")
+        self.bn_var = guard.alloc(off, torch.float32, self.device, label="bn running var").fill_(1.0)
+        self.bn_nbt = guard.alloc(len(bns), torch.int64, self.device, zero=True, label="bn num_batches_tracked")
         self.bn_index = {id(m): i for i, m in enumerate(bns)}
         self.bns = bns
         for m in bns:
@@ -107,8 +108,8 @@ class FlatState:
         self.bn_world = 1
         self.bn_layers: List["BNLayer"] = []
         # Adam device scalars: [lr, step]
-        self.lr = torch.zeros(1, device=self.device)
-        self.step = torch.zeros(1, device=self.device)
+        self.lr = guard.alloc(1, torch.float32, self.device, zero=True, label="lr")
+        self.step = guard.alloc(1, torch.float32, self.device, zero=True, label="adam step")
 
     def off(self, p: nn.Parameter) -> int:
         return self.offsets[id(p)]
@@ -156,10 +157,10 @@ class Arena:
         self.views: List[torch.Tensor] = []
 
     def empty(self, shape, dtype=torch.bfloat16) -> torch.Tensor:
-        return torch.empty(shape, device=self.device, dtype=dtype)
+        return guard.alloc(shape, dtype, self.device, label=f"arena {tuple(shape)} {dtype}")
 
     def zeros(self, shape, dtype=torch.bfloat16) -> torch.Tensor:
-        return torch.zeros(shape, device=self.device, dtype=dtype)
+        return guard.alloc(shape, dtype, self.device, zero=True, label=f"arena {tuple(shape)} {dtype}")
 
     def zeroed(self, shape, dtype=torch.float32) -> "LazyView":
         lv = LazyView(tuple(int(s) for s in shape), dtype)
@@ -167,6 +168,11 @@ class Arena:
         return lv
 
     def finalize(self):
+        if guard.enabled():  # every zeroed view in its own guarded buffer (cleared one by one)
+            for v in self._zero_specs:
+                v.bind(guard.alloc(v.shape, v.dtype, self.device, zero=True, label=f"zeroed {v.shape} {v.dtype}"))
+            self._zero = {}
+            return
         # one backing buffer per dtype (fp64 BN replica sums, fp32 workspaces, int32 counters)
         for dt in sorted({v.dtype for v in self._zero_specs}, key=str):
             specs = [v for v in self._zero_specs if v.dtype == dt]
@@ -180,6 +186,10 @@ class Arena:
                 o += pad_to(n, 64)
 
     def clear(self):
+        if guard.enabled():
+            for v in self._zero_specs:
+                v.t.zero_()
+            return
         for buf in self._zero.values():
             buf.zero_()
 

@@ -24,6 +24,7 @@ import torch
 
 from ..models.multi_classifier import (BasicConv2d, InceptionA, InceptionB, InceptionC, InceptionD, InceptionE,
                                        Multi_Classifier)
+from . import guard
 from .core import Act, Arena, BNLayer, ConvLayer, FlatState, P, grads_of, new_act, src_dict, stem_pack_geom
 from .lowering import ACT_RELU, LoweredProgram
 from .program import Phase, k_cls_head, k_pool, k_wgfin
@@ -271,7 +272,7 @@ class InceptionProgram(LoweredProgram):
     def _alloc(self):
         m, A, B = self.model, self.arena, self.B
         self.x = A.zeros((B, self.H0, self.W0, 8))
-        self.labels = torch.zeros((B,), dtype=torch.int64, device=self.device)
+        self.labels = guard.alloc((B,), torch.int64, self.device, zero=True, label="labels")
         self.ops = []
         self.op_meta = []   # per op: None (stem, stream 0) or (block index, branch index)
         self._bi, self._cur = 0, None
@@ -297,13 +298,13 @@ class InceptionProgram(LoweredProgram):
         self.dfeat = new_act(A, 1, B, a.H, a.W, a.C, torch.float32)
         v.grads.append(self.dfeat)
         self.fc_feat = A.empty((B, a.C), torch.float32)
-        self.logp = torch.zeros((B, N), device=self.device)   # logits of the last batch
+        self.logp = guard.alloc((B, N), torch.float32, self.device, zero=True, label="logits")  # of the last batch
         self.dlogits = A.empty((B, N), torch.float32)
-        self.seed = torch.zeros(1, dtype=torch.int64, device=self.device)  # dropout RNG counter
+        self.seed = guard.alloc(1, torch.int64, self.device, zero=True, label="dropout counter")
         self.extra_state = [self.seed]
         # metrics [joint, distance, event] x [loss, correct, count, abs_err]; confusion: distance, event
-        self.metrics = torch.zeros((3, 4), device=self.device)
-        self.confusion = torch.zeros((2, 16, 16), device=self.device, dtype=torch.int32)
+        self.metrics = guard.alloc((3, 4), torch.float32, self.device, zero=True, label="metrics")
+        self.confusion = guard.alloc((2, 16, 16), torch.int32, self.device, zero=True, label="confusion")
         self.nvalid = torch.full((1,), B, device=self.device, dtype=torch.int64)
         self.convs: List[ConvLayer] = [op.conv for op in self.ops if isinstance(op, CBR)]
         self._plan_nol()

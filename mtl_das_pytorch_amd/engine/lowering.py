@@ -7,7 +7,7 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ..ops.functional import PATCH_R, WGRAD_PATCH, WGRAD_TILES
+from ..ops.functional import WGRAD_PATCH, WGRAD_TILES
 from ..ops.hip import lib
 from .core import Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, pad_to
 from .program import (Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad,
@@ -19,8 +19,8 @@ ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
 def _wgrad_cost(cfg: int, G: int, d: dict) -> int:
     """MFMA work (MACs incl. tile padding) of one weight-gradient launch -- used to balance fan-out."""
     if cfg in WGRAD_PATCH:
-        TN, CB, _ = WGRAD_PATCH[cfg]
-        px = d["splits"] * d["m_per_split"] * PATCH_R * pad_to(d["Wo"], 8)
+        TN, CB, _, R = WGRAD_PATCH[cfg]
+        px = d["splits"] * d["m_per_split"] * R * pad_to(d["Wo"], 8)
         return px * G * math.ceil(d["Npad"] / TN) * TN * 9 * d["Cs"]
     TN, TK, MCH = WGRAD_TILES[cfg]
     return d["splits"] * d["m_per_split"] * G * TN * TK * math.ceil(d["Npad"] / TN) * (d["Kpad"] // TK)

@@ -27,6 +27,7 @@ import torch
 
 from ..models.mtl import MTLNet
 from ..ops.hip import lib
+from . import guard
 from .core import NREP, Act, Arena, BNLayer, ConvLayer, FlatState, P, new_act, src_dict, stem_pack_geom
 from .lowering import ACT_NONE, ACT_RELU, ACT_SIGMOID, ADD_RELU, POOL_RELU, SIGMUL, LoweredProgram
 from .program import Phase, k_head, k_wgfin
@@ -84,7 +85,7 @@ class MTLProgram(LoweredProgram):
     def _alloc(self):
         m, A, B, T, f = self.model, self.arena, self.B, self.T, self.flat
         self.x = A.zeros((B, self.H0, self.W0, 8))
-        self.labels = torch.zeros((B, 2), dtype=torch.int64, device=self.device)
+        self.labels = guard.alloc((B, 2), torch.int64, self.device, zero=True, label="labels")
         self.xin = Act(self.x, 0, 8, 8, 0, B, self.H0, self.W0)
         # stem
         geom = stem_pack_geom(m.conv1[0], self.H0, self.W0)  # 1-channel input: taps packed as channels
@@ -161,9 +162,9 @@ class MTLProgram(LoweredProgram):
         self.dA4 = new_act(A, T, B, L4["H"], L4["W"], L4["C"], torch.float32)
         self.levels[3]["dA"] = self.dA4
         # head outputs / metrics (NOT in the per-step zeroed region: they accumulate across steps)
-        self.logp = torch.zeros((T, B, 16), device=self.device)
-        self.metrics = torch.zeros((T, 4), device=self.device)
-        self.confusion = torch.zeros((T, 16, 16), device=self.device, dtype=torch.int32)
+        self.logp = guard.alloc((T, B, 16), torch.float32, self.device, zero=True, label="logp")
+        self.metrics = guard.alloc((T, 4), torch.float32, self.device, zero=True, label="metrics")
+        self.confusion = guard.alloc((T, 16, 16), torch.int32, self.device, zero=True, label="confusion")
         self.nvalid = torch.full((1,), B, device=self.device, dtype=torch.int64)
         self.convs: List[ConvLayer] = [c1] + [L[k] for L in self.rbs for k in ("ca", "cb", "cs") if k in L] + \
                                       [L[k] for L in self.levels for k in ("c0", "c3", "co") if k in L]

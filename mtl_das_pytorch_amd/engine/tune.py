@@ -15,14 +15,15 @@ from typing import Dict, Iterable, Optional
 
 import torch
 
-from ..ops.functional import (CONV_DEEP_CFG0, CONV_DEEP_NCFG, CONV_LDS_CFG0, CONV_LDS_NCFG, WGRAD_PATCH, WGRAD_TILES,
-                              conv_workspace)
+from ..ops.functional import (CONV_DEEP_CFG0, CONV_DEEP_NCFG, CONV_GLDS_CFG0, CONV_GLDS_NCFG, CONV_LDS_CFG0,
+                              CONV_LDS_NCFG, WGRAD_PATCH, WGRAD_TILES, conv_workspace)
 from ..ops.hip import lib
 
 # conv.hip register-pipelined tiles 0-13 (pipeline depth 2, and 4 at CONV_DEEP_CFG0 + tile), then
-# conv_lds.hip LDS-staged tiles x K chunk x K split
+# conv_lds.hip LDS-staged tiles x K chunk x K split, and its LDS-DMA tiles x K split
 CONV_CFGS = (list(range(14)) + list(range(CONV_LDS_CFG0, CONV_LDS_CFG0 + CONV_LDS_NCFG))
-             + list(range(CONV_DEEP_CFG0, CONV_DEEP_CFG0 + CONV_DEEP_NCFG)))
+             + list(range(CONV_DEEP_CFG0, CONV_DEEP_CFG0 + CONV_DEEP_NCFG))
+             + list(range(CONV_GLDS_CFG0, CONV_GLDS_CFG0 + CONV_GLDS_NCFG)))
 
 
 def fused_max_m(kind: int) -> int:
@@ -72,6 +73,30 @@ def _time(fn, inner: int = 10, reps: int = 5) -> float:
     return s.elapsed_time(e) / (inner * reps)
 
 
+# isolated timings of every valid config of each measured conv signature (filled by autotune_phases,
+# consumed by tune_in_context): sig -> [(ms, cfg)] ascending
+ISOLATED: Dict[str, list] = {}
+
+
+def _isolated(mode: int, G: int, d: dict, sig: str) -> list:
+    """Isolated graph-replay time of every valid config of one conv launch (cached in ISOLATED)."""
+    if sig in ISOLATED:
+        return ISOLATED[sig]
+    L = lib()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    res = []
+    for c in CONV_CFGS:
+        dc = dict(d)
+        ws = conv_workspace(mode, c, G, dc, dev)
+        if ws is None:
+            continue
+        res.append((_time(lambda: L.conv(mode, c, G, torch.cuda.current_stream().cuda_stream, dc)), c))
+        del ws
+    res.sort()
+    ISOLATED[sig] = res
+    return res
+
+
 def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, verbose: bool = False,
                     measure: bool = True) -> Dict[str, int]:
     """Choose the conv tile config of every conv launch in ``phases`` (mutates the launches).  With
@@ -88,17 +113,7 @@ def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, ve
             if sig not in cache and not measure:
                 continue
             if sig not in cache:
-                best, best_t = cfg, float("inf")
-                dev = torch.device("cuda", torch.cuda.current_device())
-                for c in CONV_CFGS:
-                    dc = dict(d)
-                    ws = conv_workspace(mode, c, G, dc, dev)
-                    if ws is None:
-                        continue
-                    t = _time(lambda: L.conv(mode, c, G, torch.cuda.current_stream().cuda_stream, dc))
-                    del ws
-                    if t < best_t:
-                        best, best_t = c, t
+                best_t, best = _isolated(mode, G, d, sig)[0]
                 cache[sig] = best
                 if verbose:
                     print(f"tuned {sig}: cfg {best} ({best_t * 1e3:.1f} us)", flush=True)
@@ -161,12 +176,14 @@ def tail_bwd_signature(kind: int, G: int, d: dict) -> str:
 
 
 def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False, measure: bool = True,
-                     batch_wgrads: bool = True) -> Dict[str, int]:
+                     batch_wgrads: bool = True, cache: Optional[Dict[str, int]] = None) -> Dict[str, int]:
     """Tune every conv launch of a lowered program (train forward, eval forward, backward), then batch the
-    weight-gradient launches per tile config (``batch_wgrads``)."""
+    weight-gradient launches per tile config (``batch_wgrads``).  ``cache``: the table to use (default: the
+    shipped one; empty with MDA_RETUNE=1)."""
     if prog.device.type != "cuda":
         return {}
-    cache = {} if os.environ.get("MDA_RETUNE") == "1" else load_cache()
+    if cache is None:
+        cache = {} if os.environ.get("MDA_RETUNE") == "1" else load_cache()
     n0 = len(cache)
     autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose, measure)
     if batch_wgrads:
@@ -176,4 +193,109 @@ def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False
         prog.batch_wgrads()
     if out_path and len(cache) != n0:
         save_cache(cache, out_path)
+    return cache
+
+
+def _set_conv_cfg(launch, cfg: int, keep: dict) -> bool:
+    """Point a conv launch at ``cfg`` (attaching its split-K workspace); False when cfg cannot run it."""
+    mode, _, G, d = launch.args
+    dc = dict(d)
+    ws = conv_workspace(mode, cfg, G, dc, torch.device("cuda", torch.cuda.current_device()))
+    if ws is None:
+        return False
+    keep[id(launch)] = ws
+    launch.args = (mode, cfg, G, dc)
+    return True
+
+
+def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str, int], topk: int = 3,
+                    reps: int = 15, rounds: int = 3, margin: float = 0.002, verbose: bool = True) -> Dict[str, int]:
+    """Refine the conv configs of a lowered program by timing the WHOLE training step, not the isolated launch.
+
+    The isolated timings of ``autotune_phases`` are taken with L2-hot operands and no neighbours; inside the
+    multi-stream step graph the same kernels overlap other streams and read operands other kernels just
+    wrote, and run up to 2x longer (docs/PERF.md).  Here the step (gather, forward, backward with the batched
+    weight gradients, Adam + re-pack, learning rate 0) is captured as one HIP graph and replayed; for every
+    conv signature (all launches sharing it change together, so the table stays one config per signature),
+    largest isolated time first, each of its ``topk`` best isolated configs is tried and kept when the
+    replayed step gets faster by more than ``margin``.  The program's mutable state is restored afterwards.
+    Updates and returns ``cache``."""
+    from .step import StateSnapshot
+    f = prog.flat
+    snap = StateSnapshot([f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step,
+                          f.lr, prog.metrics, prog.confusion, prog.logp] + list(getattr(prog, "extra_state", [])))
+    f.lr.zero_()
+    idx = torch.arange(prog.B, device=prog.device) % X.shape[0]
+    gather = prog.gather_phase(X, labels, idx)
+    fns = [prog.arena.clear, gather.run, prog.fwd_train.run, prog.bwd.run, prog.opt["adam"].run]
+    keep = {}
+    for ph in (prog.fwd_train, prog.bwd):
+        ph.__dict__.setdefault("ws_keep", {})
+
+    def step_ms() -> float:
+        for fn_ in fns:  # eager pass: code objects of a new config loaded before capture
+            fn_()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for fn_ in fns:
+                fn_()
+        g.replay()
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(rounds):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                g.replay()
+            e.record()
+            torch.cuda.synchronize()
+            best = min(best, s.elapsed_time(e) / reps)
+        del g
+        return best
+
+    groups: Dict[str, list] = {}
+    for ph in (prog.fwd_train, prog.bwd):
+        for l in ph.launches:
+            if l.name in ("conv_fwd", "conv_dgrad"):
+                mode, cfg, G, d = l.args
+                groups.setdefault(conv_signature(mode, G, d), []).append(l)
+    order = []
+    for sig, ls in groups.items():
+        mode, cfg, G, d = ls[0].args
+        iso = _isolated(mode, G, d, sig)
+        cur = next((t for t, c in iso if c == cfg), iso[0][0] if iso else 0.0)
+        order.append((cur * len(ls), sig))
+    order.sort(reverse=True)
+    base = step_ms()
+    t0 = base
+    if verbose:
+        print(f"in-context tuning: {len(groups)} conv signatures, step {base * 1e3:.1f} us", flush=True)
+    for _, sig in order:
+        ls = groups[sig]
+        mode, cur, G, d = ls[0].args
+        cands = [c for _, c in _isolated(mode, G, d, sig)[:topk] if c != cur]
+        best_cfg = cur
+        for c in cands:
+            if not all(_set_conv_cfg(l, c, keep) for l in ls):
+                for l in ls:
+                    _set_conv_cfg(l, best_cfg, keep)
+                continue
+            t = step_ms()
+            if t < base * (1.0 - margin):
+                base, best_cfg = t, c
+            else:
+                for l in ls:
+                    _set_conv_cfg(l, best_cfg, keep)
+        if best_cfg != cur:
+            cache[sig] = best_cfg
+            if verbose:
+                print(f"  {sig}: cfg {cur} -> {best_cfg}, step {base * 1e3:.1f} us", flush=True)
+    for ph in (prog.fwd_train, prog.bwd, prog.fwd_eval):
+        ph.__dict__["ws_keep"].update(keep)
+    if verbose:
+        print(f"in-context tuning: step {t0 * 1e3:.1f} -> {base * 1e3:.1f} us", flush=True)
+    snap.restore()
+    prog.opt["pack"].run()
+    torch.cuda.synchronize()
     return cache

@@ -74,12 +74,20 @@ def _fwd_cfg(N, M):
 CONV_LDS_CFG0, CONV_LDS_NCFG = 16, 64  # csrc/kernels.h: LDS-staged conv configs (conv_lds.hip)
 CONV_DEEP_CFG0, CONV_DEEP_NCFG = 128, 14  # conv_igemm tiles 0-13 at register-pipeline depth 4 (conv.hip)
 LDS_TILES = [(64, 64), (128, 64), (64, 128), (128, 128), (32, 64), (64, 32), (32, 32), (128, 16)]
+CONV_GLDS_CFG0, CONV_GLDS_NCFG = 160, 32  # LDS-DMA conv configs (conv_lds.hip conv_glds_kernel)
+GLDS_TILES = [(64, 64), (128, 64), (64, 128), (128, 128), (256, 64), (128, 32), (256, 128), (64, 32)]
 
 
 def lds_cfg(tile: int, kc: int = 64, splits: int = 1) -> int:
     """Config id of the LDS-staged conv kernel: tile index into LDS_TILES (BM pixels x BN channels), K chunk
     64 / 128, cross-block split of K into 1 / 2 / 4 / 8."""
     return CONV_LDS_CFG0 + 8 * tile + 4 * (kc == 128) + {1: 0, 2: 1, 4: 2, 8: 3}[splits]
+
+
+def glds_cfg(tile: int, splits: int = 1) -> int:
+    """Config id of the LDS-DMA conv kernel: tile index into GLDS_TILES (BM pixels x BN channels, K chunk 64,
+    3-stage ring), cross-block split of K into 1 / 2 / 4 / 8."""
+    return CONV_GLDS_CFG0 + 4 * tile + {1: 0, 2: 1, 4: 2, 8: 3}[splits]
 
 
 def conv_workspace(mode: int, cfg: int, G: int, d: dict, device) -> Optional[tuple]:
@@ -95,8 +103,9 @@ def conv_workspace(mode: int, cfg: int, G: int, d: dict, device) -> Optional[tup
         d.pop("ws", None)
         d.pop("cnt", None)
         return ()
-    w = torch.empty(ws, device=device, dtype=torch.float32)
-    c = torch.zeros(nt, device=device, dtype=torch.int32)
+    from ..engine import guard
+    w = guard.alloc(ws, torch.float32, device, label=f"split-K workspace cfg {cfg}")
+    c = guard.alloc(nt, torch.int32, device, zero=True, label=f"split-K tickets cfg {cfg}")
     d["ws"], d["cnt"] = w.data_ptr(), c.data_ptr()
     return (w, c)
 
@@ -135,7 +144,8 @@ def prepare_conv2d(x, w, bias=None, stride=1, padding=0, stats=None, x2=None, cf
     if Ci > Cs:
         raise ValueError("weight has more input channels than the input")
     wf = pack_weight_fwd(w.float(), Cs)
-    y = torch.empty(B, Ho, Wo, Co, device=x.device, dtype=torch.bfloat16)
+    from ..engine import guard
+    y = guard.alloc((B, Ho, Wo, Co), torch.bfloat16, x.device, label=f"conv out cfg {cfg}")
     src = {"p0": ptr(x), "ld0": x.shape[-1], "C0": x.shape[-1], "C1": C1}
     if x2 is not None:
         _check(x2, torch.bfloat16)
@@ -170,7 +180,8 @@ def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg
     sh, sw = (stride, stride) if isinstance(stride, int) else stride
     ph, pw = (padding, padding) if isinstance(padding, int) else padding
     wd = pack_weight_dgrad(w.float(), Cs)
-    dx = torch.empty(B, H, W, Cs, device=dy.device, dtype=torch.float32)
+    from ..engine import guard
+    dx = guard.alloc((B, H, W, Cs), torch.float32, dy.device, label=f"dgrad out cfg {cfg}")
     d = {"src": {"p0": ptr(dy), "ld0": Co, "C0": Co, "C1": 0}, "w": ptr(wd), "out": ptr(dx), "ldo": Cs,
          "B": B, "Hs": Ho, "Ws": Wo, "Ho": H, "Wo": W, "N": Cs, "Npad": wd.shape[0], "Cs": Co, "KH": KH, "KW": KW,
          "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": wd.shape[1]}
@@ -197,23 +208,25 @@ WGRAD_TILES = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 
                8: (16, 192, 64), 9: (16, 128, 64), 10: (32, 192, 64), 11: (32, 320, 32)}  # (TN, TK, MCH)
 
 
-# 3x3 / stride-1 / pad-1 patch kernels (csrc/conv.hip wgrad_patch_block): (TN, CB, max padded width)
-WGRAD_PATCH = {12: (16, 16, 88), 13: (32, 16, 88), 14: (32, 32, 48), 15: (64, 32, 24)}
-PATCH_R = 4  # output rows per work unit
+# 3x3 / stride-1 patch kernels, padding 1 or 0 (csrc/conv.hip wgrad_patch_block):
+# (TN, CB, max padded width, output rows per strip)
+WGRAD_PATCH = {12: (16, 16, 88, 4), 13: (32, 16, 88, 4), 14: (32, 32, 48, 4), 15: (64, 32, 24, 4),
+               16: (32, 32, 128, 2), 17: (64, 32, 128, 2), 18: (64, 16, 128, 2), 19: (32, 16, 128, 2)}
 
 
 def patch_valid(cfg, Cs, KH, KW, stride, padding, Hi, Wi, Ho, Wo, C0=None, C1=0) -> bool:
-    TN, CB, W8 = WGRAD_PATCH[cfg]
+    TN, CB, W8, R = WGRAD_PATCH[cfg]
     s = (stride, stride) if isinstance(stride, int) else tuple(stride)
     p = (padding, padding) if isinstance(padding, int) else tuple(padding)
-    return ((KH, KW) == (3, 3) and s == (1, 1) and p == (1, 1) and (Hi, Wi) == (Ho, Wo) and Cs % CB == 0
-            and _pad(Wo, 8) <= W8 and (C1 == 0 or C0 % CB == 0))
+    return ((KH, KW) == (3, 3) and s == (1, 1) and p[0] in (0, 1) and p[1] in (0, 1)
+            and (Ho, Wo) == (Hi + 2 * p[0] - 2, Wi + 2 * p[1] - 2) and Cs % CB == 0
+            and _pad(Wo, 8) <= W8 and (R * _pad(Wo, 8)) % 32 == 0 and (C1 == 0 or C0 % CB == 0))
 
 
 def patch_plan(cfg, B, Ho, Npad, Cs, G=1, target=512):
-    """(splits, units per split) of a patch wgrad: unit = (image, strip of PATCH_R output rows)."""
-    TN, CB, _ = WGRAD_PATCH[cfg]
-    U = B * math.ceil(Ho / PATCH_R)
+    """(splits, units per split) of a patch wgrad: unit = (image, strip of R output rows)."""
+    TN, CB, _, R = WGRAD_PATCH[cfg]
+    U = B * math.ceil(Ho / R)
     tiles = math.ceil(Npad / TN) * (Cs // CB) * G
     splits = max(1, min(U, math.ceil(target / tiles)))
     ups = math.ceil(U / splits)
@@ -252,7 +265,8 @@ def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=No
             splits = max(1, min(math.ceil(M / MCH), math.ceil(512 / tiles)))
         mps = _pad(math.ceil(M / splits), MCH)
         splits = math.ceil(M / mps)
-    slab = torch.empty(1, splits, Npad, Kpad, device=x.device, dtype=torch.float32)
+    from ..engine import guard
+    slab = guard.alloc((1, splits, Npad, Kpad), torch.float32, x.device, label=f"wgrad slab cfg {cfg}")
     src = {"p0": ptr(x), "ld0": x.shape[-1], "C0": x.shape[-1], "C1": C1}
     if x2 is not None:
         src.update({"p1": ptr(x2), "ld1": C1})

@@ -190,3 +190,17 @@ def test_inception_aux_logits_shape_error():
         m(torch.randn(2, 1, 100, 250))
     with pytest.raises(ValueError, match="4 x 13"):
         InceptionProgram(m, 2, "cpu")
+
+
+def test_guard_allocator_cpu_fallback():
+    """On the CPU (or with the guard off) the guard allocator is plain torch.zeros / torch.empty."""
+    from mtl_das_pytorch_amd.engine import guard
+    t = guard.alloc((3, 4), torch.float32, "cpu", zero=True)
+    assert t.shape == (3, 4) and not t.any()
+    guard.enable(True)
+    try:
+        t = guard.alloc(5, torch.int64, "cpu", zero=True)  # CPU tensors are never guarded
+        assert t.shape == (5,) and guard.count() == 0 and guard.check() == []
+    finally:
+        guard.enable(False)
+        guard.reset()

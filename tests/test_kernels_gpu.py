@@ -112,16 +112,22 @@ def test_conv_wgrad_whole_k_tiles(fn, case, cfg):
 @pytest.mark.parametrize("case,cfg", [((2, 33, 83, 16, 16, 3, 1, 1), 12), ((3, 33, 83, 16, 32, 3, 1, 1), 13),
                                       ((2, 17, 42, 16, 32, 3, 1, 1), 12), ((4, 17, 42, 32, 32, 3, 1, 1), 14),
                                       ((4, 17, 42, 32, 64, 3, 1, 1), 14), ((4, 9, 21, 64, 64, 3, 1, 1), 15),
-                                      ((4, 5, 11, 128, 128, 3, 1, 1), 15), ((2, 7, 13, 32, 48, 3, 1, 1), 14)])
+                                      ((4, 5, 11, 128, 128, 3, 1, 1), 15), ((2, 7, 13, 32, 48, 3, 1, 1), 14),
+                                      # "valid" 3x3 (padding 0) and the wide stem maps (configs 16-19, 2-row strips)
+                                      ((2, 23, 60, 80, 192, 3, 1, 0), 13), ((2, 23, 60, 80, 48, 3, 1, 0), 12),
+                                      ((2, 47, 122, 32, 64, 3, 1, 1), 17), ((2, 49, 124, 32, 32, 3, 1, 0), 16),
+                                      ((2, 47, 122, 32, 64, 3, 1, 1), 18), ((3, 47, 122, 32, 40, 3, 1, 1), 19),
+                                      ((2, 33, 96, 16, 16, 3, 1, 0), 19)])
 @pytest.mark.parametrize("nol", [False, True])
 def test_conv_wgrad_patch(fn, case, cfg, nol):
-    """3x3 / stride-1 patch weight gradients (configs 12-15: the input strip staged once in LDS, all 9 taps
-    read from it): widths that are not multiples of 8, heights that are not multiples of the 4-row strip,
-    Cout not a multiple of the tile, several channel slices, and normalise-on-load of the input."""
+    """3x3 / stride-1 patch weight gradients (configs 12-19: the input strip staged once in LDS, all 9 taps
+    read from it): widths that are not multiples of 8, heights that are not multiples of the strip,
+    Cout not a multiple of the tile, several channel slices, padding 1 and 0, and normalise-on-load of
+    the input."""
     B, H, W, C, Co, k, s, p = case
     x, w, _, _, _ = _mk(case, seed=cfg)
     g = torch.Generator().manual_seed(cfg + 7)
-    dy = torch.randn(B, Co, H, W, generator=g).bfloat16().float().cuda()
+    dy = torch.randn(B, Co, H + 2 * p - 2, W + 2 * p - 2, generator=g).bfloat16().float().cuda()
     if nol:
         consts = torch.zeros(1, 4, C, device="cuda")
         consts[0, 0] = torch.rand(C, generator=g).cuda() + 0.5

@@ -1,12 +1,13 @@
 """Re-measure the per-layer kernel choices of every model at the benchmark batch and write the tuned table.
 
     python tools/retune.py [--batch 32] [--models MTL,single_event,single_distance,multi_classifier]
-                           [--out gpurun_out/tuned_cfgs.json] [--keep]
+                           [--out gpurun_out/tuned_cfgs.json] [--keep] [--in-context [--topk 3]]
 
 Starts from an empty table (``--keep`` starts from the shipped one and only fills missing layers), tunes
 every conv forward / data-gradient / weight-gradient launch and BN-backward variant of each model's
-program (engine/tune.py), and writes the merged table.  Copy it over
-mtl_das_pytorch_amd/engine/tuned_cfgs.json to ship it.
+program by isolated timing (engine/tune.py autotune_phases); ``--in-context`` then refines the conv
+choices by timing the whole captured training step per candidate (engine/tune.py tune_in_context).
+Writes the merged table; copy it over mtl_das_pytorch_amd/engine/tuned_cfgs.json to ship it.
 """
 import argparse
 import os
@@ -18,8 +19,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mtl_das_pytorch_amd.engine.inception import InceptionProgram  # noqa: E402
 from mtl_das_pytorch_amd.engine.mtl import MTLProgram  # noqa: E402
-from mtl_das_pytorch_amd.engine.tune import autotune_phases, load_cache, save_cache  # noqa: E402
-from mtl_das_pytorch_amd.models import build_model  # noqa: E402
+from mtl_das_pytorch_amd.data.synthetic import generate  # noqa: E402
+from mtl_das_pytorch_amd.engine.tune import autotune_phases, autotune_program, load_cache, save_cache, tune_in_context  # noqa: E402,E501
+from mtl_das_pytorch_amd.models import build_model, encode_joint  # noqa: E402
 
 
 def main():
@@ -28,6 +30,8 @@ def main():
     ap.add_argument("--models", default="MTL,single_event,single_distance,multi_classifier")
     ap.add_argument("--out", default=os.path.join("gpurun_out", "tuned_cfgs.json"))
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--in-context", action="store_true")
+    ap.add_argument("--topk", type=int, default=3)
     args = ap.parse_args()
     cache = load_cache() if args.keep else {}
     for name in args.models.split(","):
@@ -38,6 +42,13 @@ def main():
         n0 = len(cache)
         autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose=True, measure=True)
         print(f"{name}: {len(cache) - n0} new entries in {time.time() - t0:.1f} s", flush=True)
+        if args.in_context:
+            prog.set_optimizer(weight_decay=1e-5)
+            autotune_program(prog, cache=cache, measure=False)  # batch the weight gradients as the bench does
+            X, d, e = generate(4 * args.batch, seed=3, device="cuda")
+            labels = encode_joint(d, e) if name == "multi_classifier" else torch.stack([d, e], 1)
+            tune_in_context(prog, X, labels, cache, topk=args.topk)
+            print(f"{name}: in-context refinement done at {time.time() - t0:.1f} s", flush=True)
         del prog, m
         torch.cuda.empty_cache()
     save_cache(cache, args.out)
