@@ -341,6 +341,8 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.attr("CONV_DEEP_NCFG") = CONV_DEEP_NCFG;
   m.attr("CONV_GLDS_CFG0") = CONV_GLDS_CFG0;
   m.attr("CONV_GLDS_NCFG") = CONV_GLDS_NCFG;
+  m.attr("CONV_PATCH_CFG0") = CONV_PATCH_CFG0;
+  m.attr("CONV_PATCH_NCFG") = CONV_PATCH_NCFG;
   m.def("wgrad", &wgrad);
   m.def("wgrad_finalize", &wgrad_finalize);
   m.def("tail_fwd", &tail_fwd);

@@ -623,6 +623,242 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a, LdsPlan pl) 
 
 #undef PSEL
 
+// ================================================================================================
+// Patch convolution (cfg in [CONV_PATCH_CFG0, +CONV_PATCH_NCFG)): 3x3 / stride-1 forward and data gradient
+// of the wide maps (Model C's 49x124 / 47x122 / 23x60 stem, Model A's 33x83 / 17x42 stages).  The im2col
+// forms above fetch every input element once per tap (9x); here a block owns a STRIP of R whole output
+// rows of one image (M tile = R * Wout pixels, row-major, so the shared tile_epilogue applies unchanged)
+// and stages the strip's input rows with halo -- (R + 2) rows x (Wout + 2) columns x CB channels -- in LDS
+// ONCE per channel slice, together with the slice's weights [BN][9 * CB].  Every tap's MFMA operand is
+// then a shifted read of the same strip: lane (pixel p, k-group q) of tap (dh, dw) reads the 16 bytes at
+// strip row r(p) + dh, column c(p) + dw, channels 8q'.. -- no im2col gather, no per-tap bounds checks
+// (padding is zero in the strip), and a normalise-on-load input is transformed once per element instead of
+// 9 times.  The data gradient is the same kernel over dy with the taps flipped (dh = 2 - kh) and the halo
+// offsets of the transposed conv.
+//
+// LDS rows are padded to CBP = CB + 8 channels and the weight rows to WKP = 9 CB (rounded up to 32) + 8, so
+// the row pitches are odd multiples of 16 bytes: the 16 lanes of each ds_read_b128 group hit 16 distinct
+// 16-byte slots of a 256-byte bank row (conflict-free).
+constexpr int PT_NT = 5;  // tile configs: BM pixels (strip capacity) x BN channels, WAM waves along M
+constexpr int PT_BM[PT_NT] = {256, 256, 256, 128, 128};
+constexpr int PT_BN[PT_NT] = {16, 32, 64, 32, 64};
+constexpr int PT_WAM[PT_NT] = {4, 4, 4, 4, 2};
+constexpr int PT_CB[3] = {16, 32, 64};
+
+template <int CB>
+constexpr int pt_ksteps() { return (9 * CB + 31) / 32; }
+template <int CB>
+constexpr int pt_wkp() { return pt_ksteps<CB>() * 32 + 8; }
+
+template <int MODE, int BM, int BN, int WAM, int CB>
+__global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a, PatchPlan pp) {
+  constexpr int WAN = 4 / WAM;
+  constexpr int WM = BM / WAM, WN = BN / WAN, FM = WM / 16, FN = WN / 16;
+  static_assert(FM >= 1 && FN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
+  constexpr int CBP = CB + 8, KS = pt_ksteps<CB>(), WKP = pt_wkp<CB>();
+  constexpr int CG = CB / 8;  // 16-byte channel groups of a strip pixel
+  constexpr int NU = 8;       // staging units per thread per round
+  constexpr bool FWD = lds_fwd<MODE>();
+  constexpr bool NOL = MODE == MODE_FWD_NOL;
+  constexpr bool BNS = MODE == MODE_DGRAD_BNS;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int WP = pp.Wout + 2;  // strip columns
+  const int SR = pp.R + 2;     // strip rows
+  bf16_t* s_x = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* s_w = s_x + SR * WP * CBP;
+  float* s_st = reinterpret_cast<float*>(s_w + BN * WKP);  // [WAM][BN][3] epilogue sums
+  float* s_k = s_st + WAM * BN * 3;                         // NOL: [2][Cs] / BNS: [8][BN] constants
+  int* s_flag = reinterpret_cast<int*>(s_k + (NOL ? 2 * a.Cs : (BNS ? 8 * BN : 0)));
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, kgl = lane >> 4;
+  const int wn = wid % WAN, wm = wid / WAN;
+  const int z = blockIdx.z, nt = blockIdx.y, ntn = gridDim.y;
+  const int b = (int)blockIdx.x / pp.nstrip, oh0 = ((int)blockIdx.x - b * pp.nstrip) * pp.R;
+  const int rows = min(pp.R, pp.Hout - oh0);
+  const int HWo = pp.Hout * pp.Wout;
+  const int mbase = b * HWo + oh0 * pp.Wout, nbase = nt * BN;
+  const int Mtile = mbase + rows * pp.Wout;  // pixels of this strip end here (the next strip / image starts)
+
+  if (NOL) bn_prepare(a.nbn, z, s_k, s_k + a.Cs, nullptr, nullptr, blockIdx.x == 0 && blockIdx.y == 0);
+  const int bN = a.bN > 0 ? a.bN : a.N;
+  const int zb = a.bpgs == 0 ? 0 : z;
+  if (BNS) {
+    for (int i = tid; i < BN; i += 256) {
+      const int n = nbase + i;
+      float k[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (n < bN) {
+        bn_channel_bwd(a.bbn, zb, n, k[0], k[1], k[2], k[3]);
+        if (a.br_bn) bn_channel_bwd(a.bbn2, zb, n, k[4], k[5], k[6], k[7]);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s_k[q * BN + i] = k[q];
+    }
+  }
+
+  const bf16_t* wz = a.w + a.wgs * z;
+  const bf16_t* base0 = a.src.p[0] + a.src.gs[0] * z;
+  const bf16_t* base1 = a.src.p[1] ? a.src.p[1] + a.src.gs[1] * z : base0;
+  const int ld0 = a.src.ld[0], ld1 = a.src.ld[1];
+  const int row0 = oh0 + pp.dy0, col0 = pp.dx0;  // source pixel of strip (0, 0)
+  const int nux = SR * WP * CG, nuw = BN * (WKP - 8) / 8, nut = nux + nuw;
+
+  // fragment bases: this lane's pixel of each M fragment -> strip element offset of tap (0, 0), channel 0
+  int pbase[FM];
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    int p = wm * WM + f * 16 + l16;
+    p = mbase + p < Mtile ? p : 0;  // rows past the strip: any in-LDS address (the epilogue drops them)
+    const int r = p / pp.Wout, c = p - r * pp.Wout;
+    pbase[f] = (r * WP + c) * CBP;
+  }
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int f = 0; f < FM; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  __syncthreads();  // NOL / BNS constants
+  for (int sl = 0; sl < pp.nslice; ++sl) {
+    const int cs0 = sl * CB;
+    // ---- stage the strip slice and the weight slice: unit u < nux -> strip (row j, column q, group g),
+    // else weight (row n, k-group g: tap g / CG, channel 8 (g % CG))
+    for (int u0 = 0; u0 < nut; u0 += 256 * NU) {
+      uint4 v[NU];
+      uint32_t okm = 0;
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        const int u = u0 + tid + 256 * i;
+        v[i] = make_uint4(0, 0, 0, 0);
+        if (u < nux) {
+          const int g = u % CG, q = (u / CG) % WP, j = u / (CG * WP);
+          const int ih = row0 + j, iw = col0 + q;
+          if (ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) {
+            const int c = cs0 + g * 8;
+            const int seg = (a.src.C1 > 0 && c >= a.src.C0) ? 1 : 0;
+            v[i] = *reinterpret_cast<const uint4*>((seg ? base1 : base0) +
+                                                   ((int64_t)(b * a.Hs + ih) * a.Ws + iw) * (seg ? ld1 : ld0) +
+                                                   (c - seg * a.src.C0));
+            okm |= 1u << i;
+          }
+        } else if (u < nut) {
+          const int w = u - nux, g = w % (WKP / 8 - 1), n = nbase + w / (WKP / 8 - 1);
+          const int tap = g / CG;
+          if (tap < 9 && n < a.Npad)
+            v[i] = *reinterpret_cast<const uint4*>(wz + (int64_t)n * a.Kpad + tap * a.Cs + cs0 + (g - tap * CG) * 8);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        const int u = u0 + tid + 256 * i;
+        if (u < nux) {
+          const int g = u % CG, pix = u / CG;
+          uint4 x = v[i];
+          if (NOL && ((okm >> i) & 1)) {  // act(BN(y)) of the producing conv, once per element
+            const int c = cs0 + g * 8;
+            uint32_t w4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              float lo = __uint_as_float(w4[h] << 16) * s_k[c + 2 * h] + s_k[a.Cs + c + 2 * h];
+              float hi = __uint_as_float(w4[h] & 0xffff0000u) * s_k[c + 2 * h + 1] + s_k[a.Cs + c + 2 * h + 1];
+              if (a.nol_kind == ACT_RELU) { lo = fmaxf(lo, 0.f); hi = fmaxf(hi, 0.f); }
+              w4[h] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+            }
+            x = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+          }
+          *reinterpret_cast<uint4*>(s_x + pix * CBP + g * 8) = x;
+        } else if (u < nut) {
+          const int w = u - nux, g = w % (WKP / 8 - 1), n = w / (WKP / 8 - 1);
+          *reinterpret_cast<uint4*>(s_w + n * WKP + g * 8) = v[i];
+        }
+      }
+    }
+    __syncthreads();
+    // ---- 9 taps x CB channels: k-group g = 4 ks + kgl is tap g / CG, channels 8 (g % CG)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int g = 4 * ks + kgl;
+      const int tap = g / CG < 9 ? g / CG : 0;  // k past 9 CB: zero weights, any strip element
+      const int kh = tap / 3, kw = tap - kh * 3;
+      const int dh = FWD ? kh : 2 - kh, dw = FWD ? kw : 2 - kw;
+      const int off = (dh * WP + dw) * CBP + (g - (g / CG) * CG) * 8;
+      bf16x8 afr[FN], bfr[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        afr[i] = *reinterpret_cast<const bf16x8*>(s_w + (wn * WN + i * 16 + l16) * WKP + g * 8);
+#pragma unroll
+      for (int f = 0; f < FM; ++f) bfr[f] = *reinterpret_cast<const bf16x8*>(s_x + pbase[f] + off);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int f = 0; f < FM; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], bfr[f], acc[i][f], 0, 0, 0);
+    }
+    __syncthreads();  // the next slice overwrites the strip and the weights
+  }
+
+  LdsPlan pl{};
+  pl.qy = 1; pl.qx = 1;
+  const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, 1, 0, nt, ntn, z, mbase, nbase, Mtile, HWo, pp.Wout, 0, 0, bN};
+  tile_epilogue<FWD, BNS, BM, BN, WAM, WM, WN, FN, FM>(a, pl, tc, acc, s_st, s_k, s_flag);
+}
+
+// Strip plan of a patch launch (host); returns 0 or -2 when the conv is not a 3x3 / stride-1 conv this
+// tile can take.  FWD: output Ho x Wo from the input (Hs, Ws); DGRAD: dx (Ho, Wo) from dy (Hs, Ws).
+int patch_plan(int mode, const ConvArgs& a, int tile, int cbi, PatchPlan& pp, size_t& lds) {
+  const bool fwd = mode == MODE_FWD || mode == MODE_FWD_NOL;
+  const int CB = PT_CB[cbi], BM = PT_BM[tile], BN = PT_BN[tile], WAM = PT_WAM[tile];
+  if (a.KH != 3 || a.KW != 3 || a.sh != 1 || a.sw != 1) return -2;
+  if (a.Cs % CB || a.Cs > 16383) return -2;
+  if (a.src.C1 > 0 && a.src.C0 % CB) return -2;  // a channel slice may not straddle the two segments
+  pp.Wout = a.Wo;
+  pp.Hout = a.Ho;
+  if (pp.Wout > BM || pp.Wout < 1) return -2;
+  pp.R = std::min(BM / pp.Wout, pp.Hout);
+  pp.nstrip = (pp.Hout + pp.R - 1) / pp.R;
+  pp.nslice = a.Cs / CB;
+  if (fwd) { pp.dy0 = -a.ph; pp.dx0 = -a.pw; }
+  else { pp.dy0 = a.ph - 2; pp.dx0 = a.pw - 2; }
+  if (fwd ? (a.Hs + 2 * a.ph - 2 != a.Ho || a.Ws + 2 * a.pw - 2 != a.Wo)
+          : (a.Ho + 2 * a.ph - 2 != a.Hs || a.Wo + 2 * a.pw - 2 != a.Ws)) return -2;
+  const bool nol = mode == MODE_FWD_NOL, bns = mode == MODE_DGRAD_BNS;
+  const int wkp = ((9 * CB + 31) / 32) * 32 + 8;
+  lds = (size_t)(pp.R + 2) * (pp.Wout + 2) * (CB + 8) * 2 + (size_t)BN * wkp * 2 +
+        ((size_t)WAM * BN * 3 + (nol ? 2 * a.Cs : (bns ? 8 * BN : 0))) * 4 + 16;
+  if (lds > 160 * 1024) return -2;
+  return 0;
+}
+
+template <int MODE>
+int launch_patch(const ConvArgs& a, int G, int tile, int cbi, hipStream_t st) {
+  PatchPlan pp;
+  size_t lds;
+  int rc = patch_plan(MODE, a, tile, cbi, pp, lds);
+  if (rc) return rc;
+  dim3 grid(a.B * pp.nstrip, (a.N + PT_BN[tile] - 1) / PT_BN[tile], G);
+#define PT_LAUNCH(T, C)                                                                                     \
+  if (tile == T && cbi == C) {                                                                              \
+    hipLaunchKernelGGL((conv_patch_kernel<MODE, PT_BM[T], PT_BN[T], PT_WAM[T], PT_CB[C]>), grid, dim3(256), lds, \
+                       st, a, pp);                                                                          \
+    return (int)hipGetLastError();                                                                          \
+  }
+#define PT_TILE(T) PT_LAUNCH(T, 0) PT_LAUNCH(T, 1) PT_LAUNCH(T, 2)
+  PT_TILE(0) PT_TILE(1) PT_TILE(2) PT_TILE(3) PT_TILE(4)
+#undef PT_TILE
+#undef PT_LAUNCH
+  return -1;
+}
+
+bool patch_cfg(int cfg, int& tile, int& cbi) {
+  const int k = cfg - CONV_PATCH_CFG0;
+  if (k < 0 || k >= PT_NT * 3) return false;
+  tile = k / 3;
+  cbi = k % 3;
+  return true;
+}
+
 // ---- host-side plan
 struct LdsCfg {
   int tile, BM, BN, WAM, KC, splits;
@@ -750,6 +986,14 @@ int launch_mode(const ConvArgs& a, int G, const LdsCfg& c, hipStream_t st) {
 int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_floats, int64_t& ntickets) {
   if (mode == MODE_FWD && a.nol) mode = MODE_FWD_NOL;  // the launch mode launch_conv will pick
   if (mode == MODE_DGRAD && a.bpart) mode = MODE_DGRAD_BNS;
+  int tile, cbi;
+  if (patch_cfg(cfg, tile, cbi)) {
+    PatchPlan pp;
+    size_t lds;
+    ws_floats = 0;
+    ntickets = 0;
+    return patch_plan(mode, a, tile, cbi, pp, lds);
+  }
   LdsCfg c;
   int rc = decode_cfg(cfg, c);
   if (rc) return rc;
@@ -765,6 +1009,16 @@ int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_
 }
 
 int launch_conv_lds(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
+  int tile, cbi;
+  if (patch_cfg(cfg, tile, cbi)) {
+    switch (mode) {
+      case MODE_FWD: return launch_patch<MODE_FWD>(a, G, tile, cbi, st);
+      case MODE_FWD_NOL: return launch_patch<MODE_FWD_NOL>(a, G, tile, cbi, st);
+      case MODE_DGRAD: return launch_patch<MODE_DGRAD>(a, G, tile, cbi, st);
+      case MODE_DGRAD_BNS: return launch_patch<MODE_DGRAD_BNS>(a, G, tile, cbi, st);
+      default: return -1;
+    }
+  }
   LdsCfg c;
   int rc = decode_cfg(cfg, c);
   if (rc) return rc;

@@ -67,6 +67,11 @@ struct LdsPhase {
   int m0;   // first blockIdx.x of the phase
   int Kp;   // nh * nw * Cs padded to the K chunk
 };
+// Strip plan of a patch conv launch (conv_lds.hip conv_patch_kernel): R output rows per block, nstrip strips
+// per image, nslice channel slices; source pixel of strip element (j, q) = (oh0 + dy0 + j, dx0 + q).
+struct PatchPlan {
+  int R, nstrip, nslice, Hout, Wout, dy0, dx0;
+};
 struct LdsPlan {
   LdsPhase ph[4];
   int nph;
@@ -221,6 +226,9 @@ constexpr int CONV_LDS_CFG0 = 16, CONV_LDS_NCFG = 64;
 constexpr int CONV_DEEP_CFG0 = 128, CONV_DEEP_NCFG = 14;
 // LDS-DMA implicit GEMM (conv_lds.hip conv_glds_kernel): cfg = CONV_GLDS_CFG0 + 4 * tile + log2(splits)
 constexpr int CONV_GLDS_CFG0 = 160, CONV_GLDS_NCFG = 32;
+// patch conv for 3x3 / stride-1 layers (conv_lds.hip conv_patch_kernel): cfg = CONV_PATCH_CFG0 + 3 * tile + cb
+// (tile: BM x BN of PT_BM / PT_BN, cb: channel slice 16 / 32 / 64)
+constexpr int CONV_PATCH_CFG0 = 192, CONV_PATCH_NCFG = 15;
 int launch_conv_lds(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 // fp32 workspace floats and ticket count a cfg needs (0 when it does not split K); < 0: cfg invalid for a
 int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_floats, int64_t& ntickets);

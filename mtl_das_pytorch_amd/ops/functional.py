@@ -76,6 +76,9 @@ CONV_DEEP_CFG0, CONV_DEEP_NCFG = 128, 14  # conv_igemm tiles 0-13 at register-pi
 LDS_TILES = [(64, 64), (128, 64), (64, 128), (128, 128), (32, 64), (64, 32), (32, 32), (128, 16)]
 CONV_GLDS_CFG0, CONV_GLDS_NCFG = 160, 32  # LDS-DMA conv configs (conv_lds.hip conv_glds_kernel)
 GLDS_TILES = [(64, 64), (128, 64), (64, 128), (128, 128), (256, 64), (128, 32), (256, 128), (64, 32)]
+CONV_PATCH_CFG0, CONV_PATCH_NCFG = 192, 15  # 3x3 / stride-1 patch conv configs (conv_lds.hip conv_patch_kernel)
+PATCH_TILES = [(256, 16), (256, 32), (256, 64), (128, 32), (128, 64)]  # strip capacity (pixels) x BN channels
+PATCH_CB = [16, 32, 64]  # channel slice staged per pass
 
 
 def lds_cfg(tile: int, kc: int = 64, splits: int = 1) -> int:
@@ -88,6 +91,12 @@ def glds_cfg(tile: int, splits: int = 1) -> int:
     """Config id of the LDS-DMA conv kernel: tile index into GLDS_TILES (BM pixels x BN channels, K chunk 64,
     3-stage ring), cross-block split of K into 1 / 2 / 4 / 8."""
     return CONV_GLDS_CFG0 + 4 * tile + {1: 0, 2: 1, 4: 2, 8: 3}[splits]
+
+
+def patch_cfg(tile: int, cb: int) -> int:
+    """Config id of the patch conv kernel: tile index into PATCH_TILES (a block owns R = BM // Wout whole
+    output rows x BN channels), channel slice cb (16 / 32 / 64; Cs must be a multiple)."""
+    return CONV_PATCH_CFG0 + 3 * tile + PATCH_CB.index(cb)
 
 
 def conv_workspace(mode: int, cfg: int, G: int, d: dict, device) -> Optional[tuple]:

@@ -179,39 +179,6 @@ def test_conv_normalise_on_load(fn, kind, case, cfg):
     assert rel(dw, wr.grad) < 5e-3
 
 
-@pytest.mark.parametrize("cfg", [None, 8, 11, 128 + 8, 128 + 11])
-@pytest.mark.parametrize("proj", [False, True])
-@pytest.mark.parametrize("case", [(4, 17, 42, 32, 32, 3, 1, 1), (4, 9, 21, 64, 128, 3, 2, 1), (4, 5, 11, 128, 128, 1, 1, 0)])
-def test_conv_residual_on_load(fn, case, proj, cfg):
-    """Forward conv whose input is a residual block's output relu(BN(y) + r') computed on load from the block's
-    pre-BN y and its residual r (identity) or BN2(r) (projection): against the fp32 conv of the materialised
-    bf16 output; the running statistics are left to the block's tail (not updated here)."""
-    B, H, W, C, Co, k, s, p = case
-    g = torch.Generator().manual_seed(60 + proj)
-    y = (torch.randn(B, C, H, W, generator=g) * 2 + 0.3).bfloat16().float().cuda()
-    r = (torch.randn(B, C, H, W, generator=g) * 1.5 - 0.2).bfloat16().float().cuda()
-    bn, gamma, beta, rm, rv, nbt = _bn_setup(fn, y, C, seed=1)
-    bn2 = None
-    rr = r
-    if proj:
-        bn2, gamma2, beta2, _, _, _ = _bn_setup(fn, r, C, seed=2)
-        rr = _torch_bn(r, gamma2, beta2)
-    Fin = F.relu(_torch_bn(y, gamma, beta) + rr).bfloat16().float()
-    w = (torch.randn(Co, C, k, k, generator=g) / math.sqrt(C * k * k)).bfloat16().float().cuda()
-    ref = F.conv2d(Fin, w, stride=s, padding=p)
-    out = fn.conv2d(nhwc(y).bfloat16(), w, stride=s, padding=p, nol=(bn, 4, nhwc(r).bfloat16(), bn2), cfg=cfg)
-    assert rel(nchw(out), ref) < 6e-3
-    assert int(nbt.item()) == 0 and torch.all(rm == 0)  # the tail owns the running-statistics update
-
-
-def test_conv_residual_on_load_rejects_lds(fn):
-    x = torch.zeros(2, 9, 21, 64, device="cuda", dtype=torch.bfloat16)
-    w = torch.zeros(64, 64, 3, 3, device="cuda")
-    bn, *_ = _bn_setup(fn, torch.zeros(2, 64, 9, 21, device="cuda"), 64)
-    with pytest.raises((ValueError, RuntimeError)):
-        fn.conv2d(x, w, padding=1, nol=(bn, 4, x, None), cfg=16)
-
-
 @pytest.mark.parametrize("cfg", LDS_SAMPLE)
 def test_conv_two_segment_input(fn, cfg):
     g = torch.Generator().manual_seed(3)

@@ -57,12 +57,8 @@ def main():
                     call = fn.prepare_conv2d_dgrad(dy, w, (a.H, a.W), stride=a.s, padding=pad, cfg=c, **kw)
                 else:
                     call = fn.prepare_conv2d(x, w, None, stride=a.s, padding=pad, cfg=c, **kw)
-            except (ValueError, RuntimeError):
-                ok = False
-                break
-            try:
                 row.append(_time(call.run) * 1e3)
-            except RuntimeError:  # a variant this config does not support (e.g. normalise-on-load by LDS-DMA)
+            except (ValueError, RuntimeError):  # a variant this config does not support (e.g. normalise-on-load by LDS-DMA)
                 if len(row) == 1:
                     ok = False
                     break

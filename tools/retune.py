@@ -1,7 +1,7 @@
 """Re-measure the per-layer kernel choices of every model at the benchmark batch and write the tuned table.
 
     python tools/retune.py [--batch 32] [--models MTL,single_event,single_distance,multi_classifier]
-                           [--out gpurun_out/tuned_cfgs.json] [--keep] [--in-context [--topk 3]]
+                           [--out gpurun_out/tuned_cfgs.json] [--keep [--drop wgrad,...]] [--in-context [--topk 3]]
 
 Starts from an empty table (``--keep`` starts from the shipped one and only fills missing layers), tunes
 every conv forward / data-gradient / weight-gradient launch and BN-backward variant of each model's
@@ -32,8 +32,12 @@ def main():
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--in-context", action="store_true")
     ap.add_argument("--topk", type=int, default=3)
+    ap.add_argument("--drop", default="", help="with --keep: comma-separated key prefixes to re-measure (e.g. wgrad)")
     args = ap.parse_args()
     cache = load_cache() if args.keep else {}
+    for pre in filter(None, args.drop.split(",")):
+        for k in [k for k in cache if k.startswith(pre)]:
+            del cache[k]
     for name in args.models.split(","):
         t0 = time.time()
         torch.manual_seed(0)
