@@ -9,8 +9,8 @@ DP path as the negative control (each rank normalises its own half).
 
 The whole-network gradient comparison is loose by nature (a 1e-5 forward difference between the B = 16
 and B = 32 kernel configurations grows to ~10% in the backward at init); the layer-local check
-(``local_dy_rel``, Model A) is exact: every backbone BN tail's dy on this rank against the closed-form
-backward with the globally all-reduced sums.
+(``local_dy_rel``) is exact: every BN tail's dy on this rank (Model A: the backbone's; Model C: all ~94
+BasicConv2d tails) against the closed-form backward with the globally all-reduced sums.
 
 Prints one JSON line per rank: {"rank", "sync", "grad_rel", "bn_rel", "bn_rank_rel", "loss_rel", "local_dy_rel"}.
     python -m torch.distributed.run --nproc-per-node 2 ... tests/syncbn_engine_worker.py MODEL SYNC
@@ -99,6 +99,34 @@ def local_syncbn_check(prog, world):
     return max(errs.values())
 
 
+def local_syncbn_check_inception(prog, world):
+    """The same chaos-free check for Model C: every BasicConv2d's BN-ReLU tail backward on this rank (its dz
+    from the engine's own gradient sources and stored y) against the closed form with the all-reduced
+    sum(dz), sum(dz xhat).  Returns the worst relative error over the ~94 layers."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_inception_gpu import _nchw
+    from test_mtl_layer_local_gpu import k4
+    from mtl_das_pytorch_amd.engine.inception import CBR
+    errs = []
+    for op in prog.ops:
+        if not isinstance(op, CBR):
+            continue
+        g = sum(_nchw(a) for a in op.out.grad_sources())
+        y = _nchw(op.y)
+        sc, sh, mu, inv = k4(op.bn)
+        dz = g * ((y * sc + sh) > 0)
+        xh = (y - mu) * inv
+        sums = torch.stack([dz.sum((0, 2, 3)), (dz * xh).sum((0, 2, 3))]).double().cpu()
+        dist.all_reduce(sums)
+        n = world * dz.shape[0] * dz.shape[2] * dz.shape[3]
+        m1, m2 = (sums / n).float().to(dz.device).view(2, 1, -1, 1, 1)
+        gam = op.bn.mods[0].weight.detach().view(1, -1, 1, 1)
+        errs.append(rel(_nchw(op.dy), gam * inv * (dz - m1 - xh * m2)))
+    print(json.dumps({"layers": len(errs), "worst": max(errs), "median": sorted(errs)[len(errs) // 2]}),
+          file=sys.stderr, flush=True)
+    return max(errs)
+
+
 def main():
     model_type, sync = sys.argv[1], int(sys.argv[2])
     ctx = init_distributed()
@@ -118,7 +146,7 @@ def main():
     runner.train_step(mine)
     torch.cuda.synchronize()
     g = prog.flat.grads.detach().clone() / world  # the data-parallel average
-    local = local_syncbn_check(prog, world) if not joint else None
+    local = local_syncbn_check(prog, world) if not joint else local_syncbn_check_inception(prog, world)
     # reference: one process, the whole 2B batch
     ref = build(model_type, world * B, dev, 1)
     ref.set_optimizer(weight_decay=0.0)

@@ -87,13 +87,12 @@ def test_engine_sync_bn(model):
         assert r["bn_rel_first8"] < 1e-4, r  # measured 2e-5 (C), plain DP > 1e-2
         if model == "MTL":  # 20 BN layers: no chaotic drift yet
             assert r["bn_rel"] < 1e-4 and r["loss_rel"] < 1e-4, r
-        if r["local_dy_rel"] is not None:  # Model A: every backbone BN backward uses the global sums
-            assert r["local_dy_rel"] < 2.5e-3, r  # bf16 rounding of dy (measured 1.7e-3)
+        # every BN backward uses the global sums (A: backbone tails, C: every BasicConv2d tail)
+        assert r["local_dy_rel"] < 2.5e-3, r  # bf16 rounding of dy (measured 1.7e-3 on A)
     for r in res[0]:  # negative control: local statistics
         assert r["bn_rank_rel"] > 1e-3 and r["bn_rel_first8"] > 1e-3, r
         assert r["bn_rel"] > 10 * max(q["bn_rel"] for q in res[1]), r
-        if r["local_dy_rel"] is not None:
-            assert r["local_dy_rel"] > 5e-2, r
+        assert r["local_dy_rel"] > 5e-2, r
     # whole-network gradient: SyncBN closer to the single process than plain DP (chaotic at init either way)
     assert max(r["grad_rel"] for r in res[1]) < 0.7 * min(r["grad_rel"] for r in res[0]), res
 
