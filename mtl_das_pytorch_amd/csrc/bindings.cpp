@@ -141,6 +141,18 @@ ConvArgs parse_conv(int mode, py::dict d) {
         (a.bpgs == 0 && (a.bygs != 0 || a.brgs != 0)))
       throw std::runtime_error("conv: bad fused BN-backward statistics arguments");
   }
+  if (d.contains("add") && !d["add"].is_none()) {  // extra gradient sources summed by the dgrad epilogue
+    py::list l = d["add"].cast<py::list>();
+    if (mode != MODE_DGRAD || l.size() > 3) throw std::runtime_error("conv: bad extra gradient sources");
+    for (size_t i = 0; i < l.size(); ++i) {
+      py::dict e = l[i].cast<py::dict>();
+      a.add[i] = P<const float>(e, "p");
+      a.addgs[i] = I(e, "gs");
+      a.ldadd[i] = (int)I(e, "ld");
+      if (!a.add[i] || a.ldadd[i] % 4 || a.ldadd[i] < a.N) throw std::runtime_error("conv: bad extra gradient source");
+    }
+    a.nadd = (int)l.size();
+  }
   if (d.contains("nol") && !d["nol"].is_none()) {  // normalise-on-load of the input (forward)
     py::dict n = d["nol"].cast<py::dict>();
     a.nbn = parse_bn(n["bn"].cast<py::dict>());
@@ -343,6 +355,10 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.attr("CONV_GLDS_NCFG") = CONV_GLDS_NCFG;
   m.attr("CONV_PATCH_CFG0") = CONV_PATCH_CFG0;
   m.attr("CONV_PATCH_NCFG") = CONV_PATCH_NCFG;
+  m.attr("CONV_GDEEP_CFG0") = CONV_GDEEP_CFG0;
+  m.attr("CONV_GDEEP_NCFG") = CONV_GDEEP_NCFG;
+  m.attr("CONV_PATCHP_CFG0") = CONV_PATCHP_CFG0;
+  m.attr("CONV_PATCHP_NCFG") = CONV_PATCHP_NCFG;
   m.def("wgrad", &wgrad);
   m.def("wgrad_finalize", &wgrad_finalize);
   m.def("tail_fwd", &tail_fwd);

@@ -327,6 +327,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
             for (int r = 0; r < 4; ++r) { s[r] += v[r]; ss[r] += v[r] * v[r]; }
           } else {
             float* o = reinterpret_cast<float*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
+            add_sources(a, z, (int64_t)m, n0, v);
             *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
             if (want_bnb && n0 < bN) {  // dz of the BN tail this gradient feeds, and its statistics
               const uint2 u = ypre[i][f], q = rpre[i][f];

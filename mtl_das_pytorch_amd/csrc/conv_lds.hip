@@ -58,49 +58,12 @@ struct TileCtx {
   int tid, lane, wid, wn, wm, l16, kgl, S, split, nt, ntn, z, mbase, nbase, Mq, HWq, Wq, oy0, ox0, bN;
 };
 
-template <bool FWD, bool BNS, int BM, int BN, int WAM, int WM, int WN, int FN, int FM>
-DEV void tile_epilogue(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f32x4 (&acc)[FN][FM], float* s_st,
-                       const float* s_k, int* s_flag) {
-  // ---- cross-block split of K: deterministic last-arriver reduction
-  if (t.S > 1) {
-    const int64_t tile = ((int64_t)t.z * gridDim.x + blockIdx.x) * t.ntn + t.nt;
-    float4* slab = reinterpret_cast<float4*>(a.ws) + tile * t.S * (BM * BN / 4);
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int f = 0; f < FM; ++f)
-        slab[(int64_t)t.split * (BM * BN / 4) + ((t.wid * FN + i) * FM + f) * 64 + t.lane] =
-            make_float4(acc[i][f][0], acc[i][f][1], acc[i][f][2], acc[i][f][3]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t.tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned tk = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_flag[0] = tk == (unsigned)(t.S - 1);
-    }
-    __syncthreads();
-    if (!s_flag[0]) return;
-    if (t.tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reusable next launch
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int f = 0; f < FM; ++f) {
-        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < t.S; ++s) {
-          const float4 u = slab[(int64_t)s * (BM * BN / 4) + ((t.wid * FN + i) * FM + f) * 64 + t.lane];
-          v[0] += u.x; v[1] += u.y; v[2] += u.z; v[3] += u.w;
-        }
-        acc[i][f] = v;
-      }
-  }
-
-  // ---- epilogue (lane: pixel l16 of each fragment, channels 4*kgl .. +3)
+// Epilogue stores of one output tile (lane: pixel l16 of each fragment, channels 4*kgl .. +3): bias + bf16
+// store (forward) / extra gradient sources + fp32 store (data gradient), and this lane's share of the BN
+// statistics accumulated into st[i][stat][r] (summed over the tiles of a persistent block before the flush).
+template <bool FWD, bool BNS, int BN, int WM, int WN, int FN, int FM>
+DEV void tile_store(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f32x4 (&acc)[FN][FM], const float* s_k,
+                    float (&st)[FN][3][4]) {
   int orow[FM];
   bool pv[FM];
 #pragma unroll
@@ -112,8 +75,6 @@ DEV void tile_epilogue(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f
     const int i = r / t.Wq, jj = r - i * t.Wq;
     orow[f] = (b * a.Ho + t.oy0 + i * pl.qy) * a.Wo + t.ox0 + jj * pl.qx;
   }
-  const bool want_stats = FWD && a.stats != nullptr;
-  const bool want_red = want_stats || BNS;
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
     const int n0 = t.nbase + t.wn * WN + i * 16 + 4 * t.kgl;
@@ -124,7 +85,6 @@ DEV void tile_epilogue(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f
 #pragma unroll
       for (int r = 0; r < 4; ++r) bias[r] = a.bias[a.bgs * t.z + n0 + r];
     }
-    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
       if (!(nok && pv[f])) continue;
@@ -138,9 +98,10 @@ DEV void tile_epilogue(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f
         w.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
         *reinterpret_cast<uint2*>(o) = w;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { s[r] += v[r]; ss[r] += v[r] * v[r]; }
+        for (int r = 0; r < 4; ++r) { st[i][0][r] += v[r]; st[i][1][r] += v[r] * v[r]; }
       } else {
         float* o = reinterpret_cast<float*>(a.out) + a.ogs * t.z + (int64_t)orow[f] * a.ldo + n0;
+        add_sources(a, t.z, (int64_t)orow[f], n0, v);
         *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
         if (BNS && n0 < t.bN) {  // dz of the BN tail this gradient feeds, and its statistics
           const uint2 u = *reinterpret_cast<const uint2*>(a.by + a.bygs * t.z + (int64_t)orow[f] * a.ldby + n0);
@@ -168,48 +129,112 @@ DEV void tile_epilogue(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f
               dz = (tv + rr) > 0.f ? dz : 0.f;
             }
             const float xh = (yv[r] - s_k[2 * BN + cl + r]) * s_k[3 * BN + cl + r];
-            s[r] += dz;
-            ss[r] += dz * xh;
-            s2[r] += dz * xh2;
+            st[i][0][r] += dz;
+            st[i][1][r] += dz * xh;
+            st[i][2][r] += dz * xh2;
           }
         }
       }
     }
-    if (want_red) {
+  }
+}
+
+// Block reduction of the accumulated statistics and one fp64 atomic per (channel, statistic) into replica
+// blockIdx.x % nrep: forward (sum y, sum y^2) rows of [G][NREP][2][N], or the fused BN-backward rows 0/1 (2
+// with a BN2 residual) of the tail's [G][NREP][3][bN].
+template <bool FWD, bool BNS, int BN, int WAM, int WN, int FN>
+DEV void tile_flush(const ConvArgs& a, const TileCtx& t, float (&st)[FN][3][4], float* s_st) {
+  const bool want_red = (FWD && a.stats != nullptr) || BNS;
+  if (!want_red) return;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {  // the 16 pixels of a lane row -> lane 15 (DPP, common.h)
-        s[r] = row16_sum(s[r]);
-        ss[r] = row16_sum(ss[r]);
-        if (BNS) s2[r] = row16_sum(s2[r]);
-      }
-      if (t.l16 == 15) {
+  for (int i = 0; i < FN; ++i) {
+    const int cl = t.wn * WN + i * 16 + 4 * t.kgl;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s_st[(t.wm * BN + cl + r) * 3 + 0] = s[r];
-          s_st[(t.wm * BN + cl + r) * 3 + 1] = ss[r];
-          s_st[(t.wm * BN + cl + r) * 3 + 2] = s2[r];
-        }
+    for (int r = 0; r < 4; ++r) {  // the 16 pixels of a lane row -> lane 15 (DPP, common.h)
+      st[i][0][r] = row16_sum(st[i][0][r]);
+      st[i][1][r] = row16_sum(st[i][1][r]);
+      if (BNS) st[i][2][r] = row16_sum(st[i][2][r]);
+    }
+    if (t.l16 == 15) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s_st[(t.wm * BN + cl + r) * 3 + 0] = st[i][0][r];
+        s_st[(t.wm * BN + cl + r) * 3 + 1] = st[i][1][r];
+        s_st[(t.wm * BN + cl + r) * 3 + 2] = BNS ? st[i][2][r] : 0.f;
       }
     }
   }
-  if (want_red) {
+  __syncthreads();
+  const int rep = blockIdx.x % (BNS ? a.bbn.pnrep : a.stats_nrep);
+  double* dst = BNS ? a.bpart : a.stats;
+  const int rows = BNS ? 3 : 2, nrow = BNS && a.br_bn ? 3 : 2, nlim = BNS ? t.bN : a.N;
+  const int64_t gb = BNS ? (a.bpgs < 0 ? (int64_t)t.z * NREP * 3 * t.bN : (int64_t)t.z * a.bpgs)
+                         : (int64_t)t.z * NREP * 2 * a.N;
+  for (int q = t.tid; q < BN * 3; q += 256) {
+    const int c = q / 3, which = q - c * 3;
+    const int n = t.nbase + c;
+    if (n < nlim && which < nrow) {
+      float v = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < WAM; ++w2) v += s_st[(w2 * BN + c) * 3 + which];
+      atomicAdd(dst + gb + ((int64_t)rep * rows + which) * nlim + n, (double)v);
+    }
+  }
+}
+
+template <bool FWD, bool BNS, int BM, int BN, int WAM, int WM, int WN, int FN, int FM>
+DEV void tile_epilogue(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f32x4 (&acc)[FN][FM], float* s_st,
+                       const float* s_k, int* s_flag) {
+  // ---- cross-block split of K: deterministic last-arriver reduction.  The fp32 partial tiles are stored
+  // WRITE-THROUGH (sc1 buffer stores: they leave the XCD's L2 at once, so no agent-scope release fence --
+  // an L2 write-back of ~6.5 us with 16 KB dirtied per block), every wave drains them, one lane draws the
+  // tile's arrival ticket (agent-scope atomic), and the last arriver reads all partials with sc1 loads
+  // (L1 bypassed: no acquire fence either) in split order.
+  if (t.S > 1) {
+    const int64_t tile = ((int64_t)t.z * gridDim.x + blockIdx.x) * t.ntn + t.nt;
+    const uint64_t base = reinterpret_cast<uint64_t>(a.ws + tile * t.S * (BM * BN));
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, t.S * BM * BN * 4, 0x00020000);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        const u32x4 v = {__float_as_uint(acc[i][f][0]), __float_as_uint(acc[i][f][1]), __float_as_uint(acc[i][f][2]),
+                         __float_as_uint(acc[i][f][3])};
+        const int off = ((t.split * (BM * BN / 4) + ((t.wid * FN + i) * FM + f) * 64 + t.lane)) * 16;
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);  // aux 16 = sc1
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its partial tile
     __syncthreads();
-    const int rep = blockIdx.x % (BNS ? a.bbn.pnrep : a.stats_nrep);
-    double* dst = BNS ? a.bpart : a.stats;
-    const int rows = BNS ? 3 : 2, nrow = BNS && a.br_bn ? 3 : 2, nlim = BNS ? t.bN : a.N;
-    const int64_t gb = BNS ? (a.bpgs < 0 ? (int64_t)t.z * NREP * 3 * t.bN : (int64_t)t.z * a.bpgs)
-                           : (int64_t)t.z * NREP * 2 * a.N;
-    for (int q = t.tid; q < BN * 3; q += 256) {
-      const int c = q / 3, which = q - c * 3;
-      const int n = t.nbase + c;
-      if (n < nlim && which < nrow) {
-        float v = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < WAM; ++w2) v += s_st[(w2 * BN + c) * 3 + which];
-        atomicAdd(dst + gb + ((int64_t)rep * rows + which) * nlim + n, (double)v);
-      }
+    if (t.tid == 0) {
+      const unsigned tk = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_flag[0] = tk == (unsigned)(t.S - 1);
     }
+    __syncthreads();
+    if (!s_flag[0]) return;
+    if (t.tid == 0) __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reusable
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int sp = 0; sp < t.S; ++sp) {
+          const int off = ((sp * (BM * BN / 4) + ((t.wid * FN + i) * FM + f) * 64 + t.lane)) * 16;
+          const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+          v[0] += __uint_as_float(u[0]); v[1] += __uint_as_float(u[1]);
+          v[2] += __uint_as_float(u[2]); v[3] += __uint_as_float(u[3]);
+        }
+        acc[i][f] = v;
+      }
   }
+
+  float st[FN][3][4] = {};
+  tile_store<FWD, BNS, BN, WM, WN, FN, FM>(a, pl, t, acc, s_k, st);
+  tile_flush<FWD, BNS, BN, WAM, WN, FN>(a, t, st, s_st);
 }
 
 template <int MODE, int BM, int BN, int WAM, int KC>
@@ -435,6 +460,9 @@ constexpr int GL_BM[GL_NT] = {64, 128, 64, 128, 256, 128, 256, 64};
 constexpr int GL_BN[GL_NT] = {64, 64, 128, 128, 64, 32, 128, 32};
 constexpr int GL_WAM[GL_NT] = {2, 2, 2, 2, 4, 4, 2, 4};
 constexpr int GL_KC = 64, GL_STAGES = 3;
+// ring stages of the deep configs: as many 128-byte-row stages as fit ~150 KB of LDS, at most 8, and at
+// most 2 + 63 / NPER (the counted vmcnt of NST - 2 chunks in flight must fit the 6-bit counter); 3 = none
+constexpr int GL_NST_DEEP[GL_NT] = {8, 6, 6, 4, 3, 7, 3, 8};
 
 __device__ uint4 g_zero16[4];  // never written: the source of every padding lane
 
@@ -443,7 +471,31 @@ typedef __attribute__((address_space(1))) void* glb_vptr;
 
 DEV int gl_swz(int r, int g) { return g ^ ((r >> 1) & 7); }
 
-template <int MODE, int BM, int BN, int WAM>
+// wait until at most `ahead` chunks (NPER DMA instructions each) of this wave are still in flight
+template <int NPER, int NST>
+DEV void gl_wait_ahead(int ahead) {
+  static_assert((NST - 2) * NPER <= 63, "vmcnt is a 6-bit counter");
+  switch (ahead) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPER) : "memory"); break;
+    case 2: if constexpr (NST > 3) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPER) : "memory"); break; }
+            [[fallthrough]];
+    case 3: if constexpr (NST > 4) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPER) : "memory"); break; }
+            [[fallthrough]];
+    case 4: if constexpr (NST > 5) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NPER) : "memory"); break; }
+            [[fallthrough]];
+    case 5: if constexpr (NST > 6) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * NPER) : "memory"); break; }
+            [[fallthrough]];
+    default: if constexpr (NST > 7) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * NPER) : "memory"); break; }
+             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// NST = stages of the LDS ring: 3 (GL_STAGES, the streaming configs) or up to 8 for the "deep" configs,
+// whose blocks issue the DMAs of up to NST - 1 K chunks before waiting for the first -- a block of a
+// small-M, long-K layer (Model C's 4x13 / 1x6 Inception convs) pays ONE load latency instead of a chain
+// of them.
+template <int MODE, int BM, int BN, int WAM, int NST>
 __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a, LdsPlan pl) {
   constexpr int WAN = 4 / WAM;
   constexpr int WM = BM / WAM, WN = BN / WAN, FM = WM / 16, FN = WN / 16;
@@ -457,7 +509,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a, LdsPlan pl) 
   constexpr bool FWD = MODE == MODE_FWD;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int* s_tx = reinterpret_cast<int*>(smem + GL_STAGES * BUF);  // input coordinates / channel per k-group
+  int* s_tx = reinterpret_cast<int*>(smem + NST * BUF);        // input coordinates / channel per k-group
   int* s_tw = s_tx + pl.ntab;                                  // weight column per k-group
   float* s_st = reinterpret_cast<float*>(s_tw + pl.ntab);      // [WAM][BN][3] epilogue sums
   float* s_k = s_st + WAM * BN * 3;                             // BNS: [8][BN] constants
@@ -581,19 +633,19 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a, LdsPlan pl) 
     for (int f = 0; f < FM; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   __syncthreads();  // tables and constants (no DMA in flight yet)
-  if (cb < ce) issue(cb, 0);
-  if (cb + 1 < ce) issue(cb + 1, 1);
+#pragma unroll
+  for (int j = 0; j < NST - 1; ++j)
+    if (cb + j < ce) issue(cb + j, j);
   for (int ch = cb; ch < ce; ++ch) {
     const int k = ch - cb;
-    // this wave's DMAs of chunk ch have landed (chunk ch + 1's may still fly), then every wave's have,
-    // and every wave is done reading chunk ch - 1 (whose buffer chunk ch + 2 overwrites)
-    if (ch + 1 < ce) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPER) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's DMAs of chunk ch have landed (the up to NST - 2 later chunks may still fly), then every
+    // wave's have, and every wave is done reading chunk ch - 1 (whose buffer chunk ch + NST - 1 overwrites)
+    gl_wait_ahead<NPER, NST>(min(ce - 1, ch + NST - 2) - ch);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (ch + 2 < ce) issue(ch + 2, (k + 2) % GL_STAGES);
-    const char* A = smem + (k % GL_STAGES) * BUF;
+    if (ch + NST - 1 < ce) issue(ch + NST - 1, (k + NST - 1) % NST);
+    const char* A = smem + (k % NST) * BUF;
     const char* Bq = A + BN * ROWB;
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
@@ -657,6 +709,7 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a, PatchPlan p
   static_assert(FM >= 1 && FN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
   constexpr int CBP = CB + 8, KS = pt_ksteps<CB>(), WKP = pt_wkp<CB>();
   constexpr int CG = CB / 8;  // 16-byte channel groups of a strip pixel
+  static_assert(256 % CG == 0, "a thread's strip units keep one channel group");
   constexpr int NU = 8;       // staging units per thread per round
   constexpr bool FWD = lds_fwd<MODE>();
   constexpr bool NOL = MODE == MODE_FWD_NOL;
@@ -724,6 +777,15 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a, PatchPlan p
   __syncthreads();  // NOL / BNS constants
   for (int sl = 0; sl < pp.nslice; ++sl) {
     const int cs0 = sl * CB;
+    // NOL: a thread's strip units all carry channel group tid % CG (CG divides 256), so its 8 scale and
+    // 8 shift constants live in registers for the whole slice (an LDS read per element cost ~17 us on
+    // the 47x122 stem conv)
+    float nsc[8], nsh[8];
+    if (NOL) {
+      const int c = cs0 + (tid % CG) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { nsc[j] = s_k[c + j]; nsh[j] = s_k[a.Cs + c + j]; }
+    }
     // ---- stage the strip slice and the weight slice: unit u < nux -> strip (row j, column q, group g),
     // else weight (row n, k-group g: tap g / CG, channel 8 (g % CG))
     for (int u0 = 0; u0 < nut; u0 += 256 * NU) {
@@ -758,12 +820,11 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a, PatchPlan p
           const int g = u % CG, pix = u / CG;
           uint4 x = v[i];
           if (NOL && ((okm >> i) & 1)) {  // act(BN(y)) of the producing conv, once per element
-            const int c = cs0 + g * 8;
             uint32_t w4[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
-              float lo = __uint_as_float(w4[h] << 16) * s_k[c + 2 * h] + s_k[a.Cs + c + 2 * h];
-              float hi = __uint_as_float(w4[h] & 0xffff0000u) * s_k[c + 2 * h + 1] + s_k[a.Cs + c + 2 * h + 1];
+              float lo = __uint_as_float(w4[h] << 16) * nsc[2 * h] + nsh[2 * h];
+              float hi = __uint_as_float(w4[h] & 0xffff0000u) * nsc[2 * h + 1] + nsh[2 * h + 1];
               if (a.nol_kind == ACT_RELU) { lo = fmaxf(lo, 0.f); hi = fmaxf(hi, 0.f); }
               w4[h] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
             }
@@ -805,6 +866,157 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a, PatchPlan p
   tile_epilogue<FWD, BNS, BM, BN, WAM, WM, WN, FN, FM>(a, pl, tc, acc, s_st, s_k, s_flag);
 }
 
+// Persistent, software-pipelined patch conv (cfg CONV_PATCHP_CFG0 + 3 * tile + cb; one channel slice,
+// Cs == CB).  The one-strip-per-block form above stages, then computes: its blocks expose the load latency
+// and only the 2-3 co-resident blocks hide it.  Here a block stages its BN x 9 CB weights once, then loops
+// over strips u = blockIdx.x, + gridDim.x, ...: the next strip goes global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, no registers) into the other of two strip buffers while the MFMAs of the
+// current one run; the BN statistics are summed in registers over all of the block's strips and flushed
+// once.  Strip image: dense [pixel q][CG 16-byte groups], group g of pixel q in slot g ^ ((q / (16 / CG)) %
+// CG): the 16 pixels of an MFMA fragment read (16 consecutive q, one g) hit 16 distinct slots of the
+// 256-byte bank rows.  Padding / halo bytes are DMA'd from a zero page.
+template <int MODE, int BM, int BN, int WAM, int CB>
+__global__ __launch_bounds__(256) void conv_patchp_kernel(ConvArgs a, PatchPlan pp) {
+  constexpr int WAN = 4 / WAM;
+  constexpr int WM = BM / WAM, WN = BN / WAN, FM = WM / 16, FN = WN / 16;
+  static_assert(FM >= 1 && FN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
+  constexpr int KS = pt_ksteps<CB>(), WKP = pt_wkp<CB>();
+  constexpr int CG = CB / 8, PPR = 16 / CG;  // 16-byte groups per pixel, pixels per 256-byte bank row
+  constexpr bool FWD = MODE == MODE_FWD;
+  constexpr bool BNS = MODE == MODE_DGRAD_BNS;
+  static_assert(MODE != MODE_FWD_NOL, "the DMA bypasses registers: no on-load transform");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int WP = pp.Wout + 2, SR = pp.R + 2;
+  const int nq = SR * WP;                       // strip pixels
+  const int nins = (nq * CG + 63) / 64;         // 1-KB DMA instructions per strip
+  const int SBP = nins * 1024;                  // bytes of one strip buffer
+  bf16_t* s_w = reinterpret_cast<bf16_t*>(smem + 2 * SBP);
+  float* s_st = reinterpret_cast<float*>(s_w + BN * WKP);  // [WAM][BN][3] epilogue sums
+  float* s_k = s_st + WAM * BN * 3;                         // BNS: [8][BN] constants
+  int* s_flag = reinterpret_cast<int*>(s_k + (BNS ? 8 * BN : 0));
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, kgl = lane >> 4;
+  const int wn = wid % WAN, wm = wid / WAN;
+  const int z = blockIdx.z, nt = blockIdx.y, ntn = gridDim.y;
+  const int nbase = nt * BN;
+  const int HWo = pp.Hout * pp.Wout;
+  const int U = a.B * pp.nstrip;
+  const int bN = a.bN > 0 ? a.bN : a.N;
+  const int zb = a.bpgs == 0 ? 0 : z;
+  if (BNS) {
+    for (int i = tid; i < BN; i += 256) {
+      const int n = nbase + i;
+      float k[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (n < bN) {
+        bn_channel_bwd(a.bbn, zb, n, k[0], k[1], k[2], k[3]);
+        if (a.br_bn) bn_channel_bwd(a.bbn2, zb, n, k[4], k[5], k[6], k[7]);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s_k[q * BN + i] = k[q];
+    }
+  }
+  const bf16_t* wz = a.w + a.wgs * z;
+  const bf16_t* base0 = a.src.p[0] + a.src.gs[0] * z;
+  const bf16_t* base1 = a.src.p[1] ? a.src.p[1] + a.src.gs[1] * z : base0;
+  const int ld0 = a.src.ld[0], ld1 = a.src.ld[1];
+  const void* zero = &g_zero16[0];
+
+  // ---- strip DMA: instruction j of wave w writes strip bytes [(4j + w) KB, +1 KB); lane l fetches 16-byte
+  // unit v = 64 (4j + w) + l = (pixel q, slot): the pixel's channel group slot ^ swz(q)
+  auto issue = [&](int u, char* buf) {
+    const int b = u / pp.nstrip, oh0 = (u - b * pp.nstrip) * pp.R;
+    const int row0 = oh0 + pp.dy0;
+    for (int j = 0; 4 * j + wid < nins; ++j) {
+      const int v = 64 * (4 * j + wid) + lane;
+      const int q = v / CG, slot = v - q * CG;
+      const void* src = zero;
+      if (q < nq) {
+        const int jr = q / WP, qc = q - jr * WP;
+        const int ih = row0 + jr, iw = pp.dx0 + qc;
+        if (ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) {
+          const int c = (slot ^ ((q / PPR) % CG)) * 8;
+          const int seg = (a.src.C1 > 0 && c >= a.src.C0) ? 1 : 0;
+          src = (seg ? base1 : base0) + ((int64_t)(b * a.Hs + ih) * a.Ws + iw) * (seg ? ld1 : ld0) + (c - seg * a.src.C0);
+        }
+      }
+      __builtin_amdgcn_global_load_lds((glb_vptr)src, (lds_vptr)(buf + (4 * j + wid) * 1024), 16, 0, 0);
+    }
+  };
+
+  // ---- weights once: [BN][WKP], k-group g = tap g / CG, channels 8 (g % CG) (zero past 9 CB / Npad)
+  for (int w = tid; w < BN * (WKP / 8 - 1); w += 256) {
+    const int g = w % (WKP / 8 - 1), n = nbase + w / (WKP / 8 - 1);
+    const int tap = g / CG;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (tap < 9 && n < a.Npad) v = *reinterpret_cast<const uint4*>(wz + (int64_t)n * a.Kpad + tap * a.Cs + (g - tap * CG) * 8);
+    *reinterpret_cast<uint4*>(s_w + (w / (WKP / 8 - 1)) * WKP + g * 8) = v;
+  }
+
+  // fragment bases: strip pixel of tap (0, 0) for this lane's pixel of each M fragment
+  int q0[FM];
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    int p = wm * WM + f * 16 + l16;
+    p = p < pp.R * pp.Wout ? p : 0;  // past the strip: any in-LDS pixel (the epilogue drops them)
+    const int r = p / pp.Wout, c = p - r * pp.Wout;
+    q0[f] = r * WP + c;
+  }
+
+  float st[FN][3][4] = {};
+  LdsPlan pl{};
+  pl.qy = 1; pl.qx = 1;
+  int cur = 0;
+  if ((int)blockIdx.x < U) issue(blockIdx.x, smem);
+  __syncthreads();  // weights and constants
+  for (int u = blockIdx.x; u < U; u += gridDim.x) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of strip u (and its last stores)
+    __builtin_amdgcn_s_barrier();                      // ... and every wave's; strip u - grid fully read
+    asm volatile("" ::: "memory");
+    if (u + (int)gridDim.x < U) issue(u + gridDim.x, smem + (cur ^ 1) * SBP);
+    const char* X = smem + cur * SBP;
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int f = 0; f < FM; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int g = 4 * ks + kgl;
+      const int tap = g / CG < 9 ? g / CG : 0;  // k past 9 CB: zero weights, any strip element
+      const int kh = tap / 3, kw = tap - kh * 3;
+      const int dq = (FWD ? kh : 2 - kh) * WP + (FWD ? kw : 2 - kw);
+      const int cg = g - (g / CG) * CG;
+      bf16x8 afr[FN], bfr[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+        afr[i] = *reinterpret_cast<const bf16x8*>(s_w + (wn * WN + i * 16 + l16) * WKP + g * 8);
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        const int q = q0[f] + dq;
+        bfr[f] = *reinterpret_cast<const bf16x8*>(X + (q * CG + (cg ^ ((q / PPR) % CG))) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int f = 0; f < FM; ++f) acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], bfr[f], acc[i][f], 0, 0, 0);
+    }
+    const int b = u / pp.nstrip, oh0 = (u - b * pp.nstrip) * pp.R;
+    const int rows = min(pp.R, pp.Hout - oh0);
+    const int mbase = b * HWo + oh0 * pp.Wout;
+    const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, 1, 0, nt, ntn, z, mbase, nbase, mbase + rows * pp.Wout, HWo,
+                     pp.Wout, 0, 0, bN};
+    tile_store<FWD, BNS, BN, WM, WN, FN, FM>(a, pl, tc, acc, s_k, st);
+    cur ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // the strip buffers are dead; s_st lives past the weights
+  const TileCtx tf{tid, lane, wid, wn, wm, l16, kgl, 1, 0, nt, ntn, z, 0, nbase, 0, HWo, pp.Wout, 0, 0, bN};
+  tile_flush<FWD, BNS, BN, WAM, WN, FN>(a, tf, st, s_st);
+}
+
 // Strip plan of a patch launch (host); returns 0 or -2 when the conv is not a 3x3 / stride-1 conv this
 // tile can take.  FWD: output Ho x Wo from the input (Hs, Ws); DGRAD: dx (Ho, Wo) from dy (Hs, Ws).
 int patch_plan(int mode, const ConvArgs& a, int tile, int cbi, PatchPlan& pp, size_t& lds) {
@@ -831,6 +1043,51 @@ int patch_plan(int mode, const ConvArgs& a, int tile, int cbi, PatchPlan& pp, si
   return 0;
 }
 
+// LDS bytes of the persistent form: two dense strip buffers (whole 1-KB DMA instructions) + the weights
+size_t patchp_lds(const PatchPlan& pp, int tile, int cbi, bool bns) {
+  const int CB = PT_CB[cbi], BN = PT_BN[tile], WAM = PT_WAM[tile], CG = CB / 8;
+  const int wkp = ((9 * CB + 31) / 32) * 32 + 8;
+  const size_t sbp = (size_t)((pp.R + 2) * (pp.Wout + 2) * CG + 63) / 64 * 1024;
+  return 2 * sbp + (size_t)BN * wkp * 2 + ((size_t)WAM * BN * 3 + (bns ? 8 * BN : 0)) * 4 + 16;
+}
+
+int patchp_check(int mode, const ConvArgs& a, int tile, int cbi, PatchPlan& pp, size_t& lds) {
+  size_t l1;
+  int rc = patch_plan(mode, a, tile, cbi, pp, l1);
+  if (rc) return rc;
+  if (mode == MODE_FWD_NOL || pp.nslice != 1) return -2;
+  lds = patchp_lds(pp, tile, cbi, mode == MODE_DGRAD_BNS);
+  return lds > 160 * 1024 ? -2 : 0;
+}
+
+template <int MODE>
+int launch_patchp(const ConvArgs& a, int G, int tile, int cbi, hipStream_t st) {
+  if constexpr (MODE == MODE_FWD_NOL) {
+    return -2;
+  } else {
+    PatchPlan pp;
+    size_t lds;
+    int rc = patchp_check(MODE, a, tile, cbi, pp, lds);
+    if (rc) return rc;
+    const int ntn = (a.N + PT_BN[tile] - 1) / PT_BN[tile];
+    const int per_cu = std::max<int>(1, (int)(160 * 1024 / lds));
+    const int U = a.B * pp.nstrip;
+    const int nblk = std::max(1, std::min(U, (256 * per_cu + ntn * G - 1) / (ntn * G)));
+    dim3 grid(nblk, ntn, G);
+#define PP_LAUNCH(T, C)                                                                                     \
+  if (tile == T && cbi == C) {                                                                              \
+    hipLaunchKernelGGL((conv_patchp_kernel<MODE, PT_BM[T], PT_BN[T], PT_WAM[T], PT_CB[C]>), grid, dim3(256), lds, \
+                       st, a, pp);                                                                          \
+    return (int)hipGetLastError();                                                                          \
+  }
+#define PP_TILE(T) PP_LAUNCH(T, 0) PP_LAUNCH(T, 1) PP_LAUNCH(T, 2)
+    PP_TILE(0) PP_TILE(1) PP_TILE(2) PP_TILE(3) PP_TILE(4)
+#undef PP_TILE
+#undef PP_LAUNCH
+    return -1;
+  }
+}
+
 template <int MODE>
 int launch_patch(const ConvArgs& a, int G, int tile, int cbi, hipStream_t st) {
   PatchPlan pp;
@@ -851,8 +1108,10 @@ int launch_patch(const ConvArgs& a, int G, int tile, int cbi, hipStream_t st) {
   return -1;
 }
 
-bool patch_cfg(int cfg, int& tile, int& cbi) {
-  const int k = cfg - CONV_PATCH_CFG0;
+// patch conv config -> (tile, channel slice, persistent form)
+bool patch_cfg(int cfg, int& tile, int& cbi, bool& pers) {
+  pers = cfg >= CONV_PATCHP_CFG0;
+  const int k = cfg - (pers ? CONV_PATCHP_CFG0 : CONV_PATCH_CFG0);
   if (k < 0 || k >= PT_NT * 3) return false;
   tile = k / 3;
   cbi = k % 3;
@@ -863,16 +1122,20 @@ bool patch_cfg(int cfg, int& tile, int& cbi) {
 struct LdsCfg {
   int tile, BM, BN, WAM, KC, splits;
   bool glds;  // LDS-DMA kernel (conv_glds_kernel)
+  int nst;    // its ring stages
 };
 
 int decode_cfg(int cfg, LdsCfg& c) {
-  c.glds = cfg >= CONV_GLDS_CFG0 && cfg < CONV_GLDS_CFG0 + CONV_GLDS_NCFG;
-  if (c.glds) {  // cfg = CONV_GLDS_CFG0 + 4 * tile + log2(splits)
-    const int k = cfg - CONV_GLDS_CFG0;
+  const bool deep = cfg >= CONV_GDEEP_CFG0 && cfg < CONV_GDEEP_CFG0 + CONV_GDEEP_NCFG;
+  c.glds = deep || (cfg >= CONV_GLDS_CFG0 && cfg < CONV_GLDS_CFG0 + CONV_GLDS_NCFG);
+  if (c.glds) {  // cfg = CONV_GLDS_CFG0 (or CONV_GDEEP_CFG0) + 4 * tile + log2(splits)
+    const int k = cfg - (deep ? CONV_GDEEP_CFG0 : CONV_GLDS_CFG0);
     c.tile = k / 4;
     c.KC = GL_KC;
     c.splits = 1 << (k % 4);
     c.BM = GL_BM[c.tile]; c.BN = GL_BN[c.tile]; c.WAM = GL_WAM[c.tile];
+    c.nst = deep ? GL_NST_DEEP[c.tile] : GL_STAGES;
+    if (deep && c.nst <= GL_STAGES) return -2;  // no deeper ring fits this tile
     return 0;
   }
   const int k = cfg - CONV_LDS_CFG0;
@@ -931,7 +1194,7 @@ int make_plan(int mode, const ConvArgs& a, const LdsCfg& c, LdsPlan& pl, int& gx
 }
 
 size_t glds_lds_bytes(const LdsCfg& c, const LdsPlan& pl, bool bns) {
-  return (size_t)GL_STAGES * (c.BM + c.BN) * GL_KC * 2 + (size_t)2 * pl.ntab * 4 +
+  return (size_t)c.nst * (c.BM + c.BN) * GL_KC * 2 + (size_t)2 * pl.ntab * 4 +
          ((size_t)c.WAM * c.BN * 3 + (bns ? 8 * c.BN : 0)) * 4 + 16;
 }
 
@@ -944,13 +1207,15 @@ int launch_glds(const ConvArgs& a, int G, const LdsCfg& c, const LdsPlan& pl, in
     const size_t lds = glds_lds_bytes(c, pl, MODE == MODE_DGRAD_BNS);
     if (lds > 160 * 1024) return -2;
     dim3 grid(gx, ntn * c.splits, G);
-#define GL_LAUNCH(T)                                                                                      \
-  if (c.tile == T) {                                                                                      \
-    hipLaunchKernelGGL((conv_glds_kernel<MODE, GL_BM[T], GL_BN[T], GL_WAM[T]>), grid, dim3(256), lds, st, a, pl); \
+#define GL_LAUNCH_N(T, NS)                                                                                \
+  if (c.tile == T && c.nst == NS) {                                                                       \
+    hipLaunchKernelGGL((conv_glds_kernel<MODE, GL_BM[T], GL_BN[T], GL_WAM[T], NS>), grid, dim3(256), lds, st, a, pl); \
     return (int)hipGetLastError();                                                                        \
   }
+#define GL_LAUNCH(T) GL_LAUNCH_N(T, GL_STAGES) if constexpr (GL_NST_DEEP[T] > GL_STAGES) { GL_LAUNCH_N(T, GL_NST_DEEP[T]) }
     GL_LAUNCH(0) GL_LAUNCH(1) GL_LAUNCH(2) GL_LAUNCH(3) GL_LAUNCH(4) GL_LAUNCH(5) GL_LAUNCH(6) GL_LAUNCH(7)
 #undef GL_LAUNCH
+#undef GL_LAUNCH_N
     return -1;
   }
 }
@@ -987,12 +1252,13 @@ int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_
   if (mode == MODE_FWD && a.nol) mode = MODE_FWD_NOL;  // the launch mode launch_conv will pick
   if (mode == MODE_DGRAD && a.bpart) mode = MODE_DGRAD_BNS;
   int tile, cbi;
-  if (patch_cfg(cfg, tile, cbi)) {
+  bool pers;
+  if (patch_cfg(cfg, tile, cbi, pers)) {
     PatchPlan pp;
     size_t lds;
     ws_floats = 0;
     ntickets = 0;
-    return patch_plan(mode, a, tile, cbi, pp, lds);
+    return pers ? patchp_check(mode, a, tile, cbi, pp, lds) : patch_plan(mode, a, tile, cbi, pp, lds);
   }
   LdsCfg c;
   int rc = decode_cfg(cfg, c);
@@ -1010,12 +1276,14 @@ int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_
 
 int launch_conv_lds(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
   int tile, cbi;
-  if (patch_cfg(cfg, tile, cbi)) {
+  bool pers;
+  if (patch_cfg(cfg, tile, cbi, pers)) {
     switch (mode) {
-      case MODE_FWD: return launch_patch<MODE_FWD>(a, G, tile, cbi, st);
-      case MODE_FWD_NOL: return launch_patch<MODE_FWD_NOL>(a, G, tile, cbi, st);
-      case MODE_DGRAD: return launch_patch<MODE_DGRAD>(a, G, tile, cbi, st);
-      case MODE_DGRAD_BNS: return launch_patch<MODE_DGRAD_BNS>(a, G, tile, cbi, st);
+      case MODE_FWD: return pers ? launch_patchp<MODE_FWD>(a, G, tile, cbi, st) : launch_patch<MODE_FWD>(a, G, tile, cbi, st);
+      case MODE_FWD_NOL: return pers ? -2 : launch_patch<MODE_FWD_NOL>(a, G, tile, cbi, st);
+      case MODE_DGRAD: return pers ? launch_patchp<MODE_DGRAD>(a, G, tile, cbi, st) : launch_patch<MODE_DGRAD>(a, G, tile, cbi, st);
+      case MODE_DGRAD_BNS:
+        return pers ? launch_patchp<MODE_DGRAD_BNS>(a, G, tile, cbi, st) : launch_patch<MODE_DGRAD_BNS>(a, G, tile, cbi, st);
       default: return -1;
     }
   }

@@ -49,12 +49,30 @@ struct ConvArgs {
   // group updates that BN's running statistics and publishes its constants (BNArgs::consts).
   BNArgs nbn;
   int nol, nol_kind;
+  // DGRAD only, optional (nadd = 0 off): up to 3 more fp32 gradient sources of the same [M][N] tensor
+  // ([M][ldadd] + z * addgs) added in the epilogue, so the output is the WHOLE gradient of the BN tail it
+  // feeds (one source: its statistics can then be fused above, and the tail runs apply-only)
+  const float* add[3];
+  int64_t addgs[3];
+  int ldadd[3];
+  int nadd;
   // LDS-staged kernels (cfg >= CONV_LDS_CFG0, conv_lds.hip) with a cross-block split of K: fp32 partial
   // tiles [G][tiles][splits][BM*BN] and one arrival ticket per output tile (zero-initialised; the reducing
   // block resets it), sized by conv_lds_workspace
   float* ws;
   unsigned* cnt;
 };
+
+// ConvArgs::add: the extra gradient sources of output element (row m, channels n0 .. n0+3), added in order
+DEV void add_sources(const ConvArgs& a, int z, int64_t m, int n0, float* v) {
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    if (s < a.nadd) {
+      const float4 q = *reinterpret_cast<const float4*>(a.add[s] + a.addgs[s] * z + m * a.ldadd[s] + n0);
+      v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+    }
+  }
+}
 
 // One output-pixel phase of an LDS-staged conv launch (conv_lds.hip): output pixels (b, oy0 + i*qy,
 // ox0 + j*qx) for i < Hq, j < Wq, reduced over taps (kh, kw) = (rh + th*u, rw + tw*v), u < nh, v < nw,
@@ -229,6 +247,10 @@ constexpr int CONV_GLDS_CFG0 = 160, CONV_GLDS_NCFG = 32;
 // patch conv for 3x3 / stride-1 layers (conv_lds.hip conv_patch_kernel): cfg = CONV_PATCH_CFG0 + 3 * tile + cb
 // (tile: BM x BN of PT_BM / PT_BN, cb: channel slice 16 / 32 / 64)
 constexpr int CONV_PATCH_CFG0 = 192, CONV_PATCH_NCFG = 15;
+// deep-ring LDS-DMA configs (conv_glds_kernel with up to 8 stages): cfg = CONV_GDEEP_CFG0 + 4 * tile + log2(splits)
+constexpr int CONV_GDEEP_CFG0 = 208, CONV_GDEEP_NCFG = 32;
+// persistent, DMA-pipelined patch conv (one channel slice): cfg = CONV_PATCHP_CFG0 + 3 * tile + cb
+constexpr int CONV_PATCHP_CFG0 = 240, CONV_PATCHP_NCFG = 15;
 int launch_conv_lds(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 // fp32 workspace floats and ticket count a cfg needs (0 when it does not split K); < 0: cfg invalid for a
 int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_floats, int64_t& ntickets);

@@ -406,8 +406,12 @@ class ConvLayer:
         return self.Kpad_w % WGRAD_TILES[cfg][1] == 0
 
     def wgrad_plan(self, cfg: int):
-        if cfg in WGRAD_PATCH:  # splits sized for ~128 blocks per job (32 / 64 / 256 measured slower)
-            return patch_plan(cfg, self.B, self.Ho, self.Npad, self.Cs, self.G, 128)
+        if cfg in WGRAD_PATCH:
+            # splits sized for ~128 blocks per job on Model A's layers (32 / 64 / 256 measured slower there);
+            # the wide-row configs (128-pixel rows: Model C's 47x122 / 21x58 stem layers) fill the GPU with
+            # ~512 blocks (tools/wgrad_cfg_sweep.py: 47x122 32->64 29 us at 512 blocks vs 53 us at 128)
+            wide = WGRAD_PATCH[cfg][2] >= 128
+            return patch_plan(cfg, self.B, self.Ho, self.Npad, self.Cs, self.G, 512 if wide else 128)
         TN, TK, MCH = WGRAD_TILES[cfg]
         tiles = math.ceil(self.Npad / TN) * (self.Kpad_w // TK) * self.G
         # whole-reduction tiles (TK >= 128) have one tile per channel block: shorter per-block pixel

@@ -203,6 +203,51 @@ class LoweredProgram:
         ph.add("conv_wgrad", k_wgrad, cfg, G, d, owner=c)
         self._last_wgrad = len(ph.launches) - 1
 
+    # Fold the gradient sources of multi-source BN tails into the last producing dgrad (fold_tail_sources);
+    # programs whose tails join streams (Inception's concat consumers) keep it off: the fold moves the
+    # tail's cross-stream waits onto that dgrad, which would serialise the branches
+    FOLD_SOURCES = False
+
+    def fold_tail_sources(self) -> int:
+        """A BN tail backward with 2-4 fp32 gradient sources, the last of them written by a data gradient on
+        the tail's own stream: that dgrad's epilogue adds the other sources (csrc ConvArgs::add), its output
+        becomes the tail's only source, and the tail's waits (the other sources' events) move onto the dgrad.
+        The tail then qualifies for fuse_dgrad_bn_stats -- the statistics come from the dgrad epilogue and
+        the tail runs apply-only: Model A's residual-block ADD_RELU tails lose their reduce pass and their
+        re-reads of four fp32 sources.  Returns the number of folded tails."""
+        import os
+        self.n_folded = 0
+        if not self.FOLD_SOURCES or os.environ.get("MDA_FOLD", "1") != "1":
+            return 0
+        ls = self.bwd.launches
+        last_dgrad = {}  # stream -> (index, launch) of its latest dgrad
+        for i, l in enumerate(ls):
+            if l.name == "conv_dgrad":
+                last_dgrad[l.stream] = (i, l)
+                continue
+            if not l.name.startswith("tailbwd"):
+                continue
+            kind, G, nchunk, d = l.args
+            g = d["g"]
+            if kind not in (ACT_NONE, ACT_RELU, ADD_RELU) or not 2 <= len(g) <= 4 or l.stream not in last_dgrad:
+                continue
+            j, D = last_dgrad[l.stream]
+            if any(k.stream == l.stream and k.name not in ("conv_wgrad",) for k in ls[j + 1:i]):
+                continue  # something else runs between the dgrad and the tail
+            mode, cfg, PG, pd = D.args
+            mine = [q for q, (p, gs, ld) in enumerate(g) if p == pd["out"] and gs == pd["ogs"] and ld == pd["ldo"]]
+            if (len(mine) != 1 or PG != G or pd.get("add") or pd["N"] != d["C"]
+                    or (pd["Ho"], pd["Wo"]) != (d["H"], d["W"]) or pd["B"] != d["B"]):
+                continue
+            pd["add"] = [{"p": p, "gs": gs, "ld": ld} for q, (p, gs, ld) in enumerate(g) if q != mine[0]]
+            d["g"] = [g[mine[0]]]
+            for k in ("dzbuf", "dzgs", "lddz"):
+                d.pop(k, None)
+            D.waits = tuple(D.waits) + tuple(l.waits)
+            l.waits = ()
+            self.n_folded += 1
+        return self.n_folded
+
     def fuse_dgrad_bn_stats(self) -> int:
         """Move the BN-backward reduction of single-source elementwise tails into the producing dgrad.
 
@@ -220,7 +265,7 @@ class LoweredProgram:
                 producers[l.args[3]["out"]] = l
             elif l.name.startswith("tailbwd"):
                 kind, G, nchunk, d = l.args
-                if kind not in (ACT_NONE, ACT_RELU, ACT_SIGMOID) or len(d["g"]) != 1 or d.get("dzbuf"):
+                if kind not in (ACT_NONE, ACT_RELU, ACT_SIGMOID, ADD_RELU) or len(d["g"]) != 1 or d.get("dzbuf"):
                     continue
                 gp, ggs, gld = d["g"][0]
                 prod = producers.get(gp)
@@ -232,6 +277,10 @@ class LoweredProgram:
                     continue
                 pd["bnb"] = {"y": d["y"], "ygs": d["ygs"], "ldy": d["ldy"], "bn": d["bn"], "part": d["part"],
                              "kind": kind}
+                if kind == ADD_RELU:  # the residual (and its BN for a projection shortcut) enters the dz mask
+                    pd["bnb"].update({"r": d["r"], "rgs": d["rgs"], "ldr": d["ldr"]})
+                    if "bn2" in d:
+                        pd["bnb"]["bn2"] = d["bn2"]
                 d["fused"] = 2
                 self.n_dgrad_bnstats += 1
         return self.n_dgrad_bnstats

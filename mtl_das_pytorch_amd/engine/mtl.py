@@ -82,6 +82,8 @@ class MTLProgram(LoweredProgram):
         self._emit()
 
     # -------------------------------------------------------------------------------------------
+    FOLD_SOURCES = True  # the residual-block tails' sources are summed by the last dgrad (fold_tail_sources)
+
     def _alloc(self):
         m, A, B, T, f = self.model, self.arena, self.B, self.T, self.flat
         self.x = A.zeros((B, self.H0, self.W0, 8))
@@ -174,6 +176,7 @@ class MTLProgram(LoweredProgram):
         self.fwd_train = self._emit_forward(True)
         self.fwd_eval = self._emit_forward(False)
         self.bwd = self._emit_backward()
+        self.fold_tail_sources()
         self.fuse_dgrad_bn_stats()
         self.opt = self._emit_optimizer()
 

@@ -16,17 +16,19 @@ from typing import Dict, Iterable, Optional
 import torch
 
 from ..ops.functional import (CONV_DEEP_CFG0, CONV_DEEP_NCFG, CONV_GLDS_CFG0, CONV_GLDS_NCFG, CONV_LDS_CFG0,
-                              CONV_LDS_NCFG, CONV_PATCH_CFG0, CONV_PATCH_NCFG, WGRAD_PATCH, WGRAD_TILES,
-                              conv_workspace)
+                              CONV_LDS_NCFG, CONV_PATCH_CFG0, CONV_PATCH_NCFG, CONV_PATCHP_CFG0, CONV_PATCHP_NCFG,
+                              GDEEP_TILES, WGRAD_PATCH, WGRAD_TILES, conv_workspace, glds_cfg)
 from ..ops.hip import lib
 
 # conv.hip register-pipelined tiles 0-13 (pipeline depth 2, and 4 at CONV_DEEP_CFG0 + tile), then
-# conv_lds.hip LDS-staged tiles x K chunk x K split, its LDS-DMA tiles x K split and the 3x3 / stride-1
-# patch tiles x channel slice
+# conv_lds.hip LDS-staged tiles x K chunk x K split, its LDS-DMA tiles x K split, the 3x3 / stride-1
+# patch tiles x channel slice (one strip per block, and persistent), the deep-ring LDS-DMA tiles x K split
 CONV_CFGS = (list(range(14)) + list(range(CONV_LDS_CFG0, CONV_LDS_CFG0 + CONV_LDS_NCFG))
              + list(range(CONV_DEEP_CFG0, CONV_DEEP_CFG0 + CONV_DEEP_NCFG))
              + list(range(CONV_GLDS_CFG0, CONV_GLDS_CFG0 + CONV_GLDS_NCFG))
-             + list(range(CONV_PATCH_CFG0, CONV_PATCH_CFG0 + CONV_PATCH_NCFG)))
+             + list(range(CONV_PATCH_CFG0, CONV_PATCH_CFG0 + CONV_PATCH_NCFG))
+             + [glds_cfg(t, s, deep=True) for t in GDEEP_TILES for s in (1, 2, 4, 8)]
+             + list(range(CONV_PATCHP_CFG0, CONV_PATCHP_CFG0 + CONV_PATCHP_NCFG)))
 
 
 def fused_max_m(kind: int) -> int:

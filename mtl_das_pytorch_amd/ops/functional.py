@@ -79,6 +79,9 @@ GLDS_TILES = [(64, 64), (128, 64), (64, 128), (128, 128), (256, 64), (128, 32), 
 CONV_PATCH_CFG0, CONV_PATCH_NCFG = 192, 15  # 3x3 / stride-1 patch conv configs (conv_lds.hip conv_patch_kernel)
 PATCH_TILES = [(256, 16), (256, 32), (256, 64), (128, 32), (128, 64)]  # strip capacity (pixels) x BN channels
 PATCH_CB = [16, 32, 64]  # channel slice staged per pass
+CONV_GDEEP_CFG0, CONV_GDEEP_NCFG = 208, 32  # LDS-DMA configs with a deep ring (up to 8 K chunks in flight)
+CONV_PATCHP_CFG0, CONV_PATCHP_NCFG = 240, 15  # persistent, DMA-pipelined patch conv (one channel slice)
+GDEEP_TILES = [0, 1, 2, 3, 5, 7]  # GLDS_TILES entries that have a deep ring (conv_lds.hip GL_NST_DEEP)
 
 
 def lds_cfg(tile: int, kc: int = 64, splits: int = 1) -> int:
@@ -87,16 +90,17 @@ def lds_cfg(tile: int, kc: int = 64, splits: int = 1) -> int:
     return CONV_LDS_CFG0 + 8 * tile + 4 * (kc == 128) + {1: 0, 2: 1, 4: 2, 8: 3}[splits]
 
 
-def glds_cfg(tile: int, splits: int = 1) -> int:
+def glds_cfg(tile: int, splits: int = 1, deep: bool = False) -> int:
     """Config id of the LDS-DMA conv kernel: tile index into GLDS_TILES (BM pixels x BN channels, K chunk 64,
-    3-stage ring), cross-block split of K into 1 / 2 / 4 / 8."""
-    return CONV_GLDS_CFG0 + 4 * tile + {1: 0, 2: 1, 4: 2, 8: 3}[splits]
+    3-stage ring, or with ``deep`` the tile's deepest ring), cross-block split of K into 1 / 2 / 4 / 8."""
+    return (CONV_GDEEP_CFG0 if deep else CONV_GLDS_CFG0) + 4 * tile + {1: 0, 2: 1, 4: 2, 8: 3}[splits]
 
 
-def patch_cfg(tile: int, cb: int) -> int:
+def patch_cfg(tile: int, cb: int, persistent: bool = False) -> int:
     """Config id of the patch conv kernel: tile index into PATCH_TILES (a block owns R = BM // Wout whole
-    output rows x BN channels), channel slice cb (16 / 32 / 64; Cs must be a multiple)."""
-    return CONV_PATCH_CFG0 + 3 * tile + PATCH_CB.index(cb)
+    output rows x BN channels), channel slice cb (16 / 32 / 64; Cs must be a multiple).  ``persistent``: the
+    block loops over strips with the next one in flight by LDS-DMA (Cs == cb, no normalise-on-load)."""
+    return (CONV_PATCHP_CFG0 if persistent else CONV_PATCH_CFG0) + 3 * tile + PATCH_CB.index(cb)
 
 
 def conv_workspace(mode: int, cfg: int, G: int, d: dict, device) -> Optional[tuple]:

@@ -62,6 +62,10 @@ def local_syncbn_check(prog, world):
                 g = g + (nchw(L["dcat"], t, 0, L["C"]) if k % 2 == 1 else nchw(L["dF"], t))
         if k < 8:
             R = rbs[k]
+            for key in ("dxs", "dxa"):  # a dgrad that summed every source of F_k (fold_tail_sources)
+                if key in R and any(l.name == "conv_dgrad" and l.args[3].get("add") and l.args[3]["out"] == R[key].p
+                                    for l in prog.bwd.launches):
+                    return nchw(R[key])
             g = g + nchw(R["dxa"]) + (nchw(R["dxs"]) if R["proj"] else nchw(R["side"]))
         return g
 

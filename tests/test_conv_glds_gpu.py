@@ -1,6 +1,6 @@
 """The LDS-DMA implicit-GEMM conv kernel (csrc/conv_lds.hip conv_glds_kernel: global_load_lds_dwordx4 into a
-swizzled 3-stage LDS ring, counted vmcnt + raw barrier) against fp32 PyTorch: every tile config x cross-block
-K split, forward (+bias, +fused BN sums), data gradient (stride 1 and the stride-2 sub-pixel phases) and the
+swizzled 3-stage LDS ring, or a deep ring of up to 8 stages, counted vmcnt + raw barrier) against fp32
+PyTorch: every tile config (both rings) x cross-block K split, forward (+bias, +fused BN sums), data gradient (stride 1 and the stride-2 sub-pixel phases) and the
 fused BN-backward statistics epilogue, on the Model A / Model C layer classes of tests/test_conv_lds_gpu.py
 plus the stem geometries this kernel is meant for."""
 import pytest
@@ -18,14 +18,17 @@ GCASES = CASES + [
 ]
 
 
-@pytest.mark.parametrize("tile", range(8))
-def test_glds_forward_all_configs(tile):
+RINGS = [(t, False) for t in range(8)] + [(t, True) for t in (0, 1, 2, 3, 5, 7)]  # (tile, deep ring)
+
+
+@pytest.mark.parametrize("tile,deep", RINGS)
+def test_glds_forward_all_configs(tile, deep):
     from mtl_das_pytorch_amd.ops import functional as fn
     for ci, case in enumerate(GCASES):
         x, w, b, s, p = _mk(case, ci)
         ref = F.conv2d(x, w, b, stride=s, padding=p)
         for splits in (1, 2, 8):
-            cfg = fn.glds_cfg(tile, splits)
+            cfg = fn.glds_cfg(tile, splits, deep)
             stats = torch.zeros(NREP, 2, w.shape[0], device="cuda", dtype=torch.float64)
             y = fn.conv2d(nhwc(x).bfloat16(), w, b, stride=s, padding=p, stats=stats, cfg=cfg)
             assert rel(nchw(y), ref) < 6e-3, (case, cfg)
@@ -34,8 +37,8 @@ def test_glds_forward_all_configs(tile):
             assert rel(st[1], (ref * ref).sum((0, 2, 3))) < 1e-3, (case, cfg)
 
 
-@pytest.mark.parametrize("tile", range(8))
-def test_glds_dgrad_all_configs(tile):
+@pytest.mark.parametrize("tile,deep", RINGS)
+def test_glds_dgrad_all_configs(tile, deep):
     from mtl_das_pytorch_amd.ops import functional as fn
     for ci, case in enumerate(GCASES):
         x, w, b, s, p = _mk(case, 100 + ci)
@@ -44,7 +47,7 @@ def test_glds_dgrad_all_configs(tile):
         dy = torch.randn_like(out).bfloat16().float()
         out.backward(dy)
         for splits in (1, 4):
-            cfg = fn.glds_cfg(tile, splits)
+            cfg = fn.glds_cfg(tile, splits, deep)
             dx = fn.conv2d_dgrad(nhwc(dy).bfloat16(), w, x.shape[2:], stride=s, padding=p, cfg=cfg)
             assert rel(nchw(dx), xr.grad) < 5e-3, (case, cfg)
 
@@ -67,10 +70,10 @@ def test_glds_dgrad_fused_bn_stats(kind):
     yb = nhwc(y).bfloat16()
     w = (torch.randn(Co, C, 3, 3, generator=g) / 17).bfloat16().float().cuda()
     go = torch.randn(B, H, W, Co, generator=g).bfloat16().cuda()
-    for tile in range(8):
+    for tile, deep in RINGS:
         for splits in (1, 2):
             part = torch.zeros(NREP, 3, C, device="cuda", dtype=torch.float64)
-            cfg = fn.glds_cfg(tile, splits)
+            cfg = fn.glds_cfg(tile, splits, deep)
             dx = fn.conv2d_dgrad(go, w, (H, W), stride=1, padding=1, cfg=cfg, bn_stats=(yb, bn, part, kind))
             dx_ref = fn.conv2d_dgrad(go, w, (H, W), stride=1, padding=1)
             assert rel(dx, dx_ref) < 1e-5, (tile, splits)

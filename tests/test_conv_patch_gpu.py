@@ -25,9 +25,10 @@ PCASES = [
 ]
 
 
-def _cfgs():
+def _cfgs():  # both forms: one strip per block, and persistent (DMA-pipelined strips, Cs == cb only)
     from mtl_das_pytorch_amd.ops import functional as fn
-    return [fn.patch_cfg(t, cb) for t in range(len(fn.PATCH_TILES)) for cb in fn.PATCH_CB]
+    return [fn.patch_cfg(t, cb, pers) for pers in (False, True) for t in range(len(fn.PATCH_TILES))
+            for cb in fn.PATCH_CB]
 
 
 def _mk(case, seed):
@@ -57,7 +58,21 @@ def test_patch_forward_all_configs():
             st = stats.sum(0)
             assert rel(st[0], ref.sum((0, 2, 3))) < 1e-3, (case, cfg)
             assert rel(st[1], (ref * ref).sum((0, 2, 3))) < 1e-3, (case, cfg)
-    assert ran >= 40
+    assert ran >= 50
+
+
+def test_patch_persistent_matches_strip_form():
+    """The persistent form (strips looped per block, DMA-prefetched, statistics summed in registers over a
+    block's strips) gives the same output as the one-strip-per-block form up to the fp32 order of the BN sums."""
+    from mtl_das_pytorch_amd.ops import functional as fn
+    x, w, b, p = _mk((3, 47, 122, 32, 64, 1), 9)
+    outs = []
+    for pers in (False, True):
+        stats = torch.zeros(NREP, 2, 64, device="cuda", dtype=torch.float64)
+        y = fn.conv2d(nhwc(x).bfloat16(), w, b, padding=p, stats=stats, cfg=fn.patch_cfg(1, 32, pers))
+        outs.append((y, stats.sum(0)))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert rel(outs[0][1], outs[1][1]) < 1e-6
 
 
 def test_patch_dgrad_all_configs():
@@ -107,10 +122,11 @@ def test_patch_normalise_on_load(kind):
         assert ran >= 3, case
 
 
+@pytest.mark.parametrize("Co", [48, 32])
 @pytest.mark.parametrize("kind", [0, 1, 2])
-def test_patch_dgrad_fused_bn_stats(kind):
+def test_patch_dgrad_fused_bn_stats(kind, Co):
     from mtl_das_pytorch_amd.ops import functional as fn
-    B, H, W, C, Co = 2, 17, 42, 32, 48
+    B, H, W, C = 2, 17, 42, 32
     g = torch.Generator().manual_seed(7 + kind)
     y = (torch.randn(B, C, H, W, generator=g) * 1.5 + 0.2).bfloat16().float().cuda()
     st = torch.zeros(NREP, 2, C, device="cuda", dtype=torch.float64)
@@ -138,7 +154,7 @@ def test_patch_dgrad_fused_bn_stats(kind):
         assert rel(dx, dx_ref) < 1e-5, cfg
         got = part.sum(0)
         assert rel(got[0], db.double()) < 1e-4 and rel(got[1], dg.double()) < 1e-4, cfg
-    assert ran >= 5  # Cs = 48: the 16-channel slice of every tile
+    assert ran >= (5 if Co == 48 else 15)  # dy channels 48: 16-channel slices only; 32: persistent forms too
 
 
 def test_patch_two_segment_input():

@@ -18,9 +18,14 @@ def test_mtl_program_structure():
     n = p.num_launches()
     # forward: 12 BN+ReLU tails are folded into their consumer conv (normalise-on-load)
     assert n["forward_train"] == 48 and n["backward"] == 90
-    # the residual tails have 2-4 gradient sources: reduce + apply (or single launch) over their sum
+    # the residual tails have 2-4 gradient sources: the last producing dgrad sums them (fold_tail_sources)
+    # and fuses the tail's statistics, so 7 of 8 run apply-only; RB8's tail has no dgrad before it
     tails = [l for l in p.bwd.launches if l.name == "tailbwd4"]
-    assert len(tails) == 8 and all(l.args[3].get("fused", 0) != 2 for l in tails)
+    assert len(tails) == 8 and p.n_folded == 8
+    assert [l.args[3].get("fused", 0) == 2 for l in tails] == [False] + [True] * 7
+    assert all(len(l.args[3]["g"]) == 1 and not l.waits for l in tails[1:])
+    folded = [l for l in p.bwd.launches if l.name == "conv_dgrad" and l.args[3].get("add")]
+    assert len(folded) == 8 and all(1 <= len(l.args[3]["add"]) <= 3 for l in folded)
     # both task branches of a level are ONE grouped launch with an even parameter stride
     L = p.levels[1]
     assert L["c0"].G == 2 and L["c0"].wstride > 0
@@ -91,15 +96,18 @@ def test_wgrad_batching_structure():
 
 
 def test_dgrad_fused_bn_stats_wiring():
-    """Single-source elementwise BN tails take their backward sums from the producing dgrad's epilogue
-    (Model A: 8 residual-block inner BNs + 4 grouped attention-generator BNs)."""
+    """Single-source BN tails take their backward sums from the producing dgrad's epilogue (Model A: 8
+    residual-block inner BNs + 4 grouped attention-generator BNs, and -- their sources folded into the last
+    dgrad -- 7 residual ADD_RELU tails and conv1's tail)."""
     from mtl_das_pytorch_amd.engine.inception import InceptionProgram
     from mtl_das_pytorch_amd.models import Multi_Classifier
     p = MTLProgram(MTL_Net(), 8, "cpu")
-    assert p.n_dgrad_bnstats == 12
+    assert p.n_dgrad_bnstats == 20
     fused = [l for l in p.bwd.launches if l.name.startswith("tailbwd") and l.args[3].get("fused") == 2]
     bnb = [l for l in p.bwd.launches if l.name == "conv_dgrad" and "bnb" in l.args[3]]
-    assert len(fused) == len(bnb) == 12
+    assert len(fused) == len(bnb) == 20
+    res = [x for x in bnb if x.args[3]["bnb"]["kind"] == 4]  # ADD_RELU: residual (+ its BN) in the mask
+    assert len(res) == 7 and sum("bn2" in x.args[3]["bnb"] for x in res) == 3
     for l in fused:
         kind, G, nchunk, d = l.args
         prod = [x for x in bnb if x.args[3]["out"] == d["g"][0][0]]

@@ -107,8 +107,9 @@ class Checker:
         assert not self.bad, self.bad
 
 
-def conv_check(chk, name, conv, z, x, dy, dx_act=None, x_requires=True):
-    """Autograd of the single conv (bf16-rounded weights, the engine's input and dy)."""
+def conv_check(chk, name, conv, z, x, dy, dx_act=None, x_requires=True, dx_extra=None):
+    """Autograd of the single conv (bf16-rounded weights, the engine's input and dy).  ``dx_extra``: the
+    gradient sources the engine's dgrad epilogue added to its output (fold_tail_sources)."""
     m = conv.mods[z]
     x = x.clone().requires_grad_(x_requires and dx_act is not None)
     w = q(m.weight.detach()).requires_grad_(True)
@@ -121,7 +122,7 @@ def conv_check(chk, name, conv, z, x, dy, dx_act=None, x_requires=True):
         db = dy.sum((0, 2, 3))
         chk.exact_zero(f"{name}.bias", m.bias.grad, db.norm().item() / dy.abs().sum((0, 2, 3)).norm().item())
     if dx_act is not None:
-        chk("dx", f"{name} dx", dx_act, x.grad)
+        chk("dx", f"{name} dx", dx_act, x.grad if dx_extra is None else x.grad + dx_extra)
 
 
 def bn_grads_check(chk, name, bn, z, dgam, dbet):
@@ -134,16 +135,35 @@ def test_mtl_backward_layer_local(engine_step):
     chk = Checker()
     T, lv, rbs = prog.T, prog.levels, prog.rbs
 
-    def sources(k):  # gradient sources of F_k (mirrors MTLProgram._emit_backward)
+    def folded(R):  # which data gradient of block R summed all gradient sources of its input (or None)
+        for key in ("dxs", "dxa"):
+            if key in R and any(l.name == "conv_dgrad" and l.args[3].get("add") and l.args[3]["out"] == R[key].p
+                                for l in prog.bwd.launches):
+                return key
+        return None
+
+    def level_sources(k):
         g = 0
         if k >= 1:
             L = lv[(k - 1) // 2]
             for t in range(T):
                 g = g + (nchw(L["dcat"], t, 0, L["C"]) if k % 2 == 1 else nchw(L["dF"], t))
+        return g
+
+    def sources(k):  # gradient sources of F_k (mirrors MTLProgram._emit_backward)
+        g = level_sources(k)
         if k < 8:
             R = rbs[k]
+            if folded(R):
+                return nchw(R[folded(R)])
             g = g + nchw(R["dxa"]) + (nchw(R["dxs"]) if R["proj"] else nchw(R["side"]))
         return g
+
+    def folded_extra(i, key):  # what the folded dgrad of block i (consuming F_i) added to its own output
+        R = rbs[i]
+        if folded(R) != key:
+            return None
+        return level_sources(i) + (nchw(R["dxa"]) if key == "dxs" else nchw(R["side"]))
 
     # ---- task levels (per task t, group z = t)
     for li in range(3, -1, -1):
@@ -209,9 +229,11 @@ def test_mtl_backward_layer_local(engine_step):
         dya, dgam, dbet = bn_backward(nchw(R["dha"]) * ((ya * sca + sha) > 0), ya, R["bna"])
         chk("dy", f"{nm} inner tail dy", nchw(R["dya"]), dya)
         bn_grads_check(chk, f"{nm}.left.1", R["bna"], 0, dgam, dbet)
-        conv_check(chk, f"{nm}.left.0", R["ca"], 0, nchw(R["in"]), nchw(R["dya"]), nchw(R["dxa"]))
+        conv_check(chk, f"{nm}.left.0", R["ca"], 0, nchw(R["in"]), nchw(R["dya"]), nchw(R["dxa"]),
+                   dx_extra=folded_extra(i, "dxa"))
         if R["proj"]:
-            conv_check(chk, f"{nm}.shortcut.0", R["cs"], 0, nchw(R["in"]), nchw(R["dys"]), nchw(R["dxs"]))
+            conv_check(chk, f"{nm}.shortcut.0", R["cs"], 0, nchw(R["in"]), nchw(R["dys"]), nchw(R["dxs"]),
+                       dx_extra=folded_extra(i, "dxs"))
 
     # ---- stem: conv1 tail (sources of f0) and the conv1 weight gradient on the real (unpacked) input
     y0 = nchw(prog.y0)

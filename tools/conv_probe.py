@@ -27,7 +27,9 @@ def main():
     ap.add_argument("--pw", type=int, default=None)
     ap.add_argument("--dgrad", action="store_true")
     ap.add_argument("--top", type=int, default=12)
+    ap.add_argument("--cfgs", default="", help="comma-separated configs to run (default: every tuner config)")
     a = ap.parse_args()
+    cfgs = [int(c) for c in a.cfgs.split(",")] if a.cfgs else CONV_CFGS
     pad = (a.p, a.p if a.pw is None else a.pw)
     dev = "cuda"
     g = torch.Generator().manual_seed(0)
@@ -45,7 +47,7 @@ def main():
     yb = torch.randn(a.B, a.H, a.W, a.Ci, generator=g).bfloat16().to(dev)
     part = torch.zeros(NREP, 3, a.Ci, device=dev, dtype=torch.float64)
     res = []
-    for c in CONV_CFGS:
+    for c in cfgs:
         row = [c]
         variants = ([{}, {"bn_stats": (yb, bn, part, 1)}] if a.dgrad else
                     [{}, {"stats": stats}, {"stats": stats, "nol": (bn, 1)},
