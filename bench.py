@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--no-tune", action="store_true", help="skip per-layer kernel autotuning (cached table only)")
     ap.add_argument("--in_channels", type=int, default=1,
                     help="input channels of the synthetic DAS matrices (reference 1; BASELINE north star 2)")
+    ap.add_argument("--sync_bn", action="store_true",
+                    help="SyncBN: BN statistics all-reduced inside the step (one GPU: run with MDA_DIST_BACKEND=nccl "
+                         "for a 1-rank RCCL group, so the collectives execute)")
     args = ap.parse_args()
 
     import torch
@@ -81,7 +84,12 @@ def main():
     torch.manual_seed(1234)  # identical init on every rank (then broadcast for certainty)
     model = build_model(args.model, in_channels=args.in_channels)
     joint = args.model == "multi_classifier"
-    prog = InceptionProgram(model, args.batch, dev) if joint else MTLProgram(model, args.batch, dev)
+    sync = args.sync_bn and ctx.enabled
+    sw = world if sync else 1
+    prog = (InceptionProgram(model, args.batch, dev, sync_world=sw) if joint
+            else MTLProgram(model, args.batch, dev, sync_world=sw))
+    if sync:  # the statistics collectives are captured into the step's HIP graph (RCCL)
+        prog.enable_sync_bn(ctx.all_reduce_ordered_)
     prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world)
     if hasattr(prog, "set_rng_stream"):  # Model C dropout: an independent mask stream per rank
         prog.set_rng_stream(0, ctx.rank)
@@ -95,7 +103,7 @@ def main():
     broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
     X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev, in_channels=args.in_channels)
     labels = encode_joint(d, e) if joint else torch.stack([d, e], 1)
-    runner = StepRunner(prog, X, labels, use_graph=not args.no_graph,
+    runner = StepRunner(prog, X, labels, use_graph=not args.no_graph and (not sync or ctx.capturable_collectives),
                         allreduce=FlatGradAllReducer(ctx) if (ctx.enabled or len(buckets) > 1) else None)
     runner.set_lr(1e-3 / 1.5)  # reference: lr/1.5 applied at the epoch-0 validation
     sampler = ShardedIndexSampler(args.dataset_size * world, args.batch, ctx, seed=7)
@@ -157,7 +165,8 @@ def main():
         "train_steps_before_heldout": args.warmup + args.steps,
         "vs_eager_pytorch_mi355x": (round(value / (EAGER_BY_MODEL[args.model] * world), 3)
                                     if args.model in EAGER_BY_MODEL else None),
-        "hip_graph": not args.no_graph,
+        "hip_graph": runner.use_graph,
+        "sync_bn": sync,
         "grad_buckets_mb": [round((hi - lo) * 4 / 2 ** 20, 2) for lo, hi in buckets],
         "dist_backend": ctx.backend,
         "rccl_ranks": dist.get_world_size() if ctx.backend == "nccl" else 0,

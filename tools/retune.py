@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--in-context", action="store_true")
     ap.add_argument("--topk", type=int, default=3)
+    ap.add_argument("--margin", type=float, default=0.002, help="in-context: relative step-time gain to keep a config")
+    ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--drop", default="", help="with --keep: comma-separated key prefixes to re-measure (e.g. wgrad)")
     args = ap.parse_args()
     cache = load_cache() if args.keep else {}
@@ -51,7 +53,7 @@ def main():
             autotune_program(prog, cache=cache, measure=False)  # batch the weight gradients as the bench does
             X, d, e = generate(4 * args.batch, seed=3, device="cuda")
             labels = encode_joint(d, e) if name == "multi_classifier" else torch.stack([d, e], 1)
-            tune_in_context(prog, X, labels, cache, topk=args.topk)
+            tune_in_context(prog, X, labels, cache, topk=args.topk, margin=args.margin, reps=args.reps)
             print(f"{name}: in-context refinement done at {time.time() - t0:.1f} s", flush=True)
         del prog, m
         torch.cuda.empty_cache()
