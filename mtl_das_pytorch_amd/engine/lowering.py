@@ -131,10 +131,8 @@ class LoweredProgram:
             new.append(l)
             bn = by_stats.get(l.args[3].get("stats") or 0) if l.name == "conv_fwd" else None
             if bn is not None:
-                ar = Launch("allreduce_bn", k_allreduce, allreduce, bn.stats, stream=l.stream, record=l.record,
-                            bucket=l.bucket)
+                new += self._collective(allreduce, bn.stats, l.stream, l.bucket, l.record)
                 l.record = None
-                new.append(ar)
                 n += 1
         self.fwd_train.launches = new
         new = []
@@ -154,10 +152,13 @@ class LoweredProgram:
                                                                 "dy2", "d2gs", "ldd2", "pgs")}
                 red["fused"] = 3
                 l.name, l.args = f"tailpart{kind}", (kind, G, nchunk, red)
-                new += [l, Launch("allreduce_bn", k_allreduce, allreduce, bn.part, stream=l.stream, bucket=l.bucket)]
-            else:  # statistics from the producing dgrad's epilogue: all-reduce them, then apply
+                new += [l] + self._collective(allreduce, bn.part, l.stream, l.bucket)
+            elif l.stream < self.COLLECTIVE_STREAMS:  # statistics from the producing dgrad's epilogue
                 l.name, l.fn, l.args = "allreduce_bn", k_allreduce, (allreduce, bn.part)
                 new.append(l)
+            else:  # (the launch keeps its waits as a kernel-free fork point in front of the collective)
+                l.name, l.fn, l.args = f"fork:{l.name}", None, ()
+                new += [l] + self._collective(allreduce, bn.part, l.stream, l.bucket)
             d = {k: v for k, v in d.items() if k not in ("dzbuf", "dzgs", "lddz")}
             d["fused"], d["gscale"] = 2, 1.0 / world
             new.append(Launch(name, k_tail_bwd, kind, G, nchunk, d, owner=l.owner, stream=l.stream, record=record,
@@ -166,6 +167,23 @@ class LoweredProgram:
         self.bwd.launches = new
         self.sync_bn_world = world
         return n
+
+    # Collectives captured into the step graph from at most these streams (0 and 1: Model A's backbone and
+    # level branches); a collective of a BN on a later stream (Model C's Inception branches) runs on stream 0
+    # between a record / wait pair of events -- issued from four capturing streams, RCCL's internal stream
+    # invalidated the HIP graph capture (hipErrorStreamCaptureInvalidated at bench.py --sync_bn, Model C)
+    COLLECTIVE_STREAMS = 2
+
+    def _collective(self, allreduce, t, stream: int, bucket, record=None) -> List[Launch]:
+        """All-reduce launch(es) of ``t`` ordered after ``stream``'s previous launches and before its next ones;
+        ``record``: the event the last of them records (the tag the replaced launch carried)."""
+        if stream < self.COLLECTIVE_STREAMS:
+            return [Launch("allreduce_bn", k_allreduce, allreduce, t, stream=stream, record=record, bucket=bucket)]
+        self._n_routed = getattr(self, "_n_routed", 0) + 1
+        tp, ta = f"sbn_p{self._n_routed}", f"sbn_a{self._n_routed}"
+        return [Launch(f"fork:{tp}", None, stream=stream, record=tp, bucket=bucket),
+                Launch("allreduce_bn", k_allreduce, allreduce, t, stream=0, waits=(tp,), record=ta, bucket=bucket),
+                Launch(f"fork:{ta}", None, stream=stream, waits=(ta,), record=record, bucket=bucket)]
 
     @staticmethod
     def nol_enabled() -> bool:

@@ -114,7 +114,10 @@ class StepRunner:
             snap.restore()
             self.p.opt["pack"].run()  # the bf16 weight images are derived state: rebuild from restored masters
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread-local capture: RCCL's process-group watchdog thread queries the events of earlier
+            # (eager warm-up) collectives while this thread captures; under the default global mode that
+            # query fails with hipErrorStreamCaptureUnsupported and the watchdog aborts the process
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 for f in fns:
                     f()
             torch.cuda.synchronize()
