@@ -120,7 +120,8 @@ class LoweredProgram:
             sums (torch.nn.SyncBatchNorm); the apply writes d(gamma), d(beta) scaled by 1/world, so after
             the data-parallel gradient average they equal torch's mean of the per-rank local sums.
         Single-launch BN backwards (fused = 1) cannot be split and are replaced by reduce + apply.
-        The collectives run between kernels, so the step runs eagerly (no HIP graph).  Returns the number
+        On RCCL the collectives are captured into the step's HIP graph (stream-ordered; those of BNs on
+        streams >= COLLECTIVE_STREAMS go through stream 0); gloo runs the step eagerly.  Returns the number
         of all-reduces inserted per training step."""
         world = self.flat.bn_world
         by_stats = {P(bn.stats): bn for bn in self.flat.bn_layers}

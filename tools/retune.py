@@ -53,7 +53,8 @@ def main():
             autotune_program(prog, cache=cache, measure=False)  # batch the weight gradients as the bench does
             X, d, e = generate(4 * args.batch, seed=3, device="cuda")
             labels = encode_joint(d, e) if name == "multi_classifier" else torch.stack([d, e], 1)
-            tune_in_context(prog, X, labels, cache, topk=args.topk, margin=args.margin, reps=args.reps)
+            tune_in_context(prog, X, labels, cache, topk=args.topk, margin=args.margin, reps=args.reps,
+                            on_change=lambda c: save_cache(c, args.out))  # progress survives a crash
             print(f"{name}: in-context refinement done at {time.time() - t0:.1f} s", flush=True)
         del prog, m
         torch.cuda.empty_cache()
