@@ -114,9 +114,15 @@ class StepRunner:
             snap.restore()
             self.p.opt["pack"].run()  # the bf16 weight images are derived state: rebuild from restored masters
             g = torch.cuda.CUDAGraph()
-            # thread-local capture: RCCL's process-group watchdog thread queries the events of earlier
-            # (eager warm-up) collectives while this thread captures; under the default global mode that
-            # query fails with hipErrorStreamCaptureUnsupported and the watchdog aborts the process
+            # RCCL's process-group watchdog thread polls the events of pending collectives: an eager (warm-up)
+            # collective still on its list while the capture joins the communicator's stream fails that poll
+            # ("event last recorded in a capturing stream") and the watchdog aborts the process.  All of them
+            # completed at the synchronize above; give the watchdog (100 ms poll) time to retire them, and
+            # capture thread-locally so its polls of other events are legal during the capture.
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+                import time
+                time.sleep(0.5)
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 for f in fns:
                     f()
