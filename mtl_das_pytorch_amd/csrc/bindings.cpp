@@ -100,6 +100,7 @@ py::tuple conv_workspace(int mode, int cfg, int G, py::dict d) {
   ConvArgs a = parse_conv(mode, d);
   int64_t ws = 0, nt = 0;
   int rc = 0;
+  cfg &= ~CONV_XCD;
   if (cfg >= CONV_DEEP_CFG0 && cfg < CONV_DEEP_CFG0 + CONV_DEEP_NCFG) rc = 0;
   else if (cfg >= CONV_LDS_CFG0) rc = conv_lds_workspace(mode, a, G, cfg, ws, nt);
   return py::make_tuple(rc, ws, nt);
@@ -348,6 +349,7 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("conv", &conv);
   m.def("conv_workspace", &conv_workspace);
   m.attr("CONV_LDS_CFG0") = CONV_LDS_CFG0;
+  m.attr("CONV_XCD") = CONV_XCD;
   m.attr("CONV_LDS_NCFG") = CONV_LDS_NCFG;
   m.attr("CONV_DEEP_CFG0") = CONV_DEEP_CFG0;
   m.attr("CONV_DEEP_NCFG") = CONV_DEEP_NCFG;

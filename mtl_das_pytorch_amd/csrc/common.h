@@ -27,6 +27,27 @@ typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t bf16_t;  // raw bf16 storage
 
+// Block coordinates of a conv launch, optionally in XCD-contiguous order (ConvArgs::xcd).  The hardware deals
+// blocks round-robin over the 8 XCDs (linear ids b and b + 8 share one L2; speed only, never correctness:
+// MI355X_MICROARCH.md, workgroup dispatch), so consecutive pixel tiles -- which share the im2col halo rows --
+// land on 8 different L2s, and every XCD fetches most of the input.  Remapped, the 8 hardware blocks that
+// share an XCD walk one contiguous range of logical tiles, y (channel tiles / K splits) fastest, then x
+// (pixel tiles), then z (groups): a tile's channel tiles and its pixel neighbours are read through one L2.
+struct Blk { int x, y, z; };
+DEV Blk block_coords(int remap) {
+  if (!remap) return Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  const unsigned gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+  const unsigned b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned q = n >> 3, r = n & 7, xc = b & 7;
+  unsigned t = xc * q + (xc < r ? xc : r) + (b >> 3);
+  Blk k;
+  k.y = (int)(t % gy);
+  t /= gy;
+  k.x = (int)(t % gx);
+  k.z = (int)(t / gx);
+  return k;
+}
+
 DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 // round-to-nearest-even; NaN-preserving via the hardware conversion
 DEV bf16_t f2bf(float f) {

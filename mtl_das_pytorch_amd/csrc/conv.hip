@@ -140,7 +140,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   float* s_bn = s_red + (RED > ST2 ? RED : ST2);  // [8][BN_T] fused BN-backward: scale, shift, mean, invstd
                                                   // of the tail's BN, then of its residual's BN2
   float* s_nol = s_bn;                             // [2][Cs] normalise-on-load scale, shift (forward only)
-  const int z = blockIdx.z;
+  const Blk blk = block_coords(a.xcd);
+  const int z = blk.z;
   const int Ktot = a.KH * a.KW * a.Cs;
   for (int i = threadIdx.x; i < nkg; i += 256) s_tab[i] = encode_kg(i, Ktot, a.Cs >> 3, a.KW, a.src.C0);
   // MODE_DGRAD_BNS: dgrad + fused BN-backward statistics -- its own instantiation, so the extra registers
@@ -150,7 +151,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   const int zb = a.bpgs == 0 ? 0 : z;    // one tail shared by every group: its constants are group 0's
   if (want_bnb) {
     for (int i = threadIdx.x; i < BN_T; i += 256) {
-      const int n = blockIdx.y * BN_T + i;
+      const int n = blk.y * BN_T + i;
       float k[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (n < bN) {
         bn_channel_bwd(a.bbn, zb, n, k[0], k[1], k[2], k[3]);
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // LDS, and block (0, 0) of each group performs that BN's running-statistics update and publishes its
   // batch constants for the backward (the work of the forward tail this mode replaces)
   constexpr bool NOL = MODE == MODE_FWD_NOL;
-  if (NOL) bn_prepare(a.nbn, z, s_nol, s_nol + a.Cs, nullptr, nullptr, blockIdx.x == 0 && blockIdx.y == 0);
+  if (NOL) bn_prepare(a.nbn, z, s_nol, s_nol + a.Cs, nullptr, nullptr, blk.x == 0 && blk.y == 0);
   const bool nol_relu = a.nol_kind == ACT_RELU;
   __syncthreads();
 
@@ -173,8 +174,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   // accumulate the stale fragments of a step past kend (seen with the depth-4 pipeline's remainder steps).
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wn = wid % WAVES_N, wm = (wid / WAVES_N) % WAVES_M, wk = wid / (WAVES_N * WAVES_M);
-  const int n_base = blockIdx.y * BN_T + wn * WN;
-  const int m_base = blockIdx.x * BM_T + wm * WM;
+  const int n_base = blk.y * BN_T + wn * WN;
+  const int m_base = blk.x * BM_T + wm * WM;
   const int HWo = a.Ho * a.Wo;
   const int M = a.B * HWo;
   const int l16 = lane & 15, kgl = lane >> 4;
@@ -294,7 +295,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 
   // ---------------------------------------------------------------- epilogue
   // BN partial sums are reduced across the block's pixel-waves in LDS and published with ONE atomic per
-  // (channel, statistic) per block into replica blockIdx.x % NREP.
+  // (channel, statistic) per block into replica blk.x % NREP.
   float* s_st = s_red;  // [WAVES_M][BN_T][3]
   const bool want_stats = is_fwd<MODE>() && a.stats != nullptr;
   const bool want_red = want_stats || want_bnb;
@@ -383,7 +384,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   }
   if (want_red) {
     __syncthreads();
-    const int rep = blockIdx.x % (want_bnb ? a.bbn.pnrep : a.stats_nrep);
+    const int rep = blk.x % (want_bnb ? a.bbn.pnrep : a.stats_nrep);
     // forward: [G][NREP][2][N] (sum y, sum y^2); fused BN backward: rows 0/1 (2 with a BN2 residual) of
     // the tail's [G][NREP][3][bN]
     const int nrow = want_bnb ? (a.br_bn ? 3 : 2) : 2;
@@ -393,7 +394,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     double* dst = want_bnb ? a.bpart : a.stats;
     for (int q = threadIdx.x; q < BN_T * 3; q += 256) {
       const int cl = q / 3, which = q - cl * 3;
-      const int n = blockIdx.y * BN_T + cl;
+      const int n = blk.y * BN_T + cl;
       if (n < nlim && which < nrow) {
         float v = 0.f;
 #pragma unroll
@@ -906,7 +907,10 @@ static int launch_conv_cfg(const ConvArgs& a, int G, int cfg, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st) {
+int launch_conv(int mode, const ConvArgs& a0, int G, int cfg, hipStream_t st) {
+  ConvArgs a = a0;
+  a.xcd = (cfg & CONV_XCD) ? 1 : 0;
+  cfg &= ~CONV_XCD;
   if ((cfg >= CONV_LDS_CFG0 && cfg < CONV_DEEP_CFG0) || cfg >= CONV_GLDS_CFG0) {  // LDS-staged kernels (conv_lds.hip)
     const int m = mode == MODE_FWD ? (a.nol ? MODE_FWD_NOL : MODE_FWD) : (a.bpart ? MODE_DGRAD_BNS : MODE_DGRAD);
     return launch_conv_lds(m, a, G, cfg, st);

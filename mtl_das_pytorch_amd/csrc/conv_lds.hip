@@ -56,6 +56,7 @@ constexpr int LDS_WAM[8] = {2, 2, 2, 2, 2, 2, 2, 4};
 // channels 4*kgl .. +3 of each 16-channel fragment.
 struct TileCtx {
   int tid, lane, wid, wn, wm, l16, kgl, S, split, nt, ntn, z, mbase, nbase, Mq, HWq, Wq, oy0, ox0, bN;
+  int bx, gx;  // logical block x (block_coords) and the grid's x extent: split-K tile id, BN replica
 };
 
 // Epilogue stores of one output tile (lane: pixel l16 of each fragment, channels 4*kgl .. +3): bias + bf16
@@ -165,7 +166,7 @@ DEV void tile_flush(const ConvArgs& a, const TileCtx& t, float (&st)[FN][3][4], 
     }
   }
   __syncthreads();
-  const int rep = blockIdx.x % (BNS ? a.bbn.pnrep : a.stats_nrep);
+  const int rep = t.bx % (BNS ? a.bbn.pnrep : a.stats_nrep);
   double* dst = BNS ? a.bpart : a.stats;
   const int rows = BNS ? 3 : 2, nrow = BNS && a.br_bn ? 3 : 2, nlim = BNS ? t.bN : a.N;
   const int64_t gb = BNS ? (a.bpgs < 0 ? (int64_t)t.z * NREP * 3 * t.bN : (int64_t)t.z * a.bpgs)
@@ -191,7 +192,7 @@ DEV void tile_epilogue(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f
   // tile's arrival ticket (agent-scope atomic), and the last arriver reads all partials with sc1 loads
   // (L1 bypassed: no acquire fence either) in split order.
   if (t.S > 1) {
-    const int64_t tile = ((int64_t)t.z * gridDim.x + blockIdx.x) * t.ntn + t.nt;
+    const int64_t tile = ((int64_t)t.z * t.gx + t.bx) * t.ntn + t.nt;
     const uint64_t base = reinterpret_cast<uint64_t>(a.ws + tile * t.S * (BM * BN));
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
@@ -239,6 +240,7 @@ DEV void tile_epilogue(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f
 
 template <int MODE, int BM, int BN, int WAM, int KC>
 __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
+  const Blk blk = block_coords(a.xcd);
   constexpr int WAN = 4 / WAM;
   constexpr int WM = BM / WAM, WN = BN / WAN, FM = WM / 16, FN = WN / 16;
   static_assert(FM >= 1 && FN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
@@ -264,17 +266,17 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
   int p = 0;
 #pragma unroll
   for (int q = 1; q < 4; ++q)
-    if (q < pl.nph && (int)blockIdx.x >= pl.ph[q].m0) p = q;
+    if (q < pl.nph && blk.x >= pl.ph[q].m0) p = q;
   const int oy0 = PSEL(oy0), ox0 = PSEL(ox0), Hq = PSEL(Hq), Wq = PSEL(Wq);
   const int rh = PSEL(rh), nh = PSEL(nh), rw = PSEL(rw), nw = PSEL(nw), ay = PSEL(ay), ax = PSEL(ax);
   const int Kp = PSEL(Kp), m0t = PSEL(m0);
   const int S = pl.splits;
   const int ntn = (a.N + BN - 1) / BN;
-  const int nt = blockIdx.y / S, split = blockIdx.y - nt * S;
-  const int z = blockIdx.z;
+  const int nt = blk.y / S, split = blk.y - nt * S;
+  const int z = blk.z;
   const int HWq = Hq * Wq;
   const int Mq = a.B * HWq;
-  const int mbase = ((int)blockIdx.x - m0t) * BM, nbase = nt * BN;
+  const int mbase = (blk.x - m0t) * BM, nbase = nt * BN;
   const int nch = Kp / KC;
   const int cps = (nch + S - 1) / S;
   const int cb = min(nch, split * cps), ce = min(nch, cb + cps);
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
       s_tw[i] = ew;
     }
   }
-  if (NOL) bn_prepare(a.nbn, z, s_k, s_k + a.Cs, nullptr, nullptr, blockIdx.x == 0 && blockIdx.y == 0);
+  if (NOL) bn_prepare(a.nbn, z, s_k, s_k + a.Cs, nullptr, nullptr, blk.x == 0 && blk.y == 0);
   const int bN = a.bN > 0 ? a.bN : a.N;  // fused BN statistics: the tail's channels, its group
   const int zb = a.bpgs == 0 ? 0 : z;
   if (BNS) {
@@ -438,7 +440,7 @@ __global__ __launch_bounds__(256) void conv_lds_kernel(ConvArgs a, LdsPlan pl) {
     __syncthreads();
   }
 
-  const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, S, split, nt, ntn, z, mbase, nbase, Mq, HWq, Wq, oy0, ox0, bN};
+  const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, S, split, nt, ntn, z, mbase, nbase, Mq, HWq, Wq, oy0, ox0, bN, blk.x, (int)gridDim.x};
   tile_epilogue<FWD, BNS, BM, BN, WAM, WM, WN, FN, FM>(a, pl, tc, acc, s_st, s_k, s_flag);
 }
 
@@ -497,6 +499,7 @@ DEV void gl_wait_ahead(int ahead) {
 // of them.
 template <int MODE, int BM, int BN, int WAM, int NST>
 __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a, LdsPlan pl) {
+  const Blk blk = block_coords(a.xcd);
   constexpr int WAN = 4 / WAM;
   constexpr int WM = BM / WAM, WN = BN / WAN, FM = WM / 16, FN = WN / 16;
   static_assert(FM >= 1 && FN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
@@ -522,17 +525,17 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a, LdsPlan pl) 
   int p = 0;
 #pragma unroll
   for (int q = 1; q < 4; ++q)
-    if (q < pl.nph && (int)blockIdx.x >= pl.ph[q].m0) p = q;
+    if (q < pl.nph && blk.x >= pl.ph[q].m0) p = q;
   const int oy0 = PSEL(oy0), ox0 = PSEL(ox0), Hq = PSEL(Hq), Wq = PSEL(Wq);
   const int rh = PSEL(rh), nh = PSEL(nh), rw = PSEL(rw), nw = PSEL(nw), ay = PSEL(ay), ax = PSEL(ax);
   const int Kp = PSEL(Kp), m0t = PSEL(m0);
   const int S = pl.splits;
   const int ntn = (a.N + BN - 1) / BN;
-  const int nt = blockIdx.y / S, split = blockIdx.y - nt * S;
-  const int z = blockIdx.z;
+  const int nt = blk.y / S, split = blk.y - nt * S;
+  const int z = blk.z;
   const int HWq = Hq * Wq;
   const int Mq = a.B * HWq;
-  const int mbase = ((int)blockIdx.x - m0t) * BM, nbase = nt * BN;
+  const int mbase = (blk.x - m0t) * BM, nbase = nt * BN;
   const int nch = Kp / KC;
   const int cps = (nch + S - 1) / S;
   const int cb = min(nch, split * cps), ce = min(nch, cb + cps);
@@ -669,7 +672,7 @@ __global__ __launch_bounds__(256) void conv_glds_kernel(ConvArgs a, LdsPlan pl) 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the stage buffers are dead; s_st / s_flag live past them
-  const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, S, split, nt, ntn, z, mbase, nbase, Mq, HWq, Wq, oy0, ox0, bN};
+  const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, S, split, nt, ntn, z, mbase, nbase, Mq, HWq, Wq, oy0, ox0, bN, blk.x, (int)gridDim.x};
   tile_epilogue<FWD, BNS, BM, BN, WAM, WM, WN, FN, FM>(a, pl, tc, acc, s_st, s_k, s_flag);
 }
 
@@ -704,6 +707,7 @@ constexpr int pt_wkp() { return pt_ksteps<CB>() * 32 + 8; }
 
 template <int MODE, int BM, int BN, int WAM, int CB>
 __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a, PatchPlan pp) {
+  const Blk blk = block_coords(a.xcd);
   constexpr int WAN = 4 / WAM;
   constexpr int WM = BM / WAM, WN = BN / WAN, FM = WM / 16, FN = WN / 16;
   static_assert(FM >= 1 && FN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile");
@@ -728,14 +732,14 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a, PatchPlan p
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l16 = lane & 15, kgl = lane >> 4;
   const int wn = wid % WAN, wm = wid / WAN;
-  const int z = blockIdx.z, nt = blockIdx.y, ntn = gridDim.y;
-  const int b = (int)blockIdx.x / pp.nstrip, oh0 = ((int)blockIdx.x - b * pp.nstrip) * pp.R;
+  const int z = blk.z, nt = blk.y, ntn = gridDim.y;
+  const int b = blk.x / pp.nstrip, oh0 = (blk.x - b * pp.nstrip) * pp.R;
   const int rows = min(pp.R, pp.Hout - oh0);
   const int HWo = pp.Hout * pp.Wout;
   const int mbase = b * HWo + oh0 * pp.Wout, nbase = nt * BN;
   const int Mtile = mbase + rows * pp.Wout;  // pixels of this strip end here (the next strip / image starts)
 
-  if (NOL) bn_prepare(a.nbn, z, s_k, s_k + a.Cs, nullptr, nullptr, blockIdx.x == 0 && blockIdx.y == 0);
+  if (NOL) bn_prepare(a.nbn, z, s_k, s_k + a.Cs, nullptr, nullptr, blk.x == 0 && blk.y == 0);
   const int bN = a.bN > 0 ? a.bN : a.N;
   const int zb = a.bpgs == 0 ? 0 : z;
   if (BNS) {
@@ -862,7 +866,7 @@ __global__ __launch_bounds__(256) void conv_patch_kernel(ConvArgs a, PatchPlan p
 
   LdsPlan pl{};
   pl.qy = 1; pl.qx = 1;
-  const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, 1, 0, nt, ntn, z, mbase, nbase, Mtile, HWo, pp.Wout, 0, 0, bN};
+  const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, 1, 0, nt, ntn, z, mbase, nbase, Mtile, HWo, pp.Wout, 0, 0, bN, blk.x, (int)gridDim.x};
   tile_epilogue<FWD, BNS, BM, BN, WAM, WM, WN, FN, FM>(a, pl, tc, acc, s_st, s_k, s_flag);
 }
 
@@ -1007,13 +1011,14 @@ __global__ __launch_bounds__(256) void conv_patchp_kernel(ConvArgs a, PatchPlan 
     const int rows = min(pp.R, pp.Hout - oh0);
     const int mbase = b * HWo + oh0 * pp.Wout;
     const TileCtx tc{tid, lane, wid, wn, wm, l16, kgl, 1, 0, nt, ntn, z, mbase, nbase, mbase + rows * pp.Wout, HWo,
-                     pp.Wout, 0, 0, bN};
+                     pp.Wout, 0, 0, bN, (int)blockIdx.x, (int)gridDim.x};
     tile_store<FWD, BNS, BN, WM, WN, FN, FM>(a, pl, tc, acc, s_k, st);
     cur ^= 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the strip buffers are dead; s_st lives past the weights
-  const TileCtx tf{tid, lane, wid, wn, wm, l16, kgl, 1, 0, nt, ntn, z, 0, nbase, 0, HWo, pp.Wout, 0, 0, bN};
+  const TileCtx tf{tid, lane, wid, wn, wm, l16, kgl, 1, 0, nt, ntn, z, 0, nbase, 0, HWo, pp.Wout, 0, 0, bN,
+                   (int)blockIdx.x, (int)gridDim.x};
   tile_flush<FWD, BNS, BN, WAM, WN, FN>(a, tf, st, s_st);
 }
 
@@ -1249,6 +1254,7 @@ int launch_mode(const ConvArgs& a, int G, const LdsCfg& c, hipStream_t st) {
 }  // namespace
 
 int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_floats, int64_t& ntickets) {
+  cfg &= ~CONV_XCD;
   if (mode == MODE_FWD && a.nol) mode = MODE_FWD_NOL;  // the launch mode launch_conv will pick
   if (mode == MODE_DGRAD && a.bpart) mode = MODE_DGRAD_BNS;
   int tile, cbi;

@@ -61,6 +61,7 @@ struct ConvArgs {
   // block resets it), sized by conv_lds_workspace
   float* ws;
   unsigned* cnt;
+  int xcd;  // block_coords remap (common.h): XCD-contiguous tile order (set from the CONV_XCD cfg flag)
 };
 
 // ConvArgs::add: the extra gradient sources of output element (row m, channels n0 .. n0+3), added in order
@@ -251,6 +252,8 @@ constexpr int CONV_PATCH_CFG0 = 192, CONV_PATCH_NCFG = 15;
 constexpr int CONV_GDEEP_CFG0 = 208, CONV_GDEEP_NCFG = 32;
 // persistent, DMA-pipelined patch conv (one channel slice): cfg = CONV_PATCHP_CFG0 + 3 * tile + cb
 constexpr int CONV_PATCHP_CFG0 = 240, CONV_PATCHP_NCFG = 15;
+// cfg flag of any conv config: launch it in XCD-contiguous tile order (ConvArgs::xcd, common.h block_coords)
+constexpr int CONV_XCD = 4096;
 int launch_conv_lds(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 // fp32 workspace floats and ticket count a cfg needs (0 when it does not split K); < 0: cfg invalid for a
 int conv_lds_workspace(int mode, const ConvArgs& a, int G, int cfg, int64_t& ws_floats, int64_t& ntickets);

@@ -17,7 +17,7 @@ import torch
 
 from ..ops.functional import (CONV_DEEP_CFG0, CONV_DEEP_NCFG, CONV_GLDS_CFG0, CONV_GLDS_NCFG, CONV_LDS_CFG0,
                               CONV_LDS_NCFG, CONV_PATCH_CFG0, CONV_PATCH_NCFG, CONV_PATCHP_CFG0, CONV_PATCHP_NCFG,
-                              GDEEP_TILES, WGRAD_PATCH, WGRAD_TILES, conv_workspace, glds_cfg)
+                              CONV_XCD, GDEEP_TILES, WGRAD_PATCH, WGRAD_TILES, conv_workspace, glds_cfg)
 from ..ops.hip import lib
 
 # conv.hip register-pipelined tiles 0-13 (pipeline depth 2, and 4 at CONV_DEEP_CFG0 + tile), then
@@ -217,7 +217,8 @@ def _set_conv_cfg(launch, cfg: int, keep: dict) -> bool:
 
 def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str, int], topk: int = 3,
                     reps: int = 15, rounds: int = 3, margin: float = 0.002, verbose: bool = True,
-                    on_change=None) -> Dict[str, int]:
+                    on_change=None, cfg_pass: bool = True, xcd_pass: bool = True,
+                    tail_pass: bool = True) -> Dict[str, int]:
     """Refine the conv configs (and the BN-tail backward variants) of a lowered program by timing the WHOLE
     training step, not the isolated launch.
 
@@ -274,7 +275,7 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
     for sig, ls in groups.items():
         mode, cfg, G, d = ls[0].args
         iso = _isolated(mode, G, d, sig)
-        cur = next((t for t, c in iso if c == cfg), iso[0][0] if iso else 0.0)
+        cur = next((t for t, c in iso if c == cfg & ~CONV_XCD), iso[0][0] if iso else 0.0)
         order.append((cur * len(ls), sig))
     order.sort(reverse=True)
     base = step_ms()
@@ -284,10 +285,11 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
     # every candidate is compared with the incumbent measured right before it: the step time drifts over
     # a minutes-long run (clocks, thermals), and a stale baseline credits that drift to whichever candidate
     # happens to be timed (a first version of this tuner "gained" 10 % that the benchmark did not show)
-    for _, sig in order:
+    for _, sig in (order if cfg_pass else []):
         ls = groups[sig]
         mode, cur, G, d = ls[0].args
-        cands = [c for _, c in _isolated(mode, G, d, sig)[:topk] if c != cur]
+        flag = cur & CONV_XCD  # the tile order is decided by its own pass below
+        cands = [c | flag for _, c in _isolated(mode, G, d, sig)[:topk] if c | flag != cur]
         best_cfg = cur
         for c in cands:
             t_inc = step_ms()
@@ -307,6 +309,30 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
                 print(f"  {sig}: cfg {cur} -> {best_cfg}, step {base * 1e3:.1f} us", flush=True)
             if on_change is not None:
                 on_change(cache)
+    # tile order: every signature's config with the XCD-contiguous block order toggled (csrc/common.h
+    # block_coords; it pays where neighbouring tiles share halo rows through one L2 -- only measurable in the
+    # step, where the operands come from other kernels' writes, not from an L2-hot isolated replay)
+    if xcd_pass:
+        for _, sig in order:
+            ls = groups[sig]
+            cur = ls[0].args[1]
+            t_inc = step_ms()
+            if not all(_set_conv_cfg(l, cur ^ CONV_XCD, keep) for l in ls):
+                for l in ls:
+                    _set_conv_cfg(l, cur, keep)
+                continue
+            t = step_ms()
+            if t < t_inc * (1.0 - margin) and step_ms() < t_inc * (1.0 - margin):
+                base = t
+                cache[sig] = cur ^ CONV_XCD
+                if verbose:
+                    print(f"  {sig}: xcd order {int(bool(cur & CONV_XCD))} -> {int(not cur & CONV_XCD)}, "
+                          f"step {base * 1e3:.1f} us", flush=True)
+                if on_change is not None:
+                    on_change(cache)
+            else:
+                for l in ls:
+                    _set_conv_cfg(l, cur, keep)
     # BN-tail backward variants (reduce + apply vs the single-launch kernel), chosen in isolation by
     # autotune_phases, re-decided in the step the same way
     tails: Dict[str, list] = {}
@@ -314,7 +340,7 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
         if l.name.startswith("tailbwd") and l.args[3].get("fused", 0) in (0, 1):
             kind, G, blocks, d = l.args
             tails.setdefault(tail_bwd_signature(kind, G, d), []).append(l)
-    for sig, ls in tails.items():
+    for sig, ls in (tails.items() if tail_pass else []):
         kind, G, blocks, d = ls[0].args
         cur = d.get("fused", 0)
         alt = 1 - cur

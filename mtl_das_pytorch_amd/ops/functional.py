@@ -82,6 +82,7 @@ PATCH_CB = [16, 32, 64]  # channel slice staged per pass
 CONV_GDEEP_CFG0, CONV_GDEEP_NCFG = 208, 32  # LDS-DMA configs with a deep ring (up to 8 K chunks in flight)
 CONV_PATCHP_CFG0, CONV_PATCHP_NCFG = 240, 15  # persistent, DMA-pipelined patch conv (one channel slice)
 GDEEP_TILES = [0, 1, 2, 3, 5, 7]  # GLDS_TILES entries that have a deep ring (conv_lds.hip GL_NST_DEEP)
+CONV_XCD = 4096  # flag on any conv config: XCD-contiguous tile order (csrc/common.h block_coords)
 
 
 def lds_cfg(tile: int, kc: int = 64, splits: int = 1) -> int:
@@ -107,7 +108,7 @@ def conv_workspace(mode: int, cfg: int, G: int, d: dict, device) -> Optional[tup
     """Attach the split-K workspace an LDS-staged conv config needs (fp32 partial tiles + zeroed arrival
     tickets) to the argument dict ``d``; returns the tensors to keep alive, or None when ``cfg`` cannot run
     these arguments."""
-    if cfg < CONV_LDS_CFG0:
+    if (cfg & ~CONV_XCD) < CONV_LDS_CFG0:
         return ()
     rc, ws, nt = lib().conv_workspace(mode, cfg, G, d)
     if rc != 0:

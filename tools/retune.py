@@ -20,7 +20,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mtl_das_pytorch_amd.engine.inception import InceptionProgram  # noqa: E402
 from mtl_das_pytorch_amd.engine.mtl import MTLProgram  # noqa: E402
 from mtl_das_pytorch_amd.data.synthetic import generate  # noqa: E402
-from mtl_das_pytorch_amd.engine.tune import autotune_phases, autotune_program, load_cache, save_cache, tune_in_context  # noqa: E402,E501
+from mtl_das_pytorch_amd.engine.tune import (autotune_phases, autotune_program, conv_signature, load_cache,  # noqa: E402
+                                             save_cache, tune_in_context)
+from mtl_das_pytorch_amd.ops.functional import CONV_XCD  # noqa: E402
 from mtl_das_pytorch_amd.models import build_model, encode_joint  # noqa: E402
 
 
@@ -35,6 +37,9 @@ def main():
     ap.add_argument("--margin", type=float, default=0.002, help="in-context: relative step-time gain to keep a config")
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--drop", default="", help="with --keep: comma-separated key prefixes to re-measure (e.g. wgrad)")
+    ap.add_argument("--passes", default="cfg,xcd,tail", help="in-context passes: conv configs, tile order, BN tails")
+    ap.add_argument("--xcd-init", default="keep", choices=("keep", "on", "off"),
+                    help="in-context: the tile order every conv signature of the model starts from")
     args = ap.parse_args()
     cache = load_cache() if args.keep else {}
     for pre in filter(None, args.drop.split(",")):
@@ -53,8 +58,18 @@ def main():
             autotune_program(prog, cache=cache, measure=False)  # batch the weight gradients as the bench does
             X, d, e = generate(4 * args.batch, seed=3, device="cuda")
             labels = encode_joint(d, e) if name == "multi_classifier" else torch.stack([d, e], 1)
+            if args.xcd_init != "keep":
+                for ph in (prog.fwd_train, prog.fwd_eval, prog.bwd):
+                    for l in ph.launches:
+                        if l.name in ("conv_fwd", "conv_dgrad"):
+                            mode, cfg, G, d = l.args
+                            cfg = (cfg | CONV_XCD) if args.xcd_init == "on" else (cfg & ~CONV_XCD)
+                            cache[conv_signature(mode, G, d)] = cfg
+                            l.args = (mode, cfg, G, d)
+            ps = args.passes.split(",")
             tune_in_context(prog, X, labels, cache, topk=args.topk, margin=args.margin, reps=args.reps,
-                            on_change=lambda c: save_cache(c, args.out))  # progress survives a crash
+                            on_change=lambda c: save_cache(c, args.out),  # progress survives a crash
+                            cfg_pass="cfg" in ps, xcd_pass="xcd" in ps, tail_pass="tail" in ps)
             print(f"{name}: in-context refinement done at {time.time() - t0:.1f} s", flush=True)
         del prog, m
         torch.cuda.empty_cache()
