@@ -9,9 +9,12 @@ rounding, independent of the network's error amplification at init.  The program
 batch (32) with the tuned kernel configs the bench uses (LDS-staged convs, split-K, fused statistics,
 normalise-on-load).  Reference: model/modelA_MTL.py:7-174.
 
-Parametrized over the input channels: 1 (the reference; the stem runs as a 1 x 7 conv over 7 packed taps)
-and 2 (BASELINE's 2-channel north star, ``--in_channels 2``: gather of two channels into the 8-channel
-stored input, the unpacked 7x7 stem at K = 392 padded to 416 and its weight gradient / finalize).
+Parametrized over the model -- A, and B (``Single_Task_Net``, one task branch; reference
+model/modelB_singleTask.py) for each task -- and over A's input channels: 1 (the reference; the stem runs as a
+1 x 7 conv over 7 packed taps) and 2 (BASELINE's 2-channel north star, ``--in_channels 2``: gather of two channels into the 8-channel
+stored input, the unpacked 7x7 stem at K = 392 padded to 416 and its weight gradient / finalize); plus A's
+data-parallel backward program (2 gradient buckets: the backward cut into pieces, weight gradients and
+finalize per piece), run here without collectives.
 """
 import pytest
 import torch
@@ -54,12 +57,14 @@ def bn_backward(dz, y, bn, z=0):
     return dy, (dz * xh).sum((0, 2, 3)), dz.sum((0, 2, 3))
 
 
-@pytest.fixture(scope="module", params=[1, 2], ids=["cin1", "cin2"])
+@pytest.fixture(scope="module", params=[("MTL", 1, 1), ("MTL", 2, 1), ("single_event", 1, 1),
+                                        ("single_distance", 1, 1), ("MTL", 1, 2)],
+                ids=["cin1", "cin2", "B_event", "B_distance", "dp_buckets2"])
 def engine_step(request):
     from mtl_das_pytorch_amd.data.synthetic import generate
     from mtl_das_pytorch_amd.engine.mtl import MTLProgram
     from mtl_das_pytorch_amd.engine.tune import autotune_program
-    from mtl_das_pytorch_amd.models import MTL_Net
+    from mtl_das_pytorch_amd.models import build_model
     # the single-op fp32 references run on PyTorch's native im2col + GEMM convolution, not MIOpen: one run
     # of this module hit an illegal address inside the reference conv backward (MIOpen solver choice)
     flags = (torch.backends.cudnn.enabled, torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32)
@@ -68,10 +73,12 @@ def engine_step(request):
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.manual_seed(0)
     B = 32
-    cin = request.param
-    model = MTL_Net(in_channels=cin)
+    name, cin, nbuckets = request.param
+    model = build_model(name, in_channels=cin)  # Model A, or Model B (Single_Task_Net: one task branch)
     prog = MTLProgram(model, B, "cuda")
     assert (prog.stem_pack[0] > 0) == (cin == 1)
+    if nbuckets > 1:  # the data-parallel backward: cut into gradient-bucket pieces, wgrads batched per piece
+        assert len(prog.segment_backward(nbuckets)) == nbuckets
     autotune_program(prog, measure=False)  # the bench's tuned kernel configs
     X, d, e = generate(B, seed=11, device="cuda", in_channels=cin)
     labels = torch.stack([d, e], 1)
@@ -251,7 +258,7 @@ def test_mtl_backward_layer_local(engine_step):
     for t in range(T):
         K = model.task_cate_num[t]
         p = prog.logp[t, :, :K].exp()
-        p[torch.arange(prog.B), labels[:, t]] -= 1
+        p[torch.arange(prog.B), labels[:, prog.lab_off[t]]] -= 1
         gsz = A4.C // K
         scale = prog.loss_weights[t] / (prog.B * gsz * A4.H * A4.W)
         ref = (p * scale).repeat_interleave(gsz, 1)[:, :, None, None].expand(-1, -1, A4.H, A4.W)
