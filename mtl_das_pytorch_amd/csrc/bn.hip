@@ -110,40 +110,62 @@ DEV void tail_fwd_impl(const TailArgs& a) {
   }
   const bf16_t* rz = a.r ? a.r + a.rgs * z : nullptr;
   const int M = a.B * a.H * a.W;
-  for (int p = blockIdx.x * L.PL + L.pl; p < M; p += gridDim.x * L.PL) {
-    float v[8];
-    load8(yz + (int64_t)p * a.ldy + c, v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
-    if (KIND == ACT_RELU) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
-    } else if (KIND == ACT_SIGMOID) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = sigmoidf_(v[j]);
-    } else if (KIND == SIGMUL) {
-      float f[8];
-      load8(rz + (int64_t)p * a.ldr + c, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = sigmoidf_(v[j]) * f[j];
-    } else if (is_add<KIND>()) {
-      float f[8];
-      load8(rz + (int64_t)p * a.ldr + c, f);
-      if (KIND == ADD_RELU2) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = f[j] * sc2[j] + sh2[j];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] + f[j], 0.f);
+  // two pixels per iteration, every load of both issued before the first store: the stores may alias the
+  // inputs as far as the compiler knows, so a one-pixel loop keeps one pixel's loads in flight per thread
+  // (the large maps -- Model C's 47x122 stem -- then ran at ~2 TB/s)
+  constexpr bool RES = KIND == SIGMUL || is_add<KIND>();
+  const int step = gridDim.x * L.PL;
+  for (int p = blockIdx.x * L.PL + L.pl; p < M; p += 2 * step) {
+    const int p2 = p + step;
+    const bool has2 = p2 < M;
+    const int q2 = has2 ? p2 : p;
+    const uint4 uy[2] = {*reinterpret_cast<const uint4*>(yz + (int64_t)p * a.ldy + c),
+                         *reinterpret_cast<const uint4*>(yz + (int64_t)q2 * a.ldy + c)};
+    uint4 ur[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    if (RES) {
+      ur[0] = *reinterpret_cast<const uint4*>(rz + (int64_t)p * a.ldr + c);
+      ur[1] = *reinterpret_cast<const uint4*>(rz + (int64_t)q2 * a.ldr + c);
     }
-    store8(oz + (int64_t)p * a.ldo + c, v);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !has2) break;
+      float v[8];
+      unpack8(uy[h], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
+      if (KIND == ACT_RELU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+      } else if (KIND == ACT_SIGMOID) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = sigmoidf_(v[j]);
+      } else if (KIND == SIGMUL) {
+        float f[8];
+        unpack8(ur[h], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = sigmoidf_(v[j]) * f[j];
+      } else if (is_add<KIND>()) {
+        float f[8];
+        unpack8(ur[h], f);
+        if (KIND == ADD_RELU2) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = f[j] * sc2[j] + sh2[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] + f[j], 0.f);
+      }
+      store8(oz + (int64_t)(h ? p2 : p) * a.ldo + c, v);
+    }
   }
 }
 
-// Default register allocation (66-80 VGPRs, 6 waves per SIMD).  A budget of 8 waves per SIMD fits every kind
-// without spilling but measured +170 us on Model A's forward (docs/PERF.md, rejected).
+// Default register allocation: ~100 VGPRs (4 waves per SIMD) for most kinds, which keeps bn_prepare's fp64
+// replica loads in flight.  Budgets measured slower: 6 waves per SIMD (<= 85 VGPRs) A 33.5k -> 30.3k samples/s
+// (round 3), 8 waves +170 us on Model A's forward (round 2; docs/PERF.md).
 template <int KIND>
-__global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) { tail_fwd_impl<KIND>(a); }
+__global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
+  tail_fwd_impl<KIND>(a);
+}
 
 // ------------------------------------------------------------------------------------------------
 // backward
@@ -440,7 +462,6 @@ template <int KIND>
 constexpr int bnb_waves() {
   return KIND == ACT_NONE ? 8 : (KIND == ACT_RELU || KIND == ACT_SIGMOID) ? 6 : (KIND == SIGMUL || KIND == ADD_RELU) ? 5 : 0;
 }
-
 // Single-launch BN backward for small maps: block (cg, -, z) owns channels [8cg, 8cg+8) for ALL M
 // pixels, so the batch reduction is a block reduction (no global atomics, no second launch, exact and
 // deterministic).  Each of the 1024 threads keeps the dz / xhat of its R <= 4 pixels in registers, so

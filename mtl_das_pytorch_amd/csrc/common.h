@@ -55,6 +55,14 @@ DEV bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&h);
 }
 
+DEV void unpack8(uint4 u, float* v) {  // 8 bf16 -> fp32
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
 DEV void load8(const bf16_t* p, float* v) {
   uint4 u = *reinterpret_cast<const uint4*>(p);
   uint32_t w[4] = {u.x, u.y, u.z, u.w};

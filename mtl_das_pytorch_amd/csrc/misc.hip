@@ -59,15 +59,6 @@ int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, 
 }
 
 
-DEV void unpack8(const uint4& u, float* v) {
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-
 // 3x3 pools of the Inception model: MAX = 1 max pool stride 2 (no padding), MAX = 0 average pool stride 1
 // padding 1 (count_include_pad: always /9).  One thread per (output pixel, 8-channel group).  All nine
 // window loads are issued before any is consumed (with the load and its use in the same bounds-checked
