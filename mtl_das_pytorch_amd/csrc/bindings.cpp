@@ -220,15 +220,9 @@ WgradArgs parse_wgrad(const py::dict& d) {
   return a;
 }
 
-AdamArgs parse_adam(const py::dict& d);
-
-// adam (optional dict, as adam_pack's): fused Adam update of every finalized conv weight
-void wgrad_finalize(int64_t descs, int nd, int64_t nblocks, double scale, int64_t stream, py::object adam) {
-  AdamArgs a{};
-  const bool fuse = !adam.is_none();
-  if (fuse) a = parse_adam(adam.cast<py::dict>());
+void wgrad_finalize(int64_t descs, int nd, int64_t nblocks, double scale, int64_t stream) {
   check(launch_wgrad_finalize(reinterpret_cast<const WgFinDesc*>(static_cast<intptr_t>(descs)), nd, nblocks,
-                              (float)scale, S(stream), fuse ? &a : nullptr), "wgrad_finalize");
+                              (float)scale, S(stream)), "wgrad_finalize");
 }
 
 TailArgs parse_tail(const py::dict& d) {
@@ -328,7 +322,7 @@ void grad_sum(py::list g, int64_t out, int ldo, int64_t M, int C, int64_t stream
   check(launch_grad_sum(parse_grads(g), reinterpret_cast<float*>(out), ldo, M, C, S(stream)), "grad_sum");
 }
 
-AdamArgs parse_adam(const py::dict& d) {
+void adam_pack(int64_t stream, py::dict d) {
   AdamArgs a{};
   a.p = P<float>(d, "p"); a.g = P<const float>(d, "g"); a.m = P<float>(d, "m"); a.v = P<float>(d, "v");
   a.n = I(d, "n");
@@ -337,14 +331,6 @@ AdamArgs parse_adam(const py::dict& d) {
   a.b1 = (float)F(d, "b1", 0.9); a.b2 = (float)F(d, "b2", 0.999); a.eps = (float)F(d, "eps", 1e-8);
   a.wd = (float)F(d, "wd", 0.0); a.grad_scale = (float)F(d, "grad_scale", 1.0);
   a.update = (int)I(d, "update", 1);
-  a.chunks = P<const int64_t>(d, "chunks");
-  a.nchunk = (int)I(d, "nchunk", 0);
-  if (a.nchunk > 0 && !a.chunks) throw std::runtime_error("adam: nchunk without chunks");
-  return a;
-}
-
-void adam_pack(int64_t stream, py::dict d) {
-  AdamArgs a = parse_adam(d);
   check(launch_adam_pack(a, P<const OptSeg>(d, "segs"), (int)I(d, "nsegs"), I(d, "nblocks"), S(stream)), "adam_pack");
 }
 
@@ -376,8 +362,7 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.attr("CONV_PATCHP_CFG0") = CONV_PATCHP_CFG0;
   m.attr("CONV_PATCHP_NCFG") = CONV_PATCHP_NCFG;
   m.def("wgrad", &wgrad);
-  m.def("wgrad_finalize", &wgrad_finalize, py::arg("descs"), py::arg("nd"), py::arg("nblocks"), py::arg("scale"),
-        py::arg("stream"), py::arg("adam") = py::none());
+  m.def("wgrad_finalize", &wgrad_finalize);
   m.def("tail_fwd", &tail_fwd);
   m.def("tail_bwd", &tail_bwd);
   m.def("mtl_head", &mtl_head);

@@ -775,10 +775,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const Wgr
 //   the split reads are coalesced; lane q sums splits q, q + lanes, ... with 8 loads in flight and the
 //   lane partials are added in lane order through LDS -- deterministic.
 // Descriptors own whole blocks, so the mapping is uniform within a block.
-__global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale,
-                                                             AdamArgs ad, int fuse) {
-  float c1 = 0.f, c2 = 0.f;
-  if (fuse) adam_consts(ad, c1, c2);
+__global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __restrict__ descs, int nd, float scale) {
   __shared__ float s_part[256];
   const int bx = (int)blockIdx.x;
   int lo = 0, hi = nd - 1;  // last descriptor with block0 <= bx
@@ -812,9 +809,7 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
     if (ok && q == 0) {
       float sum = 0.f;
       for (int l = 0; l < L; ++l) sum += s_part[l * EPB + ie];
-      float* dst = D.grad + g * D.ggs + (co * D.Ci + ci) * taps + tap;
-      if (fuse) adam_elem(ad, dst - ad.g, sum * scale, c1, c2);
-      else *dst = sum * scale;
+      D.grad[g * D.ggs + (co * D.Ci + ci) * taps + tap] = sum * scale;
     }
     return;
   }
@@ -864,11 +859,8 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(const WgFinDesc* __
       if (ok[j]) a0[j] += src[j][(int64_t)sp * sstride];
   }
 #pragma unroll
-  for (int j = 0; j < FIN_EPT; ++j) {
-    if (!ok[j]) continue;
-    if (fuse) adam_elem(ad, dst[j] - ad.g, (a0[j] + a1[j]) * scale, c1, c2);
-    else *dst[j] = (a0[j] + a1[j]) * scale;
-  }
+  for (int j = 0; j < FIN_EPT; ++j)
+    if (ok[j]) *dst[j] = (a0[j] + a1[j]) * scale;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1031,12 +1023,9 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
   return (int)hipGetLastError();
 }
 
-int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st,
-                          const AdamArgs* ad) {
+int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st) {
   if (nblocks <= 0) return 0;
-  const AdamArgs none{};
-  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, d_descs, nd, scale,
-                     ad ? *ad : none, ad ? 1 : 0);
+  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, d_descs, nd, scale);
   return (int)hipGetLastError();
 }
 

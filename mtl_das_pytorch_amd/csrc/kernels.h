@@ -236,29 +236,7 @@ struct AdamArgs {
   const float* lr; const float* step;  // device scalars (step = number of completed steps)
   float b1, b2, eps, wd, grad_scale;
   int update;  // 0: pack only
-  // optional (nchunk > 0): the Adam update covers only these [start, start + len) chunks of the flat buffer
-  // (len <= 1024, multiples of 4) -- the parameters the fused weight-gradient finalize does not update
-  const int64_t* chunks;
-  int nchunk;
 };
-
-// Adam step constants of the current step (t = completed steps + 1): c1 = lr / (1 - b1^t), c2 = 1 / sqrt(1 - b2^t)
-DEV void adam_consts(const AdamArgs& a, float& c1, float& c2) {
-  const float t = a.step[0] + 1.f;
-  c1 = a.lr[0] / (1.f - powf(a.b1, t));
-  c2 = 1.f / sqrtf(1.f - powf(a.b2, t));
-}
-
-// One element of the flat buffer: the arithmetic of adam_kernel (optim.hip), so a fused update is bitwise the
-// unfused one
-DEV void adam_elem(const AdamArgs& a, int64_t i, float grad, float c1, float c2) {
-  float p = a.p[i], m = a.m[i], v = a.v[i];
-  const float gj = grad * a.grad_scale + a.wd * p;
-  m = a.b1 * m + (1.f - a.b1) * gj;
-  v = a.b2 * v + (1.f - a.b2) * gj * gj;
-  p -= c1 * m / (sqrtf(v) * c2 + a.eps);
-  a.p[i] = p; a.m[i] = m; a.v[i] = v;
-}
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 // LDS-staged implicit GEMM (conv_lds.hip): cfg = CONV_LDS_CFG0 + 8 * tile + 4 * (KC == 128) + log2(splits)
@@ -285,10 +263,7 @@ constexpr int WGRAD_PATCH_CFG0 = 12, WGRAD_PATCH_NCFG = 8;  // wgrad cfgs 12-19:
 int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8, int& R);
 int wgrad_ntiles(int cfg, const WgradArgs& a);  // tiles per group of a wgrad launch, < 0: cfg invalid for a
 int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st);
-// ad (optional): fused Adam -- each finalized weight gradient updates its parameter and moments in place
-// instead of being stored (single-GPU steps; the gradient buffer is then not written)
-int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st,
-                          const AdamArgs* ad = nullptr);
+int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);
 int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, int fused, hipStream_t st);
 int launch_mtl_head(const HeadArgs& a, hipStream_t st);

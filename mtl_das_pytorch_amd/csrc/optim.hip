@@ -45,31 +45,6 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a, int64_t n) {
   }
 }
 
-// Adam over a list of chunks of the flat buffer (AdamArgs::chunks): block b updates chunk b, one float4 per
-// thread.  Used with the fused weight-gradient finalize, which has already updated every conv weight.
-__global__ __launch_bounds__(256) void adam_chunks_kernel(AdamArgs a) {
-  const int64_t start = a.chunks[2 * blockIdx.x], len = a.chunks[2 * blockIdx.x + 1];
-  if (4 * (int64_t)threadIdx.x >= len) return;
-  float c1, c2;
-  adam_consts(a, c1, c2);
-  const int64_t i = (start >> 2) + threadIdx.x;
-  float4 p = reinterpret_cast<float4*>(a.p)[i];
-  const float4 g = reinterpret_cast<const float4*>(a.g)[i];
-  float4 m = reinterpret_cast<float4*>(a.m)[i];
-  float4 v = reinterpret_cast<float4*>(a.v)[i];
-  float* pp = &p.x; const float* gg = &g.x; float* mm = &m.x; float* vv = &v.x;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float gj = gg[j] * a.grad_scale + a.wd * pp[j];
-    mm[j] = a.b1 * mm[j] + (1.f - a.b1) * gj;
-    vv[j] = a.b2 * vv[j] + (1.f - a.b2) * gj * gj;
-    pp[j] -= c1 * mm[j] / (sqrtf(vv[j]) * c2 + a.eps);
-  }
-  reinterpret_cast<float4*>(a.p)[i] = p;
-  reinterpret_cast<float4*>(a.m)[i] = m;
-  reinterpret_cast<float4*>(a.v)[i] = v;
-}
-
 // Data-gradient image [Ci][(kh,kw,co)] of one (64 co) x (cit ci) tile of a [Co][Ci][taps] weight, through
 // LDS: the reads walk each co's contiguous (ci, tap) run, the writes 16-byte chunks of 8 co -- both
 // coalesced.  (The per-element mapping read the masters with a stride of Ci*taps floats: every 4-byte
@@ -151,11 +126,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ P, 
 __global__ void step_inc_kernel(float* step) { step[0] += 1.f; }
 
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st) {
-  if (a.update && a.nchunk > 0) {
-    hipLaunchKernelGGL(adam_chunks_kernel, dim3(a.nchunk), dim3(256), 0, st, a);
-    int rc = (int)hipGetLastError();
-    if (rc) return rc;
-  } else if (a.update) {
+  if (a.update) {
     const int64_t n4 = a.n >> 2;
     const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
     hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, st, a, a.n);

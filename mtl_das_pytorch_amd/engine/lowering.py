@@ -10,8 +10,7 @@ import torch
 from ..ops.functional import WGRAD_PATCH, WGRAD_TILES
 from ..ops.hip import lib
 from .core import Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, pad_to
-from .program import (Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin,
-                      k_wgfin_adam, k_wgrad,
+from .program import (Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad,
                       k_wgrad_batched)
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
@@ -592,45 +591,6 @@ class LoweredProgram:
         pack = Phase("pack")
         pack.add("pack", k_adam, dict(base, update=0))
         return {"adam": upd, "pack": pack}
-
-    def fused_step_phases(self) -> Optional[tuple]:
-        """(backward, optimizer) phases of a single-GPU step whose weight-gradient finalize also applies Adam
-        to every conv weight (csrc/conv.hip wgrad_finalize_kernel with AdamArgs): the summed split slabs update
-        the parameter and its moments in place, so the conv weights' fp32 gradients are never written to and
-        read back from the flat buffer (Model C: 87 MB each way), and the optimizer launch only updates the
-        remaining parameters (BN affine, fc), chunk by chunk, before the bf16 re-pack.  The arithmetic is
-        adam_kernel's.  None when the backward has several finalizes (gradient buckets: the all-reduce must
-        sit between the finalize and Adam) or the optimizer is not set up.  Build after autotuning (the
-        finalize table depends on the tuned split counts)."""
-        ls = self.bwd.launches
-        fins = [i for i, l in enumerate(ls) if l.name == "wgrad_finalize"]
-        if len(fins) != 1 or any(l.name == "cut" for l in ls) or not hasattr(self, "_opt_base"):
-            return None
-        i = fins[0]
-        fin = ls[i]
-        table, nd, nblocks = fin.args
-        ad = dict(self._opt_base, update=1, **self._opt_hparams)
-        f = self.flat
-        covered = []
-        for c in self.convs:
-            n = c.Co * c.Ci * c.KH * c.KW
-            o0 = f.off(c.mods[0].weight)
-            covered += [(o0 + g * c.wstride, o0 + g * c.wstride + n) for g in range(c.G)]
-        chunks, pos = [], 0
-        for a, b in sorted(covered) + [(f.numel, f.numel)]:
-            lo = pad_to(pos, 4)  # a slot starts on a multiple of 4: [pos, lo) is a conv slot's zero padding
-            for q in range(lo, a, 1024):
-                chunks.append((q, min(1024, a - q)))
-            pos = max(pos, b)
-        bwd = Phase(self.bwd.name)
-        bwd.launches = list(ls)
-        bwd.launches[i] = Launch("wgrad_finalize", k_wgfin_adam, table, nd, nblocks, ad, owner=fin.owner,
-                                 stream=fin.stream, waits=fin.waits, record=fin.record, bucket=fin.bucket)
-        bwd.alias = dict(self.bwd.alias)
-        self._fused_chunks = torch.tensor(chunks, dtype=torch.int64).reshape(-1, 2).to(self.device)
-        opt = Phase("adam_rest")
-        opt.add("adam_pack", k_adam, dict(ad, chunks=P(self._fused_chunks), nchunk=len(chunks)))
-        return bwd, opt
 
     def set_optimizer(self, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, grad_scale: float = 1.0):
         self._opt_hparams = dict(b1=betas[0], b2=betas[1], eps=eps, wd=weight_decay, grad_scale=grad_scale)

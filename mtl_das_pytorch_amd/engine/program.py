@@ -187,10 +187,6 @@ def k_wgfin(table, nd, nblocks, st):
     lib().wgrad_finalize(table.data_ptr(), nd, nblocks, 1.0, st)
 
 
-def k_wgfin_adam(table, nd, nblocks, adam, st):
-    lib().wgrad_finalize(table.data_ptr(), nd, nblocks, 1.0, st, adam)
-
-
 def k_adam(d, st):
     lib().adam_pack(st, d)
 

@@ -19,8 +19,6 @@ a re-capture.
 """
 from __future__ import annotations
 
-import os
-
 from typing import Callable, Dict, List, Optional
 
 import torch
@@ -56,10 +54,6 @@ class StepRunner:
         self._packed = False
         self._bwd_pieces = None
         self.buckets = list(getattr(program, "buckets", None) or [(0, program.flat.numel)])
-        # single-GPU full steps fuse Adam into the weight-gradient finalize: the conv weights' gradients are
-        # then not stored in flat.grads (their other users run the unfused phases: DP pieces, train_compute)
-        self.fuse_optimizer = os.environ.get("MDA_FUSE_OPT", "1") == "1"
-        self._fused = None
 
     # -------------------------------------------------------------------------------------------
     def _mutable_state(self) -> List[torch.Tensor]:
@@ -91,11 +85,6 @@ class StepRunner:
         if kind == "train_opt":
             return [p.opt["adam"].run]
         if kind == "train_full":
-            if self._fused is None:  # finalize + Adam fused (LoweredProgram.fused_step_phases), built once
-                self._fused = (p.fused_step_phases() if self.fuse_optimizer else None) or False
-            if self._fused:
-                bwd, opt = self._fused
-                return [p.arena.clear, gather.run, p.fwd_train.run, bwd.run, opt.run]
             return [p.arena.clear, gather.run, p.fwd_train.run, p.bwd.run, p.opt["adam"].run]
         if kind == "eval":
             return [gather.run, p.fwd_eval.run]

@@ -243,39 +243,3 @@ def test_pack_images_match_layouts(model_name):
     assert n > 10
 
 
-
-
-@pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
-def test_fused_finalize_adam_matches_unfused(model_name):
-    """Single-GPU full steps with Adam fused into the weight-gradient finalize (LoweredProgram
-    .fused_step_phases) leave parameters, Adam moments, BN statistics and the step counter exactly as the
-    unfused finalize -> Adam pair does, over 3 captured steps with weight decay."""
-    from mtl_das_pytorch_amd.data.synthetic import generate
-    from mtl_das_pytorch_amd.engine.step import StepRunner
-    from mtl_das_pytorch_amd.engine.tune import autotune_program
-    from mtl_das_pytorch_amd.models import build_model, encode_joint
-    out = []
-    for fuse in (False, True):
-        torch.manual_seed(0)
-        m = build_model(model_name)
-        if model_name == "multi_classifier":
-            from mtl_das_pytorch_amd.engine.inception import InceptionProgram
-            prog = InceptionProgram(m, 8, "cuda", p_drop=0.0)
-        else:
-            from mtl_das_pytorch_amd.engine.mtl import MTLProgram
-            prog = MTLProgram(m, 8, "cuda")
-        prog.set_optimizer(weight_decay=1e-5)
-        autotune_program(prog, measure=False)
-        X, d, e = generate(16, seed=1, device="cuda")
-        lab = encode_joint(d, e) if model_name == "multi_classifier" else torch.stack([d, e], 1)
-        r = StepRunner(prog, X, lab, use_graph=True)
-        r.fuse_optimizer = fuse
-        r.set_lr(1e-3)
-        for i in range(3):
-            r.train_step(torch.arange(8, device="cuda") + 8 * (i % 2))
-        torch.cuda.synchronize()
-        assert bool(r._fused) == fuse
-        f = prog.flat
-        out.append([t.clone() for t in (f.params, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.step)])
-    for a, b in zip(*out):
-        assert torch.equal(a, b), (a - b).abs().max().item()

@@ -212,38 +212,3 @@ def test_guard_allocator_cpu_fallback():
     finally:
         guard.enable(False)
         guard.reset()
-
-
-@pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
-def test_fused_optimizer_partition(model_name):
-    """The single-GPU step's fused finalize + Adam (LoweredProgram.fused_step_phases) updates every parameter
-    element exactly once: conv weights in the finalize, everything else in 4-aligned chunks of <= 1024."""
-    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
-    from mtl_das_pytorch_amd.models import build_model
-    m = build_model(model_name)
-    p = InceptionProgram(m, 4, "cpu") if model_name == "multi_classifier" else MTLProgram(m, 4, "cpu")
-    p.set_optimizer(weight_decay=1e-5)
-    p.batch_wgrads()
-    bwd, opt = p.fused_step_phases()
-    fins = [l for l in bwd.launches if l.name == "wgrad_finalize"]
-    assert len(fins) == 1 and fins[0].args[3]["update"] == 1 and fins[0].args[3]["wd"] == 1e-5
-    assert [l.name for l in opt.launches] == ["adam_pack"] and opt.launches[0].args[0]["nchunk"] > 0
-    f = p.flat
-    mark = torch.zeros(f.numel, dtype=torch.int32)
-    for c in p.convs:
-        n, o0 = c.Co * c.Ci * c.KH * c.KW, f.off(c.mods[0].weight)
-        for g in range(c.G):
-            mark[o0 + g * c.wstride:o0 + g * c.wstride + n] += 1
-    for s, ln in p._fused_chunks.tolist():
-        assert s % 4 == 0 and ln % 4 == 0 and 0 < ln <= 1024
-        mark[s:s + ln] += 1
-    real = torch.zeros(f.numel, dtype=torch.bool)
-    for prm in p.model.parameters():
-        real[f.off(prm):f.off(prm) + prm.numel()] = True
-    assert int(mark.max()) == 1 and not ((mark == 0) & real).any()
-    # gradient buckets (data parallel) keep the unfused finalize: the all-reduce sits before Adam
-    m2 = build_model(model_name)
-    p2 = InceptionProgram(m2, 4, "cpu") if model_name == "multi_classifier" else MTLProgram(m2, 4, "cpu")
-    p2.segment_backward(2)
-    p2.batch_wgrads()
-    assert p2.fused_step_phases() is None
