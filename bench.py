@@ -176,15 +176,9 @@ def main():
     }
     if ctx.is_main:
         print(json.dumps(out), flush=True)
+    runner.close()  # graphs, streams and events released while the HIP runtime is alive
     shutdown(ctx)
 
 
 if __name__ == "__main__":
     main()
-    # the result line is out: leave without the interpreter's teardown, whose destruction order of HIP
-    # graphs / streams / the runtime crashed one tool run at exit (SIGSEGV after its last line).
-    # Under a profiler (rocprofv3 flushes its buffers from exit handlers) the normal exit is kept.
-    sys.stdout.flush()
-    sys.stderr.flush()
-    if os.environ.get("MDA_CLEAN_EXIT") != "1" and not any(k.startswith("ROCPROF") for k in os.environ):
-        os._exit(0)

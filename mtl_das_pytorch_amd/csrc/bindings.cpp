@@ -59,9 +59,12 @@ GradSrcs parse_grads(const py::list& l) {
   g.n = (int)l.size();
   for (int i = 0; i < g.n; ++i) {
     py::tuple t = l[i].cast<py::tuple>();
-    g.p[i] = reinterpret_cast<const float*>(static_cast<intptr_t>(t[0].cast<int64_t>()));
+    g.p[i] = reinterpret_cast<const bf16_t*>(static_cast<intptr_t>(t[0].cast<int64_t>()));
     g.gs[i] = t[1].cast<int64_t>();
     g.ld[i] = t[2].cast<int>();
+    // consumers read 8 channels (16 bytes) per load
+    if ((reinterpret_cast<uintptr_t>(g.p[i]) & 15) || g.ld[i] % 8 || g.gs[i] % 8)
+      throw std::runtime_error("gradient source: 16-byte aligned base, pitch and group stride (multiples of 8) required");
   }
   return g;
 }
@@ -147,10 +150,12 @@ ConvArgs parse_conv(int mode, py::dict d) {
     if (mode != MODE_DGRAD || l.size() > 3) throw std::runtime_error("conv: bad extra gradient sources");
     for (size_t i = 0; i < l.size(); ++i) {
       py::dict e = l[i].cast<py::dict>();
-      a.add[i] = P<const float>(e, "p");
+      a.add[i] = P<const bf16_t>(e, "p");
       a.addgs[i] = I(e, "gs");
       a.ldadd[i] = (int)I(e, "ld");
-      if (!a.add[i] || a.ldadd[i] % 4 || a.ldadd[i] < a.N) throw std::runtime_error("conv: bad extra gradient source");
+      // the epilogue reads 4 channels (8 bytes) per load
+      if (!a.add[i] || a.ldadd[i] % 4 || a.ldadd[i] < a.N || (reinterpret_cast<uintptr_t>(a.add[i]) & 7) || a.addgs[i] % 4)
+        throw std::runtime_error("conv: bad extra gradient source");
     }
     a.nadd = (int)l.size();
   }
@@ -235,8 +240,8 @@ TailArgs parse_tail(const py::dict& d) {
   a.B = (int)I(d, "B"); a.H = (int)I(d, "H"); a.W = (int)I(d, "W"); a.C = (int)I(d, "C");
   if (d.contains("g")) a.g = parse_grads(d["g"].cast<py::list>());
   a.part = P<double>(d, "part"); a.chunk_px = (int)I(d, "chunk_px");
-  a.dzbuf = P<float>(d, "dzbuf"); a.dzgs = I(d, "dzgs"); a.lddz = (int)I(d, "lddz");
-  a.side = P<float>(d, "side"); a.sgs = I(d, "sgs"); a.lds = (int)I(d, "lds");
+  a.dzbuf = P<bf16_t>(d, "dzbuf"); a.dzgs = I(d, "dzgs"); a.lddz = (int)I(d, "lddz");
+  a.side = P<bf16_t>(d, "side"); a.sgs = I(d, "sgs"); a.lds = (int)I(d, "lds");
   a.dy = P<bf16_t>(d, "dy"); a.dgs = I(d, "dgs"); a.ldd = (int)I(d, "ldd");
   a.dy2 = P<bf16_t>(d, "dy2"); a.d2gs = I(d, "d2gs"); a.ldd2 = (int)I(d, "ldd2");
   a.dgamma = P<float>(d, "dgamma"); a.dbeta = P<float>(d, "dbeta");
@@ -263,7 +268,7 @@ void mtl_head(int64_t stream, py::dict d) {
   py::list ncls = d["ncls"].cast<py::list>(), w = d["w"].cast<py::list>();
   if (a.T > 4 || (int)ncls.size() != a.T || (int)w.size() != a.T) throw std::runtime_error("mtl_head: bad task list");
   for (int t = 0; t < a.T; ++t) { a.ncls[t] = ncls[t].cast<int>(); a.w[t] = w[t].cast<float>(); if (a.ncls[t] > 16) throw std::runtime_error("ncls > 16"); }
-  a.logp = P<float>(d, "logp"); a.dfeat = P<float>(d, "dfeat"); a.dgs = I(d, "dgs");
+  a.logp = P<float>(d, "logp"); a.dfeat = P<bf16_t>(d, "dfeat"); a.dgs = I(d, "dgs");
   a.metrics = P<float>(d, "metrics"); a.confusion = P<int>(d, "confusion");
   a.nvalid = P<const int64_t>(d, "nvalid");
   check(launch_mtl_head(a, S(stream)), "mtl_head");
@@ -278,7 +283,7 @@ void cls_head(int64_t stream, py::dict d) {
   a.p_drop = (float)F(d, "p_drop");
   a.seed = P<const int64_t>(d, "seed");
   a.feat = P<float>(d, "feat"); a.logits = P<float>(d, "logits"); a.dlogits = P<float>(d, "dlogits");
-  a.dx = P<float>(d, "dx"); a.metrics = P<float>(d, "metrics"); a.confusion = P<int>(d, "confusion");
+  a.dx = P<bf16_t>(d, "dx"); a.metrics = P<float>(d, "metrics"); a.confusion = P<int>(d, "confusion");
   a.dW = P<float>(d, "dW"); a.db = P<float>(d, "db");
   a.nvalid = P<const int64_t>(d, "nvalid");
   check(launch_cls_head(a, P<int64_t>(d, "seed"), S(stream)), "cls_head");
@@ -298,9 +303,9 @@ void pool3(int is_max, int backward, int64_t stream, py::dict d) {
   if (d.contains("g")) {
     // a list of (ptr, group stride, pitch) sources, or one pointer with pitch "ldg"
     if (py::isinstance<py::list>(d["g"])) a.g = parse_grads(d["g"].cast<py::list>());
-    else { a.g.n = 1; a.g.p[0] = P<const float>(d, "g"); a.g.ld[0] = (int)I(d, "ldg"); }
+    else { a.g.n = 1; a.g.p[0] = P<const bf16_t>(d, "g"); a.g.ld[0] = (int)I(d, "ldg"); }
   }
-  a.dx = P<float>(d, "dx"); a.lddx = (int)I(d, "lddx");
+  a.dx = P<bf16_t>(d, "dx"); a.lddx = (int)I(d, "lddx");
   a.B = (int)I(d, "B"); a.H = (int)I(d, "H"); a.W = (int)I(d, "W"); a.C = (int)I(d, "C");
   a.Ho = (int)I(d, "Ho"); a.Wo = (int)I(d, "Wo");
   a.am = P<uint8_t>(d, "am");
@@ -319,7 +324,7 @@ void synth_das(int64_t stream, py::dict d) {
 }
 
 void grad_sum(py::list g, int64_t out, int ldo, int64_t M, int C, int64_t stream) {
-  check(launch_grad_sum(parse_grads(g), reinterpret_cast<float*>(out), ldo, M, C, S(stream)), "grad_sum");
+  check(launch_grad_sum(parse_grads(g), reinterpret_cast<bf16_t*>(out), ldo, M, C, S(stream)), "grad_sum");
 }
 
 void adam_pack(int64_t stream, py::dict d) {

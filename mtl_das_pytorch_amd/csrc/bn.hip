@@ -13,10 +13,10 @@
 // num_batches_tracked, matching nn.BatchNorm2d in train mode.
 //
 // Backward is two launches per fused op: `reduce` recomputes dz (the gradient w.r.t. the BN output)
-// from the saved bf16 y and the upstream fp32 gradients, and accumulates sum(dz), sum(dz * xhat);
+// from the saved bf16 y and the upstream bf16 gradients (summed in fp32), and accumulates sum(dz), sum(dz * xhat);
 // `apply` recomputes dz and writes dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)) as the bf16
 // operand of the conv dgrad/wgrad, and block 0 stores d(gamma), d(beta) into the flat gradient buffer.
-// Side outputs (written once, fp32): SIGMUL -> g*sigmoid (gradient of the shared feature F),
+// Side outputs (written once, bf16): SIGMUL -> g*sigmoid (gradient of the shared feature F),
 // ADD_RELU with identity shortcut -> dz (gradient of the block input through the shortcut).
 #include "kernels.h"
 
@@ -268,8 +268,8 @@ DEV void compute_dz(const TailArgs& a, const BwdCtx& X, int z, int p, int c, flo
 // order immaterial after rounding, as for the forward statistics) and the apply sums the NREP replicas of
 // its channels.  Per-block cross-lane reductions are strided DPP
 // row shifts (lanes of the same channel group are CGB apart), finished in LDS over the block's 16 rows.
-// Optionally the reduce stores dz (fp32) so the apply does not re-read multi-source gradients or
-// re-evaluate 2x2 pool windows.
+// Optionally the reduce stores dz (bf16; the statistics are then accumulated from the rounded value the
+// apply will read) so the apply does not re-read multi-source gradients or re-evaluate 2x2 pool windows.
 constexpr int BNB_T = 256;
 
 // channel groups of 8 per block: whole rows for C <= 64 (C/8 must be divisible), 64-channel slices above
@@ -325,10 +325,14 @@ DEV void bnb_reduce_impl(const TailArgs& a) {
   float sdz[8], sdx[8], sdx2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { sdz[j] = 0.f; sdx[j] = 0.f; sdx2[j] = 0.f; }
-  float* dzz = a.dzbuf ? a.dzbuf + a.dzgs * z : nullptr;
+  bf16_t* dzz = a.dzbuf ? a.dzbuf + a.dzgs * z : nullptr;
   for (int p = p0 + pl; p < p1; p += PL) {
     float dz[8], xh[8], xh2[8], side[8];
     compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
+    if (dzz) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dz[j] = rbf(dz[j]);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       sdz[j] += dz[j];
@@ -336,8 +340,8 @@ DEV void bnb_reduce_impl(const TailArgs& a) {
       if (two) sdx2[j] += dz[j] * xh2[j];
     }
     if ((KIND == SIGMUL || KIND == ADD_RELU) && a.side)
-      store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
-    if (dzz) store8f(dzz + (int64_t)p * a.lddz + c, dz);
+      store8(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
+    if (dzz) store8(dzz + (int64_t)p * a.lddz + c, dz);
   }
   const int lane = threadIdx.x & 63, row = threadIdx.x >> 4;
   const bool top = (lane & 15) >= 16 - CGB;
@@ -415,16 +419,16 @@ DEV void bnb_apply_impl(const TailArgs& a) {
   const int M = a.B * a.H * a.W;
   const int p0 = chunk * a.chunk_px, p1 = min(M, p0 + a.chunk_px);
   const bf16_t* yz = a.y + a.ygs * z;
-  const float* dzz = a.dzbuf ? a.dzbuf + a.dzgs * z : nullptr;
+  const bf16_t* dzz = a.dzbuf ? a.dzbuf + a.dzgs * z : nullptr;
   for (int p = p0 + pl; p < p1; p += PL) {
     float dz[8], y[8], o[8];
     if (dzz) {
-      load8f(dzz + (int64_t)p * a.lddz + c, dz);
+      load8(dzz + (int64_t)p * a.lddz + c, dz);
     } else {
       float xh[8], xh2[8], side[8];
       compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
       if ((KIND == SIGMUL || KIND == ADD_RELU) && a.side && a.apply_side)
-        store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
+        store8(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
     }
     load8(yz + (int64_t)p * a.ldy + c, y);
 #pragma unroll
@@ -507,7 +511,7 @@ __global__ __launch_bounds__(FUSED_T) void tail_bwd_fused_kernel(TailArgs a) {
     if (p < M) {
       compute_dz<KIND>(a, X, z, p, c, dzc[r], xhc[r], xh2c[r], side);
       if ((KIND == SIGMUL || KIND == ADD_RELU) && a.side)
-        store8f(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
+        store8(a.side + a.sgs * z + (int64_t)p * a.lds + c, side);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {

@@ -4,8 +4,9 @@
 //   * activations are NHWC, addressed as rows of pixels with a row pitch `ld` (elements), so a
 //     channel slice of a concatenation buffer is just (base + channel_offset, ld = total_channels);
 //   * MFMA operands are bf16, accumulation and every reduction is fp32;
-//   * gradient buffers of activations are fp32 and written exactly once (no read-modify-write);
-//     a consumer that needs the sum of several gradient sources takes a GradSrcs list;
+//   * gradient buffers of activations are bf16 (as under autocast) and written exactly once (no
+//     read-modify-write): every producer accumulates in fp32 and rounds once at its store, a consumer that
+//     needs the sum of several gradient sources takes a GradSrcs list and sums them in fp32;
 //   * per-channel BN statistics are accumulated into NREP replicas (blockIdx % NREP) to spread
 //     atomic contention over the 8 XCD L2s; consumers sum the replicas;
 //   * wave size is 64; blocks are 256 threads (4 waves).
@@ -129,9 +130,9 @@ struct Src2 {
   int C0, C1;
 };
 
-// Up to 6 fp32 gradient sources summed on load (deterministic gradient accumulation).
+// Up to 6 bf16 gradient sources summed on load in fp32 (deterministic gradient accumulation).
 struct GradSrcs {
-  const float* p[6];
+  const bf16_t* p[6];
   int64_t gs[6];
   int ld[6];
   int n;
@@ -142,10 +143,27 @@ DEV void gsum8(const GradSrcs& g, int z, int64_t pix, int c, float* v) {
   for (int j = 0; j < 8; ++j) v[j] = 0.f;
   for (int s = 0; s < g.n; ++s) {
     float t[8];
-    load8f(g.p[s] + g.gs[s] * z + pix * g.ld[s] + c, t);
+    load8(g.p[s] + g.gs[s] * z + pix * g.ld[s] + c, t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] += t[j];
   }
+}
+
+// fp32 -> bf16 -> fp32 (the value a bf16 gradient store keeps): statistics that a later pass recomputes from
+// the stored gradient are accumulated from this rounded value, so both passes see the same numbers
+DEV float rbf(float f) { return bf2f(f2bf(f)); }
+
+// 4 consecutive bf16 values (8 bytes) <-> fp32
+DEV void store4(bf16_t* p, const float* v) {
+  uint2 w;
+  w.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  w.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = w;
+}
+DEV void load4(const bf16_t* p, float* v) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
 }
 
 // Per-BN-layer state. Everything is indexed by group z with the given strides (0 = shared).

@@ -10,7 +10,7 @@
 //                    into the producing conv.
 //  conv_igemm<DGRAD> dx[m, n] = sum_k Wt[n, k] * gather(dy)[k, m]      m = (b, ih, iw), n = cin,
 //                    k = (kh, kw, cout); strided convs gather only the taps with (ih+p-kh) % s == 0.
-//                    fp32 output (gradient buffers are fp32 and written exactly once).
+//                    bf16 output, rounded once from the fp32 accumulator (plus any extra gradient sources).
 //  conv_wgrad        dW[n, k] = sum_m dy[m, n] * im2col(x)[m, k]; both operands are staged in LDS
 //                    pixel-major (natural NHWC rows, 16-B writes) and read as MFMA operands with the
 //                    gfx950 transpose read ds_read_b64_tr_b16.  Split over m; fp32 partial slabs are
@@ -327,9 +327,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) { s[r] += v[r]; ss[r] += v[r] * v[r]; }
           } else {
-            float* o = reinterpret_cast<float*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
+            bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + a.ogs * z + (int64_t)m * a.ldo + n0;
             add_sources(a, z, (int64_t)m, n0, v);
-            *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+            store4(o, v);
             if (want_bnb && n0 < bN) {  // dz of the BN tail this gradient feeds, and its statistics
               const uint2 u = ypre[i][f], q = rpre[i][f];
               const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float t = yv[r] * s_bn[cl + r] + s_bn[BN_T + cl + r];
-                float dz = v[r], xh2 = 0.f;
+                float dz = rbf(v[r]), xh2 = 0.f;  // the stored gradient: the apply pass recomputes dz from it
                 if (a.bkind == ACT_RELU) {
                   dz = t > 0.f ? dz : 0.f;
                 } else if (a.bkind == ACT_SIGMOID) {

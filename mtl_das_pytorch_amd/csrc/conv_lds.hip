@@ -32,7 +32,7 @@
 //
 // Modes: MODE_FWD, MODE_FWD_NOL (normalise-on-load of the input), MODE_DGRAD, MODE_DGRAD_BNS (fused
 // BN-backward statistics in the epilogue); the epilogues match conv.hip's (bias, bf16 store, fp64
-// replica BN sums / fp32 gradient store, dz statistics).
+// replica BN sums / bf16 gradient store, dz statistics).
 #include "kernels.h"
 
 namespace mda {
@@ -60,7 +60,7 @@ struct TileCtx {
 };
 
 // Epilogue stores of one output tile (lane: pixel l16 of each fragment, channels 4*kgl .. +3): bias + bf16
-// store (forward) / extra gradient sources + fp32 store (data gradient), and this lane's share of the BN
+// store (forward) / extra gradient sources + bf16 store (data gradient), and this lane's share of the BN
 // statistics accumulated into st[i][stat][r] (summed over the tiles of a persistent block before the flush).
 template <bool FWD, bool BNS, int BN, int WM, int WN, int FN, int FM>
 DEV void tile_store(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f32x4 (&acc)[FN][FM], const float* s_k,
@@ -101,9 +101,9 @@ DEV void tile_store(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f32x
 #pragma unroll
         for (int r = 0; r < 4; ++r) { st[i][0][r] += v[r]; st[i][1][r] += v[r] * v[r]; }
       } else {
-        float* o = reinterpret_cast<float*>(a.out) + a.ogs * t.z + (int64_t)orow[f] * a.ldo + n0;
+        bf16_t* o = reinterpret_cast<bf16_t*>(a.out) + a.ogs * t.z + (int64_t)orow[f] * a.ldo + n0;
         add_sources(a, t.z, (int64_t)orow[f], n0, v);
-        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        store4(o, v);
         if (BNS && n0 < t.bN) {  // dz of the BN tail this gradient feeds, and its statistics
           const uint2 u = *reinterpret_cast<const uint2*>(a.by + a.bygs * t.z + (int64_t)orow[f] * a.ldby + n0);
           const float yv[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
@@ -115,7 +115,7 @@ DEV void tile_store(const ConvArgs& a, const LdsPlan& pl, const TileCtx& t, f32x
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float tv = yv[r] * s_k[cl + r] + s_k[BN + cl + r];
-            float dz = v[r], xh2 = 0.f;
+            float dz = rbf(v[r]), xh2 = 0.f;  // the stored gradient: the apply pass recomputes dz from it
             if (a.bkind == ACT_RELU) {
               dz = tv > 0.f ? dz : 0.f;
             } else if (a.bkind == ACT_SIGMOID) {

@@ -93,13 +93,13 @@ __global__ __launch_bounds__(256) void mtl_head_kernel(HeadArgs a) {
     __syncthreads();
     if (a.dfeat) {
       // d loss_t / d feat[p][c] = w_t * (p_j - y_j) / B / gsz / HW for channel c in group j
-      float* d = a.dfeat + a.dgs * t + (int64_t)b * a.HW * a.C;
+      bf16_t* d = a.dfeat + a.dgs * t + (int64_t)b * a.HW * a.C;
       const float scale = a.w[t] / ((float)a.B * gsz * a.HW);
-      const int n4 = a.HW * a.C / 4;  // 16-byte stores; a group of 4 channels shares its class (gsz % 4 == 0)
+      const int n4 = a.HW * a.C / 4;  // 8-byte bf16 stores; a group of 4 channels shares its class (gsz % 4 == 0)
       for (int i = threadIdx.x; i < n4; i += 256) {
         const int ch = (i * 4) % a.C;
-        const float v = s_prob[ch / gsz] * scale;
-        reinterpret_cast<float4*>(d)[i] = make_float4(v, v, v, v);
+        const uint32_t h = (uint32_t)f2bf(s_prob[ch / gsz] * scale);
+        reinterpret_cast<uint2*>(d)[i] = make_uint2(h | (h << 16), h | (h << 16));
       }
     }
   }
@@ -244,8 +244,8 @@ __global__ __launch_bounds__(CLS_T) void cls_head_kernel(ClsArgs a) {
     } else {
       for (int n = 0; n < a.N; ++n) acc += s_dl[n] * a.W[(int64_t)n * a.C + c];
     }
-    acc *= msk[i] / (float)a.HW;
-    for (int p = 0; p < a.HW; ++p) a.dx[((int64_t)b * a.HW + p) * a.C + c] = acc;
+    const bf16_t h = f2bf(acc * (msk[i] / (float)a.HW));
+    for (int p = 0; p < a.HW; ++p) a.dx[((int64_t)b * a.HW + p) * a.C + c] = h;
   }
 }
 

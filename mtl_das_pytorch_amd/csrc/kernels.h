@@ -15,7 +15,7 @@ struct ConvArgs {
   int64_t wgs;
   const float* bias;  // FWD only, may be null
   int64_t bgs;
-  void* out;  // FWD: bf16, DGRAD: fp32; [M][ldo] (+ z * ogs)
+  void* out;  // bf16 [M][ldo] (+ z * ogs): FWD the pre-BN y, DGRAD the data gradient
   int64_t ogs;
   int ldo;
   double* stats;  // FWD: [G][NREP][2][N] fp64 (may be null); replica blockIdx.x % stats_nrep
@@ -49,10 +49,11 @@ struct ConvArgs {
   // group updates that BN's running statistics and publishes its constants (BNArgs::consts).
   BNArgs nbn;
   int nol, nol_kind;
-  // DGRAD only, optional (nadd = 0 off): up to 3 more fp32 gradient sources of the same [M][N] tensor
-  // ([M][ldadd] + z * addgs) added in the epilogue, so the output is the WHOLE gradient of the BN tail it
-  // feeds (one source: its statistics can then be fused above, and the tail runs apply-only)
-  const float* add[3];
+  // DGRAD only, optional (nadd = 0 off): up to 3 more bf16 gradient sources of the same [M][N] tensor
+  // ([M][ldadd] + z * addgs) added (in fp32, before the one rounding) in the epilogue, so the output is the
+  // WHOLE gradient of the BN tail it feeds (one source: its statistics can then be fused above, and the
+  // tail runs apply-only)
+  const bf16_t* add[3];
   int64_t addgs[3];
   int ldadd[3];
   int nadd;
@@ -69,8 +70,9 @@ DEV void add_sources(const ConvArgs& a, int z, int64_t m, int n0, float* v) {
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
     if (s < a.nadd) {
-      const float4 q = *reinterpret_cast<const float4*>(a.add[s] + a.addgs[s] * z + m * a.ldadd[s] + n0);
-      v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+      float q[4];
+      load4(a.add[s] + a.addgs[s] * z + m * a.ldadd[s] + n0, q);
+      v[0] += q[0]; v[1] += q[1]; v[2] += q[2]; v[3] += q[3];
     }
   }
 }
@@ -154,10 +156,10 @@ struct TailArgs {
   bf16_t* out; int64_t ogs; int ldo;
   int B, H, W, C;
   // backward only
-  GradSrcs g;                       // upstream fp32 gradient(s) on the tail's output grid
+  GradSrcs g;                       // upstream bf16 gradient(s) on the tail's output grid
   double* part; int chunk_px;       // [G][NREP][3][C] fp64 replica sums (zeroed per step); pixels per chunk
-  float* dzbuf; int64_t dzgs; int lddz;  // optional dz store (reduce) / load (apply), fp32
-  float* side; int64_t sgs; int lds;
+  bf16_t* dzbuf; int64_t dzgs; int lddz;  // optional dz store (reduce) / load (apply), bf16
+  bf16_t* side; int64_t sgs; int lds;     // side gradient output (bf16)
   bf16_t* dy; int64_t dgs; int ldd;
   bf16_t* dy2; int64_t d2gs; int ldd2;
   float* dgamma; float* dbeta; float* dgamma2; float* dbeta2; int64_t pgs;
@@ -175,7 +177,7 @@ struct HeadArgs {
   int ncls[4];
   float w[4];
   float* logp;      // [T][B][16]
-  float* dfeat;     // [T][B*HW][C] fp32 (+ t * dgs), may be null (eval)
+  bf16_t* dfeat;    // [T][B*HW][C] bf16 (+ t * dgs), may be null (eval)
   int64_t dgs;
   float* metrics;   // [T][4]: loss_sum, correct, count, abs_err_sum
   int* confusion;   // [T][16][16]
@@ -192,7 +194,7 @@ struct ClsArgs {
   float* feat;                   // [B][C] post-dropout features (fp32)
   float* logits;                 // [B][N]
   float* dlogits;                // [B][N] (training)
-  float* dx;                     // [B*HW][C] fp32 grad (training), may be null
+  bf16_t* dx;                    // [B*HW][C] bf16 grad (training), may be null
   float* metrics;                // [3][4]: joint, distance, event -> loss, correct, count, abs_err
   int* confusion;                // [2][16][16]: distance, event
   float* dW; float* db;          // flat-grad slots (cls_wgrad)
@@ -203,8 +205,8 @@ struct ClsArgs {
 struct PoolArgs {
   const bf16_t* x; int ldx;     // input [B*H*W][C] (bf16)
   bf16_t* y; int ldy;           // output [B*Ho*Wo][C]
-  GradSrcs g;                   // backward: grad of output = sum of fp32 sources (concat consumers)
-  float* dx; int lddx;          // backward: grad of input (fp32)
+  GradSrcs g;                   // backward: grad of output = sum of bf16 sources (concat consumers)
+  bf16_t* dx; int lddx;         // backward: grad of input (bf16)
   int B, H, W, C, Ho, Wo;
   uint8_t* am;                  // optional max-pool argmax (window position 0..8) [B*Ho*Wo][C]: written by
                                 // the training forward, read by the backward instead of re-reading the windows
@@ -284,7 +286,7 @@ struct SynthArgs {
 int launch_synth_das(const SynthArgs& a, int n, hipStream_t st);
 int launch_philox_kat(const uint32_t* ctr, uint64_t key, uint32_t* out, int n, hipStream_t st);
 int launch_tick(uint64_t* buf, int i, hipStream_t st);
-int launch_grad_sum(const GradSrcs& g, float* out, int ldo, int64_t M, int C, hipStream_t st);
+int launch_grad_sum(const GradSrcs& g, bf16_t* out, int ldo, int64_t M, int C, hipStream_t st);
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st);
 
 }  // namespace mda

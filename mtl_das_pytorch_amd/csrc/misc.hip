@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void pool3_fwd_kernel(PoolArgs a) {
 }
 
 // Gradient of the input: sum over the output windows covering an input pixel (<= 4 for the stride-2 max
-// pool, <= 9 for the average pool) and over the fp32 gradient sources; per source, every window's loads are
+// pool, <= 9 for the average pool) and over the bf16 gradient sources; per source, every window's loads are
 // issued before any is consumed.  MAX = 1: max pool, the argmax stored by the training forward routes the
 // gradient (a.am); MAX = 2: max pool without it (eval-mode programs, the functional API without `am`), each window is re-read to find its
 // maximum (a separate instantiation: sharing one kernel spilled the argmax path to scratch); MAX = 0: average.
@@ -149,26 +149,22 @@ __global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {
         w[t] = ok[t] ? *reinterpret_cast<const uint2*>(a.am + (int64_t)q[t] * a.C + cg * 8) : make_uint2(0, 0);
       }
       for (int sidx = 0; sidx < a.g.n; ++sidx) {
-        const float* gp = a.g.p[sidx];
+        const bf16_t* gp = a.g.p[sidx];
         const int ld = a.g.ld[sidx];
-        float4 g0[4], g1[4];
+        uint4 gu[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const float* src = gp + (int64_t)q[t] * ld + cg * 8;
-          g0[t] = ok[t] ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
-          g1[t] = ok[t] ? *reinterpret_cast<const float4*>(src + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const bf16_t* src = gp + (int64_t)q[t] * ld + cg * 8;
+          gu[t] = ok[t] ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {  // (a window outside the range has w = 0 and g = 0: adds nothing)
           const uint32_t m = (uint32_t)me[t];
-          acc[0] += ((w[t].x & 255u) == m) ? g0[t].x : 0.f;
-          acc[1] += (((w[t].x >> 8) & 255u) == m) ? g0[t].y : 0.f;
-          acc[2] += (((w[t].x >> 16) & 255u) == m) ? g0[t].z : 0.f;
-          acc[3] += ((w[t].x >> 24) == m) ? g0[t].w : 0.f;
-          acc[4] += ((w[t].y & 255u) == m) ? g1[t].x : 0.f;
-          acc[5] += (((w[t].y >> 8) & 255u) == m) ? g1[t].y : 0.f;
-          acc[6] += (((w[t].y >> 16) & 255u) == m) ? g1[t].z : 0.f;
-          acc[7] += ((w[t].y >> 24) == m) ? g1[t].w : 0.f;
+          float gv[8];
+          unpack8(gu[t], gv);
+          const uint32_t wb[2] = {w[t].x, w[t].y};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += (((wb[j >> 2] >> (8 * (j & 3))) & 255u) == m) ? gv[j] : 0.f;
         }
       }
     } else if (MAX == 2) {
@@ -198,27 +194,28 @@ __global__ __launch_bounds__(256) void pool3_bwd_kernel(PoolArgs a) {
     } else {
       // average pool, stride 1, padding 1: the output windows oh in [ih-1, ih+1], ow in [iw-1, iw+1]
       for (int sidx = 0; sidx < a.g.n; ++sidx) {
-        const float* gp = a.g.p[sidx];
+        const bf16_t* gp = a.g.p[sidx];
         const int ld = a.g.ld[sidx];
-        float4 g0[9], g1[9];
+        uint4 gu[9];
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
           const int oh = ih - 1 + t / 3, ow = iw - 1 + t % 3;
           const bool ok = oh >= 0 && oh < a.Ho && ow >= 0 && ow < a.Wo;
-          const float* src = gp + (int64_t)((b * a.Ho + oh) * a.Wo + ow) * ld + cg * 8;
-          g0[t] = ok ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
-          g1[t] = ok ? *reinterpret_cast<const float4*>(src + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const bf16_t* src = gp + (int64_t)((b * a.Ho + oh) * a.Wo + ow) * ld + cg * 8;
+          gu[t] = ok ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
-          acc[0] += g0[t].x; acc[1] += g0[t].y; acc[2] += g0[t].z; acc[3] += g0[t].w;
-          acc[4] += g1[t].x; acc[5] += g1[t].y; acc[6] += g1[t].z; acc[7] += g1[t].w;
+          float gv[8];
+          unpack8(gu[t], gv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += gv[j];
         }
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
     }
-    store8f(a.dx + (int64_t)p * a.lddx + cg * 8, acc);
+    store8(a.dx + (int64_t)p * a.lddx + cg * 8, acc);
   }
 }
 
@@ -246,19 +243,19 @@ int launch_tick(uint64_t* buf, int i, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// sum of up to 6 fp32 gradient sources into one buffer (used where a consumer is not a fused tail)
-__global__ __launch_bounds__(256) void grad_sum_kernel(GradSrcs g, float* out, int ldo, int64_t M, int C) {
+// sum of up to 6 bf16 gradient sources into one buffer (used where a consumer is not a fused tail)
+__global__ __launch_bounds__(256) void grad_sum_kernel(GradSrcs g, bf16_t* out, int ldo, int64_t M, int C) {
   const int CG = C >> 3;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < M * CG; i += (int64_t)gridDim.x * 256) {
     const int64_t p = i / CG;
     const int c = (int)(i - p * CG) * 8;
     float v[8];
     gsum8(g, 0, p, c, v);
-    store8f(out + p * ldo + c, v);
+    store8(out + p * ldo + c, v);
   }
 }
 
-int launch_grad_sum(const GradSrcs& g, float* out, int ldo, int64_t M, int C, hipStream_t st) {
+int launch_grad_sum(const GradSrcs& g, bf16_t* out, int ldo, int64_t M, int C, hipStream_t st) {
   const int64_t n = M * (C / 8);
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(grad_sum_kernel, dim3(blocks), dim3(256), 0, st, g, out, ldo, M, C);

@@ -28,6 +28,10 @@ from ..ops.hip import lib, ptr
 from . import guard
 
 NREP = 32  # must match csrc/common.h
+# storage type of every activation gradient (data gradients, gradient sources, BN-tail side outputs and dz
+# buffers): bf16 as under autocast -- producers accumulate in fp32 and round once at the store, consumers sum
+# their sources in fp32 (csrc/common.h); half the bytes of the fp32 gradients every backward kernel moved
+GRAD_DT = torch.bfloat16
 BN_PX_PER_REP = 256  # forward BN-statistic replicas: about one per this many pixels
 
 

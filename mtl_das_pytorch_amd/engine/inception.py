@@ -7,7 +7,7 @@ outputs straight into channel slices of the block's output buffer (the tail / po
 concat width), and the next block's convs read that buffer in place.
 
 Backward walks the ops in reverse.  Each consumer of a value writes the gradient w.r.t. its input ONCE
-into its own fp32 buffer and registers it as a *gradient source* of the value; the producing kernel
+into its own bf16 buffer and registers it as a *gradient source* of the value; the producing kernel
 (the BN-tail backward, or the pool backward) sums the sources on load.  A branch output that lives in a
 slice of a concat buffer gets the matching channel slices of the concat value's sources, so the
 concat backward is free as well.  The classifier (GAP -> Dropout -> Linear -> CE) is the fused
@@ -25,13 +25,13 @@ import torch
 from ..models.multi_classifier import (BasicConv2d, InceptionA, InceptionB, InceptionC, InceptionD, InceptionE,
                                        Multi_Classifier)
 from . import guard
-from .core import Act, Arena, BNLayer, ConvLayer, FlatState, P, grads_of, new_act, src_dict, stem_pack_geom
+from .core import GRAD_DT, Act, Arena, BNLayer, ConvLayer, FlatState, P, grads_of, new_act, src_dict, stem_pack_geom
 from .lowering import ACT_RELU, LoweredProgram
 from .program import Phase, k_cls_head, k_pool, k_wgfin
 
 
 class Val:
-    """A bf16 activation of the lowered graph and the fp32 gradient sources its consumers register.
+    """A bf16 activation of the lowered graph and the bf16 gradient sources its consumers register.
     ``parent``/``coff``: this value is channels [coff, coff+C) of a concat value."""
 
     def __init__(self, act: Act, parent: "Val" = None, coff: int = 0, needs_grad: bool = True):
@@ -64,7 +64,7 @@ class CBR:
         self.bn = BNLayer([bc.bn], f, A, B * c.Ho * c.Wo)
         self.y = new_act(A, 1, B, c.Ho, c.Wo, c.Co)
         self.dy = new_act(A, 1, B, c.Ho, c.Wo, c.Co)
-        self.dx = new_act(A, 1, B, s.H, s.W, s.C, torch.float32) if src.needs_grad else None
+        self.dx = new_act(A, 1, B, s.H, s.W, s.C, GRAD_DT) if src.needs_grad else None
         self.nol_from: Optional["CBR"] = None  # producer whose BN+ReLU this conv applies on load
         self.skip_tail = False                 # the (single) consumer normalises self.y on load
 
@@ -96,7 +96,7 @@ class Pool:
         Ho, Wo = ((s.H - 3) // 2 + 1, (s.W - 3) // 2 + 1) if is_max else (s.H, s.W)
         if (Ho, Wo, s.C) != (out.act.H, out.act.W, out.act.C):
             raise ValueError("pool output shape mismatch")
-        self.dx = new_act(prog.arena, 1, prog.B, s.H, s.W, s.C, torch.float32) if src.needs_grad else None
+        self.dx = new_act(prog.arena, 1, prog.B, s.H, s.W, s.C, GRAD_DT) if src.needs_grad else None
         # max pool: the training forward stores each output's window argmax (1 byte) for the backward
         self.am = None
         if is_max and self.dx is not None:
@@ -295,7 +295,7 @@ class InceptionProgram(LoweredProgram):
             raise ValueError("feature width does not match fc")
         self.HWf = a.H * a.W
         N = m.num_classes
-        self.dfeat = new_act(A, 1, B, a.H, a.W, a.C, torch.float32)
+        self.dfeat = new_act(A, 1, B, a.H, a.W, a.C, GRAD_DT)
         v.grads.append(self.dfeat)
         self.fc_feat = A.empty((B, a.C), torch.float32)
         self.logp = guard.alloc((B, N), torch.float32, self.device, zero=True, label="logits")  # of the last batch

@@ -9,8 +9,8 @@ import torch
 
 from ..ops.functional import WGRAD_PATCH, WGRAD_TILES
 from ..ops.hip import lib
-from .core import Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, pad_to
-from .program import (Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad,
+from .core import GRAD_DT, Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, pad_to
+from .program import (COMM_STREAM, Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad,
                       k_wgrad_batched)
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
@@ -92,7 +92,7 @@ class LoweredProgram:
             # the apply pass reads the stored dz instead of re-reading several gradient sources /
             # re-evaluating the pool window
             if bn.dzbuf is None:
-                bn.dzbuf = self.arena.empty((G, y.M, y.C), torch.float32)
+                bn.dzbuf = self.arena.empty((G, y.M, y.C), GRAD_DT)
             d.update({"dzbuf": P(bn.dzbuf), "dzgs": y.M * y.C if G > 1 else 0, "lddz": y.C})
         d.update(bn.grad_ptrs())
         if r is not None:
@@ -239,6 +239,10 @@ class LoweredProgram:
         if not self.FOLD_SOURCES or os.environ.get("MDA_FOLD", "1") != "1":
             return 0
         ls = self.bwd.launches
+        recorded_at = {}  # event tag -> index of the launch that records it
+        for i, l in enumerate(ls):
+            if l.record is not None:
+                recorded_at[l.record] = i
         last_dgrad = {}  # stream -> (index, launch) of its latest dgrad
         for i, l in enumerate(ls):
             if l.name == "conv_dgrad":
@@ -257,6 +261,11 @@ class LoweredProgram:
             mine = [q for q, (p, gs, ld) in enumerate(g) if p == pd["out"] and gs == pd["ogs"] and ld == pd["ldo"]]
             if (len(mine) != 1 or PG != G or pd.get("add") or pd["N"] != d["C"]
                     or (pd["Ho"], pd["Wo"]) != (d["H"], d["W"]) or pd["B"] != d["B"]):
+                continue
+            # the tail's waits move onto the earlier dgrad: each awaited event must be recorded before it in
+            # launch order (else Phase.run would meet the wait before the record -- or a reused tag would
+            # make the dgrad wait on a stale event and race the added sources)
+            if any(recorded_at.get(self.bwd.alias.get(w, w), len(ls)) >= j for w in l.waits):
                 continue
             pd["add"] = [{"p": p, "gs": gs, "ld": ld} for q, (p, gs, ld) in enumerate(g) if q != mine[0]]
             d["g"] = [g[mine[0]]]
@@ -427,6 +436,38 @@ class LoweredProgram:
         self.bwd.launches = new
         self.buckets = buckets
         return buckets
+
+    def backward_with_allreduce(self, allreduce) -> Phase:
+        """The backward with every gradient bucket's all-reduce embedded in it, so the whole
+        data-parallel step -- forward, backward, collectives, optimizer -- is one HIP graph.  Each bucket's
+        finalize (segment_backward: one per bucket, at the end of its piece) records an event, and an
+        ``allreduce(grads[lo:hi])`` launch on the communication stream waits for it: bucket k's collective
+        overlaps pieces k+1.. of the backward, and the optimizer, the next phase, waits for every collective
+        through the phase-end join of the communication stream.  ``allreduce`` must be stream-ordered
+        (DistContext.all_reduce_ordered_; captured on RCCL)."""
+        f = self.flat
+        buckets = getattr(self, "buckets", None) or [(0, f.numel)]
+        ph = Phase("backward_dp")
+        ph.alias = dict(self.bwd.alias)
+        n = 0
+        for l in self.bwd.launches:
+            if l.name == "cut":
+                continue
+            if l.name != "wgrad_finalize":
+                ph.launches.append(l)
+                continue
+            if l.record is not None:
+                raise ValueError("a gradient bucket's finalize already records an event")
+            tag = f"bucket{l.bucket}_grads"
+            ph.launches.append(Launch(l.name, l.fn, *l.args, owner=l.owner, stream=l.stream, waits=l.waits,
+                                      record=tag, bucket=l.bucket))
+            lo, hi = buckets[l.bucket]
+            ph.launches.append(Launch("allreduce_grads", k_allreduce, allreduce, f.grads[lo:hi], stream=COMM_STREAM,
+                                      waits=(tag,), bucket=l.bucket))
+            n += 1
+        if n != len(buckets):
+            raise ValueError(f"{n} finalize launches for {len(buckets)} gradient buckets")
+        return ph
 
     WGRAD_MAX_BATCHES = 3
 

@@ -28,7 +28,7 @@ import torch
 from ..models.mtl import MTLNet
 from ..ops.hip import lib
 from . import guard
-from .core import NREP, Act, Arena, BNLayer, ConvLayer, FlatState, P, new_act, src_dict, stem_pack_geom
+from .core import GRAD_DT, NREP, Act, Arena, BNLayer, ConvLayer, FlatState, P, new_act, src_dict, stem_pack_geom
 from .lowering import ACT_NONE, ACT_RELU, ACT_SIGMOID, ADD_RELU, POOL_RELU, SIGMUL, LoweredProgram
 from .program import Phase, k_head, k_wgfin
 
@@ -114,15 +114,15 @@ class MTLProgram(LoweredProgram):
                 L["bns"] = BNLayer([rb.shortcut[1]], f, A, B * Ho * Wo)
                 L["ys"] = new_act(A, 1, B, Ho, Wo, C)
                 L["dys"] = new_act(A, 1, B, Ho, Wo, C)
-                L["dxs"] = new_act(A, 1, B, prev.H, prev.W, prev.C, torch.float32)
+                L["dxs"] = new_act(A, 1, B, prev.H, prev.W, prev.C, GRAD_DT)
             else:
-                L["side"] = new_act(A, 1, B, Ho, Wo, C, torch.float32)
+                L["side"] = new_act(A, 1, B, Ho, Wo, C, GRAD_DT)
             L["in"] = prev
             L["ya"], L["ha"], L["yb"] = (new_act(A, 1, B, Ho, Wo, C) for _ in range(3))
             L["out"] = new_act(A, 1, B, Ho, Wo, C)
             L["dyb"], L["dya"] = new_act(A, 1, B, Ho, Wo, C), new_act(A, 1, B, Ho, Wo, C)
-            L["dha"] = new_act(A, 1, B, Ho, Wo, C, torch.float32)
-            L["dxa"] = new_act(A, 1, B, prev.H, prev.W, prev.C, torch.float32)
+            L["dha"] = new_act(A, 1, B, Ho, Wo, C, GRAD_DT)
+            L["dxa"] = new_act(A, 1, B, prev.H, prev.W, prev.C, GRAD_DT)
             self.rbs.append(L)
             prev = L["out"]
         self.F = [L["out"] for L in self.rbs]  # F1..F8 (index 0..7)
@@ -145,23 +145,23 @@ class MTLProgram(LoweredProgram):
             L["ym1"], L["hm"] = new_act(A, T, B, H, W, cm), new_act(A, T, B, H, W, cm)
             L["ym2"], L["Aout"] = new_act(A, T, B, H, W, C), new_act(A, T, B, H, W, C)
             L["dym2"] = new_act(A, T, B, H, W, C)
-            L["dF"] = new_act(A, T, B, H, W, C, torch.float32)   # side: gradient of F_{2l} per task
-            L["dhm"] = new_act(A, T, B, H, W, cm, torch.float32)
+            L["dF"] = new_act(A, T, B, H, W, C, GRAD_DT)   # side: gradient of F_{2l} per task
+            L["dhm"] = new_act(A, T, B, H, W, cm, GRAD_DT)
             L["dym1"] = new_act(A, T, B, H, W, cm)
-            L["dcat"] = new_act(A, T, B, H, W, cin, torch.float32)
+            L["dcat"] = new_act(A, T, B, H, W, cin, GRAD_DT)
             if lvl < 3:
                 o = outs[lvl]
                 L["co"] = ConvLayer([o[t][0] for t in range(T)], f, A, B, H, W)
                 L["bno"] = BNLayer([o[t][1] for t in range(T)], f, A, B * H * W)
                 Co = L["co"].Co
                 L["yo"], L["dyo"] = new_act(A, T, B, H, W, Co), new_act(A, T, B, H, W, Co)
-                L["dA"] = new_act(A, T, B, H, W, C, torch.float32)
+                L["dA"] = new_act(A, T, B, H, W, C, GRAD_DT)
                 Hp, Wp = (H + 1) // 2, (W + 1) // 2
                 L["Bp"] = new_act(A, T, B, Hp, Wp, Co)
                 prevB = L["Bp"]
             self.levels.append(L)
         L4 = self.levels[3]
-        self.dA4 = new_act(A, T, B, L4["H"], L4["W"], L4["C"], torch.float32)
+        self.dA4 = new_act(A, T, B, L4["H"], L4["W"], L4["C"], GRAD_DT)
         self.levels[3]["dA"] = self.dA4
         # head outputs / metrics (NOT in the per-step zeroed region: they accumulate across steps)
         self.logp = guard.alloc((T, B, 16), torch.float32, self.device, zero=True, label="logp")

@@ -26,6 +26,9 @@ from ..ops.hip import lib, stream
 MULTI_STREAM = os.environ.get("MDA_STREAMS", "1") == "1"
 # streams used at most (ids above are folded onto the last one -- still a valid schedule)
 MAX_STREAMS = 4
+# logical id of the communication stream: data-parallel gradient all-reduces embedded in the backward
+# (LoweredProgram.backward_with_allreduce) run there, beside the compute streams, never folded onto them
+COMM_STREAM = 7
 
 
 class Launch:
@@ -96,9 +99,9 @@ class Phase:
             return
         main = torch.cuda.current_stream()
         if self._streams is None or self._streams[0].device != main.device:
-            self._streams = [torch.cuda.Stream(device=main.device) for _ in range(3)]
-        streams = [main] + self._streams
-        sid_of = lambda l: min(l.stream, MAX_STREAMS - 1)
+            self._streams = [torch.cuda.Stream(device=main.device) for _ in range(MAX_STREAMS)]
+        streams = [main] + self._streams  # [MAX_STREAMS] is the communication stream
+        sid_of = lambda l: MAX_STREAMS if l.stream == COMM_STREAM else min(l.stream, MAX_STREAMS - 1)
         used = {sid_of(l) for l in self.launches}
         start = main.record_event()
         for sid in used - {0}:

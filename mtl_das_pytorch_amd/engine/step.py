@@ -6,12 +6,14 @@ A training step is
     gradient buckets)  ->  [fused Adam + bf16 re-pack] [step++]
 
 Single GPU: the whole step is ONE captured HIP graph (``torch.cuda.CUDAGraph`` is a hipGraph on ROCm),
-so a step costs one graph launch from the host.  Data parallel: RCCL runs eagerly between graphs -- no
-reliance on collective capture.  With one bucket the compute graph is followed by one all-reduce and the
-optimizer graph.  With several (LoweredProgram.segment_backward) the backward is captured as one graph
-per bucket piece; after replaying piece k the host issues bucket k's all-reduce asynchronously (RCCL's
-stream waits for piece k) and replays piece k+1, which then runs concurrently with the collective; the
-optimizer graph waits for every bucket.
+so a step costs one graph launch from the host.  Data parallel with capturable collectives (RCCL, see
+DistContext.capturable_collectives): still ONE graph -- the gradient buckets' all-reduces are captured
+on a communication stream inside it (LoweredProgram.backward_with_allreduce), each waiting only for its
+bucket's finalize.  Otherwise RCCL runs eagerly between graphs: with one bucket the compute graph is
+followed by one all-reduce and the optimizer graph; with several (LoweredProgram.segment_backward) the
+backward is captured as one graph per bucket piece; after replaying piece k the host issues bucket k's
+all-reduce asynchronously (RCCL's stream waits for piece k) and replays piece k+1, which then runs
+concurrently with the collective; the optimizer graph waits for every bucket.
 
 The batch indices live in a persistent device buffer that the host refreshes (device-to-device copy)
 before each replay; the learning rate is a device scalar, so the reference's LR schedule never forces
@@ -53,6 +55,9 @@ class StepRunner:
         self.graphs: Dict[str, torch.cuda.CUDAGraph] = {}
         self._packed = False
         self._bwd_pieces = None
+        self._bwd_dp = None
+        # the DP step as one graph with the bucket collectives captured in it (FlatGradAllReducer.capturable)
+        self.capture_dp = self.use_graph and allreduce is not None and getattr(allreduce, "capturable", False)
         self.buckets = list(getattr(program, "buckets", None) or [(0, program.flat.numel)])
 
     # -------------------------------------------------------------------------------------------
@@ -86,6 +91,10 @@ class StepRunner:
             return [p.opt["adam"].run]
         if kind == "train_full":
             return [p.arena.clear, gather.run, p.fwd_train.run, p.bwd.run, p.opt["adam"].run]
+        if kind == "train_full_dp":
+            if self._bwd_dp is None:
+                self._bwd_dp = p.backward_with_allreduce(self.allreduce.ordered)
+            return [p.arena.clear, gather.run, p.fwd_train.run, self._bwd_dp.run, p.opt["adam"].run]
         if kind == "eval":
             return [gather.run, p.fwd_eval.run]
         raise ValueError(kind)
@@ -114,15 +123,9 @@ class StepRunner:
             snap.restore()
             self.p.opt["pack"].run()  # the bf16 weight images are derived state: rebuild from restored masters
             g = torch.cuda.CUDAGraph()
-            # RCCL's process-group watchdog thread polls the events of pending collectives: an eager (warm-up)
-            # collective still on its list while the capture joins the communicator's stream fails that poll
-            # ("event last recorded in a capturing stream") and the watchdog aborts the process.  All of them
-            # completed at the synchronize above; give the watchdog (100 ms poll) time to retire them, and
-            # capture thread-locally so its polls of other events are legal during the capture.
-            import torch.distributed as dist
-            if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-                import time
-                time.sleep(0.5)
+            # Collectives captured here run on the capture-only RCCL communicator (DistContext.capture_group),
+            # which never has eager work for the process-group watchdog to poll; the capture is thread-local
+            # so that the watchdog's polls of the default communicator's eager work stay legal meanwhile.
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 for f in fns:
                     f()
@@ -139,6 +142,8 @@ class StepRunner:
         self.idx.copy_(idx, non_blocking=True)
         if self.allreduce is None:
             self._run("train_full")
+        elif self.capture_dp:
+            self._run("train_full_dp")
         elif len(self.buckets) == 1:
             self._run("train_compute")
             self.allreduce(self.p.flat.grads)
@@ -175,3 +180,22 @@ class StepRunner:
     def reset_metrics(self):
         self.p.metrics.zero_()
         self.p.confusion.zero_()
+
+    def close(self):
+        """Release every HIP object the runner and its program's phases hold -- graph executables, the phases'
+        side streams and recorded events -- while the HIP runtime is certainly alive (at interpreter exit the
+        order in which module globals, the runtime and these objects are finalised is not defined).  The
+        runner can be used again afterwards (graphs are re-captured on demand)."""
+        torch.cuda.synchronize()
+        for g in self.graphs.values():
+            g.reset()
+        self.graphs.clear()
+        p = self.p
+        phases = [p.fwd_train, p.fwd_eval, p.bwd] + list(p.opt.values()) + list(self._bwd_pieces or [])
+        if self._bwd_dp is not None:
+            phases.append(self._bwd_dp)
+        for ph in phases:
+            ph._live_events = None
+            ph._streams = None
+        self._bwd_pieces = self._bwd_dp = None
+        torch.cuda.synchronize()

@@ -22,6 +22,13 @@ def _pad(x, m):
     return (x + m - 1) // m * m
 
 
+def _grad(g: torch.Tensor) -> torch.Tensor:
+    """An activation gradient as the kernels read it: contiguous bf16 (csrc/common.h GradSrcs)."""
+    if not g.is_cuda:
+        raise RuntimeError("HIP ops need a GPU tensor")
+    return g.to(torch.bfloat16).contiguous()
+
+
 def _check(t: torch.Tensor, dtype=None):
     if not t.is_cuda:
         raise RuntimeError("HIP ops need a GPU tensor")
@@ -195,7 +202,7 @@ def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg
     ph, pw = (padding, padding) if isinstance(padding, int) else padding
     wd = pack_weight_dgrad(w.float(), Cs)
     from ..engine import guard
-    dx = guard.alloc((B, H, W, Cs), torch.float32, dy.device, label=f"dgrad out cfg {cfg}")
+    dx = guard.alloc((B, H, W, Cs), torch.bfloat16, dy.device, label=f"dgrad out cfg {cfg}")
     d = {"src": {"p0": ptr(dy), "ld0": Co, "C0": Co, "C1": 0}, "w": ptr(wd), "out": ptr(dx), "ldo": Cs,
          "B": B, "Hs": Ho, "Ws": Wo, "Ho": H, "Wo": W, "N": Cs, "Npad": wd.shape[0], "Cs": Co, "KH": KH, "KW": KW,
          "sh": sh, "sw": sw, "ph": ph, "pw": pw, "Kpad": wd.shape[1]}
@@ -212,7 +219,7 @@ def prepare_conv2d_dgrad(dy, w, in_hw, stride=1, padding=0, cin_stored=None, cfg
 
 def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw: Tuple[int, int], stride=1, padding=0,
                  cin_stored: Optional[int] = None, cfg: Optional[int] = None, bn_stats=None):
-    """Gradient w.r.t. the NHWC input: fp32 ``[B, H, W, Cin_stored]``."""
+    """Gradient w.r.t. the NHWC input: bf16 ``[B, H, W, Cin_stored]`` (fp32 accumulation, one rounding)."""
     return prepare_conv2d_dgrad(dy, w, in_hw, stride, padding, cin_stored, cfg, bn_stats).run()
 
 
@@ -360,7 +367,8 @@ def bnb_plan(M: int, C: int, G: int = 1, target_blocks: int = 1024):
 def bn_tail_backward(kind: int, y: torch.Tensor, bn: dict, grads: Sequence[torch.Tensor], dgamma, dbeta,
                      r: Optional[torch.Tensor] = None, bn2: Optional[dict] = None, dgamma2=None, dbeta2=None,
                      fused: bool = False, store_dz: bool = False, part: Optional[torch.Tensor] = None):
-    """Returns ``(dy bf16, side fp32 | None, dy2 bf16 | None)``; writes dgamma/dbeta (and 2) in place.
+    """Returns ``(dy bf16, side bf16 | None, dy2 bf16 | None)``; writes dgamma/dbeta (and 2) in place.
+    ``grads``: the upstream gradient sources (bf16, as the engine stores them; other dtypes are rounded);
     ``fused``: single-launch variant (block per 8 channels over all pixels) instead of reduce + apply;
     ``store_dz``: the reduce stores dz and the apply reads it instead of recomputing it;
     ``part``: the statistics were already accumulated (by a dgrad with ``bn_stats``): apply pass only."""
@@ -372,18 +380,19 @@ def bn_tail_backward(kind: int, y: torch.Tensor, bn: dict, grads: Sequence[torch
     else:
         part = torch.zeros(NREP, 3, C, device=y.device, dtype=torch.float64)
     dy = torch.empty_like(y)
+    grads = [_grad(g) for g in grads]
     d = {"y": ptr(y), "ldy": C, "bn": bn, "B": B, "H": H, "W": W, "C": C,
          "g": [(ptr(g), 0, g.shape[-1]) for g in grads], "part": ptr(part), "chunk_px": chunk_px,
          "dy": ptr(dy), "ldd": C, "dgamma": ptr(dgamma), "dbeta": ptr(dbeta), "fused": mode}
     dzbuf = None
     if store_dz:
-        dzbuf = torch.empty(B, H, W, C, device=y.device)
+        dzbuf = torch.empty(B, H, W, C, device=y.device, dtype=torch.bfloat16)
         d.update({"dzbuf": ptr(dzbuf), "lddz": C})
     side = dy2 = None
     if r is not None:
         d.update({"r": ptr(r), "ldr": r.shape[-1]})
     if kind in (SIGMUL,) or (kind == ADD_RELU and bn2 is None):
-        side = torch.empty(B, H, W, C, device=y.device, dtype=torch.float32)
+        side = torch.empty(B, H, W, C, device=y.device, dtype=torch.bfloat16)
         d.update({"side": ptr(side), "lds": C})
     if bn2 is not None:
         dy2 = torch.empty_like(y)
@@ -409,9 +418,11 @@ def pool3(x: torch.Tensor, is_max: bool, am: Optional[torch.Tensor] = None):
 
 
 def pool3_backward(x: torch.Tensor, g: torch.Tensor, is_max: bool, am: Optional[torch.Tensor] = None):
+    """Input gradient (bf16) of :func:`pool3` from the output gradient ``g`` (bf16; other dtypes are rounded)."""
     B, H, W, C = x.shape
     _, Ho, Wo, _ = g.shape
-    dx = torch.empty(B, H, W, C, device=x.device, dtype=torch.float32)
+    g = _grad(g)
+    dx = torch.empty(B, H, W, C, device=x.device, dtype=torch.bfloat16)
     d = {"x": ptr(x), "ldx": C, "g": ptr(g), "ldg": C, "dx": ptr(dx), "lddx": C, "B": B, "H": H, "W": W, "C": C,
          "Ho": Ho, "Wo": Wo}
     if am is not None:  # the kernel reads the argmax with 8-byte loads per 8-channel group

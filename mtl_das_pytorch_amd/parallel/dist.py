@@ -34,6 +34,13 @@ class DistContext:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: Optional[str] = None
+    # RCCL: a second communicator that runs ONLY collectives captured into HIP graphs.  PyTorch's
+    # process-group watchdog thread polls the completion events of every eager collective it still lists;
+    # on ROCm that poll fails once the communicator's stream has joined a graph capture ("event last
+    # recorded in a capturing stream") and the watchdog aborts the process.  Captured collectives are never
+    # listed, so a communicator that never runs an eager collective never has anything to poll: capture is
+    # safe by construction, with no dependence on the watchdog's timing.
+    capture_group: object = None
 
     @property
     def enabled(self) -> bool:
@@ -44,8 +51,10 @@ class DistContext:
     @property
     def capturable_collectives(self) -> bool:
         """Collectives can be captured into a HIP graph (RCCL: stream-ordered device collectives); gloo's
-        host round trip cannot, so a step with in-step collectives (SyncBN) then runs eagerly."""
-        return self.backend == "nccl"
+        host round trip cannot, so a step with in-step collectives (SyncBN) then runs eagerly.  With more
+        than one rank the captured form is opt-in (``MDA_CAPTURE_COLLECTIVES=1``): it has been validated on
+        one-rank RCCL groups only, and the eager form is the known-good default there."""
+        return self.capture_group is not None
 
     @property
     def is_main(self) -> bool:
@@ -70,7 +79,11 @@ class DistContext:
         CPU all-reduce runs, and the copy back is queued on the stream."""
         if not self.enabled:
             return t
-        if self.backend == "nccl" or t.device.type != "cuda":
+        if self.backend == "nccl":
+            # under capture: the capture-only communicator (see ``capture_group``)
+            dist.all_reduce(t, group=self.capture_group if torch.cuda.is_current_stream_capturing() else None)
+            return t
+        if t.device.type != "cuda":
             dist.all_reduce(t)
             return t
         c = t.cpu()
@@ -123,7 +136,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[int] = N
             if backend == "nccl":
                 kw["device_id"] = device
             dist.init_process_group(**kw)
-        return DistContext(0, 1, 0, device, backend)
+        return _with_capture_group(DistContext(0, 1, 0, device, backend))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     backend = backend or ("nccl" if use_gpu else "gloo")
@@ -136,7 +149,17 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[int] = N
         if backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
-    return DistContext(rank, world, local_rank, device, backend)
+    return _with_capture_group(DistContext(rank, world, local_rank, device, backend))
+
+
+def _with_capture_group(ctx: DistContext) -> DistContext:
+    """Create the capture-only RCCL communicator (DistContext.capture_group) where captured collectives are
+    used: one-rank groups always, several ranks with MDA_CAPTURE_COLLECTIVES=1.  Every rank makes the same
+    call (new_group is collective); the default group is bound to the device, so the new communicator is
+    initialised eagerly here -- never lazily inside a capture."""
+    if ctx.backend == "nccl" and (ctx.world == 1 or os.environ.get("MDA_CAPTURE_COLLECTIVES") == "1"):
+        ctx.capture_group = dist.new_group(backend="nccl")
+    return ctx
 
 
 def shutdown(ctx: DistContext):
@@ -152,6 +175,10 @@ class FlatGradAllReducer:
         self.ctx = ctx
         self.bucket_elems = int(bucket_mb * 2 ** 20 / 4) if bucket_mb > 0 else 0
         self._pending = []
+        # the bucket all-reduces may be embedded in the step's HIP graph (engine/step.py "train_full_dp"):
+        # ``ordered`` is then the stream-ordered form the captured launches call
+        self.capturable = ctx.capturable_collectives and os.environ.get("MDA_DP_CAPTURE", "1") == "1"
+        self.ordered = ctx.all_reduce_ordered_
 
     def start(self, t: torch.Tensor):
         """Issue an asynchronous all-reduce(SUM) of one gradient bucket (a contiguous view of the flat

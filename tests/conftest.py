@@ -41,15 +41,15 @@ def _no_miopen_references():
     torch.backends.cudnn.enabled = prev
 
 
-@pytest.fixture(autouse=True, scope="session")
+@pytest.fixture(autouse=True)
 def _guard_bands_intact():
-    """With MDA_GUARD=1 every engine buffer the session allocated sits between canary bands
-    (engine/guard.py); at the end of the session none of them may have been written."""
+    """With MDA_GUARD=1 every engine buffer sits between canary bands (engine/guard.py); after each test none
+    of the live ones may have been written (the registry holds weak references: buffers a test's programs
+    freed drop out, so a full-suite guard run does not accumulate device memory)."""
     yield
     from mtl_das_pytorch_amd.engine import guard
     if guard.enabled() and guard.count():
         import torch
         torch.cuda.synchronize()
         bad = guard.check()
-        print(f"guard: {guard.count()} guarded buffers checked, {len(bad)} with a written band")
         assert not bad, bad

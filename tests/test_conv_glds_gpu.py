@@ -76,7 +76,9 @@ def test_glds_dgrad_fused_bn_stats(kind):
             cfg = fn.glds_cfg(tile, splits, deep)
             dx = fn.conv2d_dgrad(go, w, (H, W), stride=1, padding=1, cfg=cfg, bn_stats=(yb, bn, part, kind))
             dx_ref = fn.conv2d_dgrad(go, w, (H, W), stride=1, padding=1)
-            assert rel(dx, dx_ref) < 1e-5, (tile, splits)
+            # bf16 outputs of two fp32 accumulation orders: an element whose sums straddle a rounding boundary
+            # differs by one bf16 ulp (~4e-3 relative), a few 1e-5 of them
+            assert rel(dx, dx_ref) < 2e-4, (tile, splits)
             dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
             fn.bn_tail_backward(kind, yb, bn, [dx_ref], dg, db)
             got = part.sum(0)

@@ -151,7 +151,7 @@ def test_patch_dgrad_fused_bn_stats(kind, Co):
             continue
         dx = call.run()
         ran += 1
-        assert rel(dx, dx_ref) < 1e-5, cfg
+        assert rel(dx, dx_ref) < 2e-4, cfg  # bf16 outputs of two accumulation orders (one-ulp flips)
         got = part.sum(0)
         assert rel(got[0], db.double()) < 1e-4 and rel(got[1], dg.double()) < 1e-4, cfg
     assert ran >= (5 if Co == 48 else 15)  # dy channels 48: 16-channel slices only; 32: persistent forms too

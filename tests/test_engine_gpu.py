@@ -60,7 +60,7 @@ def _ref_grads(m, x, labels, idx, cols):
 def test_engine_train_step_matches_autograd(which):
     """The engine's gradients are compared with fp32 autograd on the SAME bf16-rounded weights.  The
     reference network at random init is ill-conditioned (0.1% weight noise moves early-layer gradients
-    by ~15-20%, see tools/dbg_engine.py), so the bound for each tensor is derived from the reference's
+    by ~15-20%, measured with a launch-by-launch comparison), so the bound for each tensor is derived from the reference's
     own sensitivity to a bf16-sized (4e-3) weight perturbation; well-conditioned tensors (head, level 4) are held
     to a tight absolute bound."""
     from mtl_das_pytorch_amd.models import MTL_Net, Single_Task_Net

@@ -212,3 +212,30 @@ def test_guard_allocator_cpu_fallback():
     finally:
         guard.enable(False)
         guard.reset()
+
+
+@pytest.mark.parametrize("nb", [1, 2])
+def test_backward_with_allreduce_structure(nb):
+    """Data-parallel step as one graph (engine/step.py train_full_dp): every gradient bucket's finalize records
+    an event and one all-reduce of exactly that bucket's flat range waits for it on the communication stream;
+    the buckets cover the flat buffer once, and the program's own backward is left untouched."""
+    from mtl_das_pytorch_amd.engine.program import COMM_STREAM
+    p = MTLProgram(MTL_Net(), 32, "cpu")
+    buckets = p.segment_backward(nb)
+    assert len(buckets) == nb
+    before = [(l.name, l.record) for l in p.bwd.launches]
+    seen = []
+    ph = p.backward_with_allreduce(lambda t: seen.append(t))
+    assert [(l.name, l.record) for l in p.bwd.launches] == before
+    fins = [l for l in ph.launches if l.name == "wgrad_finalize"]
+    ars = [l for l in ph.launches if l.name == "allreduce_grads"]
+    assert len(fins) == len(ars) == nb and not any(l.name == "cut" for l in ph.launches)
+    covered = 0
+    for f, a in zip(fins, ars):
+        assert a.stream == COMM_STREAM and a.waits == (f.record,)
+        lo, hi = buckets[f.bucket]
+        t = a.args[1]
+        assert t.data_ptr() == p.flat.grads[lo:hi].data_ptr() and t.numel() == hi - lo
+        covered += t.numel()
+        assert ph.launches.index(a) > ph.launches.index(f)
+    assert covered == p.flat.numel

@@ -82,7 +82,7 @@ def test_inception_train_step_matches_autograd(monkeypatch):
     """Engine vs fp32 autograd on the same bf16 weights, with the reference rounding activations where
     the engine stores them in bf16 (Inception-v3 at random init amplifies a 1.7e-3 per-layer rounding
     difference to ~20% at the logits, so an un-emulated reference says nothing about correctness; every
-    layer individually is exact to bf16 rounding -- tools/dbg_inception.py).  Gradient bound per tensor
+    layer individually is exact to bf16 rounding -- test_inception_backward_layer_local).  Gradient bound per tensor
     as in the Model A test: 1.5x the reference's own sensitivity to bf16-sized weight noise + 0.05."""
     model, ref, prog, X, labels = _setup()
     _emulate_bf16_storage(ref, monkeypatch)

@@ -47,3 +47,16 @@ def test_training_step_is_bitwise_deterministic(model_type, use_graph):
         prog, lab = MTLProgram(m, 16, "cuda"), torch.stack([d, e], 1)
     res = check_step(prog, X, lab, torch.arange(16, device="cuda"), use_graph=use_graph, runs=3)
     assert res["bitwise_equal"], res
+
+
+def test_race_bisection_finds_nothing_on_a_deterministic_step():
+    """The launch-level race bisection (engine/determinism.py first_divergent_launch) runs the step launch by
+    launch twice and compares every written buffer bitwise: the engine's step has no divergent launch."""
+    from mtl_das_pytorch_amd.data.synthetic import generate
+    from mtl_das_pytorch_amd.engine.determinism import first_divergent_launch
+    from mtl_das_pytorch_amd.engine.mtl import MTLProgram
+    from mtl_das_pytorch_amd.models import build_model
+    torch.manual_seed(0)
+    prog = MTLProgram(build_model("MTL"), 16, "cuda")
+    X, d, e = generate(16, seed=3, device="cuda")
+    assert first_divergent_launch(prog, X, torch.stack([d, e], 1), torch.arange(16, device="cuda")) is None

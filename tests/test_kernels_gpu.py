@@ -362,10 +362,11 @@ def test_inception_pools(fn, is_max):
     ref = F.max_pool2d(x, 3, 2) if is_max else F.avg_pool2d(x, 3, 1, 1)
     y = fn.pool3(nhwc(x.detach()).bfloat16(), is_max)
     assert rel(nchw(y), ref) < 6e-3
-    go = torch.randn_like(ref)
+    go = torch.randn_like(ref).bfloat16().float()  # gradients are stored bf16
     ref.backward(go)
     dx = fn.pool3_backward(nhwc(x.detach()).bfloat16(), nhwc(go), is_max)
-    assert rel(nchw(dx), x.grad) < 1e-5
+    assert dx.dtype == torch.bfloat16
+    assert rel(nchw(dx), x.grad) < 4e-3  # fp32 sum of the bf16 window gradients, one bf16 rounding
     if is_max:  # argmax stored by the forward: identical gradient (same first-max tie rule), windows not re-read
         am = torch.full((y.numel(),), 255, dtype=torch.uint8, device="cuda")
         y2 = fn.pool3(nhwc(x.detach()).bfloat16(), is_max, am=am)
@@ -378,7 +379,7 @@ def test_inception_pools(fn, is_max):
         fn.pool3(nhwc(xt.detach()).bfloat16(), is_max, am=am)
         dx2 = fn.pool3_backward(nhwc(xt.detach()).bfloat16(), nhwc(go), is_max, am=am)
         assert torch.equal(dx2, fn.pool3_backward(nhwc(xt.detach()).bfloat16(), nhwc(go), is_max))
-        assert rel(nchw(dx2), xt.grad) < 1e-5
+        assert rel(nchw(dx2), xt.grad) < 4e-3
         # NaN propagates like torch: the output is NaN and the gradient goes to the NaN's position
         xn = x.detach().clone()
         xn[0, 3, 4, 5] = float("nan")
@@ -388,7 +389,7 @@ def test_inception_pools(fn, is_max):
         yn = nchw(fn.pool3(nhwc(xn.detach()).bfloat16(), is_max, am=am))
         assert torch.equal(torch.isnan(yn), torch.isnan(rn))
         dxn = nchw(fn.pool3_backward(nhwc(xn.detach()).bfloat16(), nhwc(go), is_max, am=am))
-        assert rel(dxn, xn.grad) < 1e-5
+        assert rel(dxn, xn.grad) < 4e-3
         with pytest.raises(ValueError):  # the argmax buffer is validated before the kernel reads it
             fn.pool3_backward(nhwc(x.detach()).bfloat16(), nhwc(go), is_max, am=am[:-8])
 
@@ -410,7 +411,7 @@ def test_mtl_head(fn):
     feat = torch.randn(T, B, C, H, W, generator=g).bfloat16().float().cuda()
     labels = torch.stack([torch.randint(0, 16, (B,)), torch.randint(0, 2, (B,))], 1).cuda()
     logp = torch.zeros(T, B, 16, device="cuda")
-    dfeat = torch.zeros(T, B * H * W, C, device="cuda")
+    dfeat = torch.zeros(T, B * H * W, C, device="cuda", dtype=torch.bfloat16)
     metrics = torch.zeros(T, 4, device="cuda")
     conf = torch.zeros(T, 16, 16, device="cuda", dtype=torch.int32)
     fb = torch.stack([nhwc(feat[t]) for t in range(T)]).bfloat16().contiguous()
@@ -432,4 +433,4 @@ def test_mtl_head(fn):
         assert conf[t].sum().item() == B
     loss.backward()
     ref = torch.stack([nhwc(fr.grad[t]).reshape(B * H * W, C) for t in range(T)])
-    assert rel(dfeat, ref) < 1e-4
+    assert rel(dfeat, ref) < 4e-3  # bf16 gradient storage

@@ -22,8 +22,12 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-# measured worst (MI355X, B = 32): dy 1.7e-3 (bf16 output), dW 3.9e-5, dx 3.3e-7, dgamma 5.5e-7, side 3.2e-8
-TOL = {"dy": 6e-3, "dx": 1e-5, "dW": 2e-4, "dgamma": 1e-5, "dbeta": 1e-5, "side": 1e-6, "dhead": 1e-6}
+# Every activation gradient the engine stores is bf16 (one rounding of an fp32 accumulation, as under
+# autocast), so dy / dx / side / dhead are compared at the bf16 output rounding: a relative L2 error of one
+# rounding of N(0,1)-like data is 2^-9 / sqrt(3) ~ 1.1e-3; 6e-3 leaves the margin of the fp32 references'
+# accumulation order.  dW / dgamma / dbeta are fp32 sums over the engine's own bf16 operands (tight).
+# measured worst (MI355X, B = 32, fp32 gradient storage of round 3): dy 1.7e-3, dW 3.9e-5, dgamma 5.5e-7
+TOL = {"dy": 6e-3, "dx": 6e-3, "dW": 2e-4, "dgamma": 1e-5, "dbeta": 1e-5, "side": 6e-3, "dhead": 6e-3}
 
 
 def rel(a, b):

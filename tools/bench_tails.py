@@ -60,7 +60,7 @@ def main():
         gam, bet = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
         rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
         nbt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        g = torch.randn(M, C, device="cuda")
+        g = torch.randn(M, C, device="cuda", dtype=torch.bfloat16)
         dy = torch.empty_like(y)
         from mtl_das_pytorch_amd.ops.functional import bnb_plan
         nchunk, chunk_px = bnb_plan(M, C)
@@ -110,7 +110,7 @@ def phases():
         stats = torch.rand(NREP, 2, C, device="cuda", dtype=torch.float64) * 10
         gam, bet = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
         rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
-        g = torch.randn(M, C, device="cuda")
+        g = torch.randn(M, C, device="cuda", dtype=torch.bfloat16)
         dy, dy2 = torch.empty_like(y), torch.empty_like(y)
         dgam, dbet = torch.zeros(2, C, device="cuda"), torch.zeros(2, C, device="cuda")
         tsc = torch.zeros(8, dtype=torch.int64, device="cuda")
