@@ -86,6 +86,8 @@ BNArgs parse_bn(const py::dict& d) {
   b.consts = P<float>(d, "consts");
   b.nrep = (int)I(d, "nrep", NREP);
   b.pnrep = (int)I(d, "pnrep", NREP);
+  b.sld = (int)I(d, "sld", b.C);
+  if (b.sld < b.C) throw std::runtime_error("bn: stats pitch below the channel count");
   if (b.pnrep < 1 || b.pnrep > NREP || (b.pnrep & (b.pnrep - 1))) throw std::runtime_error("bn: pnrep must be a power of two <= NREP");
   if (b.nrep < 1 || b.nrep > NREP || (b.nrep & (b.nrep - 1))) throw std::runtime_error("bn: nrep must be a power of two <= NREP");
   return b;

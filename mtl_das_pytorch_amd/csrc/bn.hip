@@ -268,8 +268,10 @@ DEV void compute_dz(const TailArgs& a, const BwdCtx& X, int z, int p, int c, flo
 // order immaterial after rounding, as for the forward statistics) and the apply sums the NREP replicas of
 // its channels.  Per-block cross-lane reductions are strided DPP
 // row shifts (lanes of the same channel group are CGB apart), finished in LDS over the block's 16 rows.
-// Optionally the reduce stores dz (bf16; the statistics are then accumulated from the rounded value the
-// apply will read) so the apply does not re-read multi-source gradients or re-evaluate 2x2 pool windows.
+// Optionally the reduce stores dz (bf16) so the apply does not re-read multi-source gradients or re-evaluate
+// 2x2 pool windows.  The statistics are accumulated from the unrounded fp32 dz, as autocast's fp32 BN
+// backward computes them (sum(dz * xhat) is a cancelling sum: rounding dz first costs ~1e-3 in d(gamma));
+// only the apply's dz operand carries the bf16 rounding, on a bf16 output.
 constexpr int BNB_T = 256;
 
 // channel groups of 8 per block: whole rows for C <= 64 (C/8 must be divisible), 64-channel slices above
@@ -329,10 +331,6 @@ DEV void bnb_reduce_impl(const TailArgs& a) {
   for (int p = p0 + pl; p < p1; p += PL) {
     float dz[8], xh[8], xh2[8], side[8];
     compute_dz<KIND>(a, X, z, p, c, dz, xh, xh2, side);
-    if (dzz) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dz[j] = rbf(dz[j]);
-    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       sdz[j] += dz[j];

@@ -189,6 +189,9 @@ struct BNArgs {
   int nrep;              // replicas in use (power of two <= NREP; the producer wrote blockIdx.x % nrep):
                          // small-M layers have few producer blocks, and every consumer block reads all of
                          // them (Model C's 1x6 layers: 32 replicas x 448 channels = 229 KB per block)
+  int sld;               // channel pitch of `stats` ([G][NREP][2][sld]): C, or the width of the combined
+                         // replica rows of a horizontally fused conv whose output channels feed several BNs
+                         // (this BN's rows then start at its channel offset)
 };
 
 template <int R>
@@ -204,15 +207,15 @@ DEV void bn_channel(const BNArgs& a, int z, int c, bool update_running, float& s
                     float& inv) {
   float var;
   if (a.training) {
-    const double* st = a.stats + (int64_t)z * NREP * 2 * a.C;
+    const double* st = a.stats + (int64_t)z * NREP * 2 * a.sld;
     double s = 0.0, ss = 0.0;
     switch (a.nrep) {  // a compile-time trip count keeps all loads of the reduction in flight
-      case 1: bn_rep_sum<1>(st, a.C, c, s, ss); break;
-      case 2: bn_rep_sum<2>(st, a.C, c, s, ss); break;
-      case 4: bn_rep_sum<4>(st, a.C, c, s, ss); break;
-      case 8: bn_rep_sum<8>(st, a.C, c, s, ss); break;
-      case 16: bn_rep_sum<16>(st, a.C, c, s, ss); break;
-      default: bn_rep_sum<NREP>(st, a.C, c, s, ss); break;
+      case 1: bn_rep_sum<1>(st, a.sld, c, s, ss); break;
+      case 2: bn_rep_sum<2>(st, a.sld, c, s, ss); break;
+      case 4: bn_rep_sum<4>(st, a.sld, c, s, ss); break;
+      case 8: bn_rep_sum<8>(st, a.sld, c, s, ss); break;
+      case 16: bn_rep_sum<16>(st, a.sld, c, s, ss); break;
+      default: bn_rep_sum<NREP>(st, a.sld, c, s, ss); break;
     }
     const double inv_n = 1.0 / (double)a.count;
     const double md = s * inv_n;

@@ -272,7 +272,11 @@ def grads_of(acts: Sequence[Act]) -> List[tuple]:
 class BNLayer:
     """Training-mode BatchNorm state for one BN module or a group of identically shaped per-task BNs."""
 
-    def __init__(self, mods: Sequence[nn.BatchNorm2d], flat: FlatState, arena: Arena, count: int):
+    def __init__(self, mods: Sequence[nn.BatchNorm2d], flat: FlatState, arena: Arena, count: int,
+                 stats_share: Optional[tuple] = None):
+        """``stats_share`` = (combined replica buffer [G][NREP][2][W], channel offset, W): the forward sums of this
+        BN are produced by a horizontally fused conv (ConvLayer ``concat``) whose output channels feed several
+        BNs -- its epilogue writes one combined replica buffer, and this BN reads its W-pitched channel range."""
         self.mods = list(mods)
         self.G = len(mods)
         m0 = mods[0]
@@ -288,7 +292,10 @@ class BNLayer:
         if self.G > 1 and rs != self.pstride:
             raise ValueError("BN running-stat stride must equal the affine-parameter stride")
         # fp64 replica sums: summation order no longer perturbs results (csrc/common.h BNArgs::stats)
-        self.stats = arena.zeroed((self.G, NREP, 2, self.C), torch.float64)
+        if stats_share is None:
+            self.stats, self.stats_off, self.sld = arena.zeroed((self.G, NREP, 2, self.C), torch.float64), 0, self.C
+        else:
+            self.stats, self.stats_off, self.sld = stats_share
         # backward: fp64 replica sums of the 2-D tiled BN backward (csrc/bn.hip bnb_*), zeroed per step
         self.nchunk, self.chunk_px = bnb_plan(count, self.C, self.G)
         self.part = arena.zeroed((self.G, NREP, 3, self.C), torch.float64)
@@ -307,7 +314,8 @@ class BNLayer:
     def args(self, training: bool) -> dict:
         f = self.flat
         m0 = self.mods[0]
-        return {"stats": P(self.stats), "gamma": P(f.params, f.off(m0.weight)), "beta": P(f.params, f.off(m0.bias)),
+        return {"stats": P(self.stats, self.stats_off), "sld": self.sld,
+                "gamma": P(f.params, f.off(m0.weight)), "beta": P(f.params, f.off(m0.bias)),
                 "run_mean": P(f.bn_mean, f.bn_offsets[id(m0)]), "run_var": P(f.bn_var, f.bn_offsets[id(m0)]),
                 "nbt": P(f.bn_nbt, f.bn_index[id(m0)]), "pstride": self.pstride, "C": self.C, "count": self.count,
                 "eps": self.eps, "momentum": self.momentum, "training": 1 if training else 0,
@@ -349,12 +357,27 @@ class ConvLayer:
     Adam-pack descriptors.  ``geom`` overrides the module's geometry with a virtual one (stem_pack_geom)."""
 
     def __init__(self, mods: Sequence[nn.Conv2d], flat: FlatState, arena: Arena, B: int, Hi: int, Wi: int,
-                 cin_stored: Optional[int] = None, geom: Optional[dict] = None):
+                 cin_stored: Optional[int] = None, geom: Optional[dict] = None, concat: bool = False):
+        """``concat``: the modules are SIBLING 1x1 convolutions of one input (Inception branches), lowered as ONE
+        conv whose output channels are their concatenation (horizontal fusion: one GEMM with N = sum of Co, one
+        data gradient over the concatenated dy, one weight-gradient job); ``members`` = [(module, channel
+        offset)].  Otherwise the modules are G identically shaped per-task copies (grid.z groups)."""
         self.mods = list(mods)
-        self.G = len(mods)
+        self.concat = concat
+        self.G = 1 if concat else len(mods)
         m = mods[0]
         self.flat = flat
         self.Co, self.Ci = m.out_channels, m.in_channels
+        self.members = [(m, 0)]
+        if concat:
+            self.members, n0 = [], 0
+            for x in self.mods:
+                if (x.in_channels, x.kernel_size, x.stride, x.padding, x.groups, x.dilation) != \
+                        (m.in_channels, (1, 1), m.stride, m.padding, 1, (1, 1)) or x.bias is not None or x.out_channels % 8:
+                    raise ValueError("horizontal fusion needs bias-free 1x1 siblings of one input with Cout % 8 == 0")
+                self.members.append((x, n0))
+                n0 += x.out_channels
+            self.Co = n0
         self.KH, self.KW = m.kernel_size
         self.sh, self.sw = m.stride
         self.ph, self.pw = m.padding
@@ -376,8 +399,8 @@ class ConvLayer:
         self.M_out = B * self.Ho * self.Wo
         self.M_in = B * Hi * Wi
         self.has_bias = m.bias is not None
-        self.wstride = flat.group_stride([x.weight for x in mods])
-        self.bstride = flat.group_stride([x.bias for x in mods]) if self.has_bias else 0
+        self.wstride = 0 if concat else flat.group_stride([x.weight for x in mods])
+        self.bstride = flat.group_stride([x.bias for x in mods]) if self.has_bias and not concat else 0
         taps = self.KH * self.KW
         self.Npad = pad_to(self.Co, 16)
         self.Kpad = pad_to(taps * self.Cs, 32)
@@ -446,6 +469,13 @@ class ConvLayer:
         """Pack jobs (csrc/optim.hip pack_kernel): the forward and data-gradient bf16 images of every
         group member, rebuilt from the fp32 masters after each optimizer step."""
         segs = []
+        if self.concat:  # member rows [n0, n0 + Co) of the forward image; its columns n0.. of the 1x1 dgrad image
+            for m, n0 in self.members:
+                common = {"off": self.flat.off(m.weight), "Co": m.out_channels, "Ci": self.Ci, "KH": 1, "KW": 1,
+                          "Cs": self.Cs, "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d}
+                segs.append(dict(common, kind=1, n=m.out_channels * self.Kpad, wf=P(self.wf, n0 * self.Kpad)))
+                segs.append(dict(common, kind=2, n=self.Npad_d * self.Kpad_d, wd=P(self.wd, n0)))
+            return segs
         for g, m in enumerate(self.mods):
             common = {"off": self.flat.off(m.weight), "Co": self.Co, "Ci": self.Ci, "KH": self.KH, "KW": self.KW,
                       "Cs": self.Cs, "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d}
@@ -453,6 +483,16 @@ class ConvLayer:
             segs.append(dict(common, kind=2, n=self.Npad_d * self.Kpad_d,
                              wd=P(self.wd, g * self.Npad_d * self.Kpad_d)))
         return segs
+
+    def finalize_descs(self) -> List[dict]:
+        """Finalize descriptors: one per member of a horizontally fused conv (its slab rows [n0, n0 + Co) into its
+        own weight's gradient), else the conv's one."""
+        if not self.concat:
+            return [self.finalize_desc()]
+        return [{"slab": P(self.slab, n0 * self.Kpad_w), "grad": P(self.flat.grads, self.flat.off(m.weight)), "ggs": 0,
+                 "G": 1, "splits": self.splits, "Npad": self.Npad, "Kpad": self.Kpad_w, "Co": m.out_channels,
+                 "Ci": self.Ci, "Cs": self.Cs, "KH": 1, "KW": 1, "elems": m.out_channels * self.Ci}
+                for m, n0 in self.members]
 
     def finalize_desc(self) -> dict:
         m0 = self.mods[0]

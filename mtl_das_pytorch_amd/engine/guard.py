@@ -15,7 +15,6 @@ changed.  Off (the default) the allocators are plain ``torch.empty`` / ``torch.z
 from __future__ import annotations
 
 import os
-import weakref
 from typing import List, Sequence, Tuple
 
 import torch
@@ -24,9 +23,7 @@ PAD = 4096          # bytes of each guard band (a multiple of every vector width
 PATTERN = 0x5A      # band byte
 
 _enabled = os.environ.get("MDA_GUARD") == "1"
-# (label, weak reference to the full uint8 buffer, body bytes): the registry does not keep buffers alive --
-# the body tensor (a view) does; a buffer freed by its program drops out of the checks
-_registry: List[Tuple[str, "weakref.ref", int]] = []
+_registry: List[Tuple[str, torch.Tensor, int]] = []  # (label, full uint8 buffer, body bytes)
 
 
 def enable(on: bool = True):
@@ -55,9 +52,7 @@ def alloc(shape, dtype=torch.float32, device="cpu", zero: bool = False, label: s
     t = full[PAD:PAD + nbytes].view(dtype).view(shape)
     if zero:
         t.zero_()
-    if len(_registry) % 256 == 0:  # prune the entries of freed buffers
-        _registry[:] = [r for r in _registry if r[1]() is not None]
-    _registry.append((label or f"{tuple(shape)} {dtype}", weakref.ref(full), nbytes))
+    _registry.append((label or f"{tuple(shape)} {dtype}", full, nbytes))
     return t
 
 
@@ -66,12 +61,9 @@ def alloc_like(t: torch.Tensor, zero: bool = True, label: str = "") -> torch.Ten
 
 
 def check() -> List[str]:
-    """Labels (with the first corrupted byte offset) of every live guarded buffer whose bands changed."""
+    """Labels (with the first corrupted byte offset) of every guarded buffer whose bands changed."""
     bad = []
-    for label, ref, body in _registry:
-        full = ref()
-        if full is None:
-            continue
+    for label, full, body in _registry:
         head, tail = full[:PAD], full[PAD + body:]
         for name, band, base in (("head", head, -PAD), ("tail", tail, body)):
             diff = (band != PATTERN).nonzero()
@@ -82,9 +74,8 @@ def check() -> List[str]:
 
 
 def count() -> int:
-    """Number of live guarded buffers."""
-    return sum(1 for r in _registry if r[1]() is not None)
+    return len(_registry)
 
 
 def labels() -> Sequence[str]:
-    return [r[0] for r in _registry if r[1]() is not None]
+    return [r[0] for r in _registry]

@@ -25,7 +25,7 @@ import torch
 from ..models.multi_classifier import (BasicConv2d, InceptionA, InceptionB, InceptionC, InceptionD, InceptionE,
                                        Multi_Classifier)
 from . import guard
-from .core import GRAD_DT, Act, Arena, BNLayer, ConvLayer, FlatState, P, grads_of, new_act, src_dict, stem_pack_geom
+from .core import GRAD_DT, NREP, Act, Arena, BNLayer, ConvLayer, FlatState, P, grads_of, new_act, src_dict, stem_pack_geom
 from .lowering import ACT_RELU, LoweredProgram
 from .program import Phase, k_cls_head, k_pool, k_wgfin
 
@@ -51,20 +51,33 @@ class Val:
 
 
 class CBR:
-    """conv -> BN -> ReLU (one BasicConv2d)."""
+    """conv -> BN -> ReLU (one BasicConv2d).  ``fused`` = (HConv, channel offset): the conv is a member of a
+    horizontally fused sibling group -- the HConv op runs it, this op is the member's BN + ReLU only (its y / dy
+    are channel slices of the group's buffers, its BN sums a slice of the group's replica rows)."""
 
-    def __init__(self, prog: "InceptionProgram", bc: BasicConv2d, src: Val, out: Val, geom: Optional[dict] = None):
+    def __init__(self, prog: "InceptionProgram", bc: BasicConv2d, src: Val, out: Val, geom: Optional[dict] = None,
+                 fused: Optional[tuple] = None):
         A, B, f = prog.arena, prog.B, prog.flat
         self.src, self.out = src, out
+        self.module = bc
         s = src.act
-        self.conv = c = ConvLayer([bc.conv], f, A, B, s.H, s.W, cin_stored=s.C, geom=geom)
-        if (c.Ho, c.Wo, c.Co) != (out.act.H, out.act.W, out.act.C):
-            raise ValueError(f"shape mismatch lowering {bc}: conv gives {(c.Ho, c.Wo, c.Co)}, "
+        self.fused = fused
+        if fused is not None:
+            hc, n0 = fused
+            self.conv = None
+            Ho, Wo, Co = hc.conv.Ho, hc.conv.Wo, bc.conv.out_channels
+            self.bn = BNLayer([bc.bn], f, A, B * Ho * Wo, stats_share=(hc.stats, n0, hc.conv.Co))
+            self.y, self.dy, self.dx = hc.y.slice(n0, Co), hc.dy.slice(n0, Co), None
+        else:
+            self.conv = c = ConvLayer([bc.conv], f, A, B, s.H, s.W, cin_stored=s.C, geom=geom)
+            Ho, Wo, Co = c.Ho, c.Wo, c.Co
+            self.bn = BNLayer([bc.bn], f, A, B * Ho * Wo)
+            self.y = new_act(A, 1, B, Ho, Wo, Co)
+            self.dy = new_act(A, 1, B, Ho, Wo, Co)
+            self.dx = new_act(A, 1, B, s.H, s.W, s.C, GRAD_DT) if src.needs_grad else None
+        if (Ho, Wo, Co) != (out.act.H, out.act.W, out.act.C):
+            raise ValueError(f"shape mismatch lowering {bc}: conv gives {(Ho, Wo, Co)}, "
                              f"destination {(out.act.H, out.act.W, out.act.C)}")
-        self.bn = BNLayer([bc.bn], f, A, B * c.Ho * c.Wo)
-        self.y = new_act(A, 1, B, c.Ho, c.Wo, c.Co)
-        self.dy = new_act(A, 1, B, c.Ho, c.Wo, c.Co)
-        self.dx = new_act(A, 1, B, s.H, s.W, s.C, GRAD_DT) if src.needs_grad else None
         self.nol_from: Optional["CBR"] = None  # producer whose BN+ReLU this conv applies on load
         self.skip_tail = False                 # the (single) consumer normalises self.y on load
 
@@ -74,15 +87,48 @@ class CBR:
         return src_dict(self.src.act), None
 
     def forward(self, prog, ph: Phase, training: bool):
-        src, nol = self._src()
-        prog._conv_fwd(ph, self.conv, src, self.y, self.bn, training, nol=nol)
+        if self.conv is not None:
+            src, nol = self._src()
+            prog._conv_fwd(ph, self.conv, src, self.y, self.bn, training, nol=nol)
         if not self.skip_tail:
             prog._tail(ph, ACT_RELU, 1, self.y, self.bn, self.out.act, training)
 
     def backward(self, prog, ph: Phase):
         prog._tail_bwd(ph, ACT_RELU, 1, self.y, self.bn, grads_of(self.out.grad_sources()), self.dy)
+        if self.conv is None:  # a fused member: its HConv's data / weight gradient run over the group's dy
+            return
         src, nol = self._src()
         prog._conv_bwd(ph, self.conv, src, self.dy, self.dx, nol=nol)
+        if self.dx is not None:
+            self.src.grads.append(self.dx)
+
+
+class HConv:
+    """Horizontal fusion of sibling 1x1 BasicConv2d convs that read the same input (an Inception block's
+    branch1x1 / branchNxN_1 heads, reference modelC_multiClassifier.py:70-83 via torchvision InceptionA/C/D/E):
+    ONE implicit GEMM with N = sum of the members' Cout writes their pre-BN outputs side by side (each member's
+    BN sums land in its slice of one combined replica buffer), and in the backward ONE data gradient over the
+    concatenated dy (K = sum of Cout) replaces the members' separate data gradients -- and their separate
+    gradient sources of the input -- plus one weight-gradient job for all of them.  The members' BN + ReLU
+    tails (and their backward) stay per member, on their branches' streams (``CBR`` with ``fused``)."""
+
+    def __init__(self, prog: "InceptionProgram", bcs: List[BasicConv2d], src: Val):
+        A, B, f = prog.arena, prog.B, prog.flat
+        self.src = src
+        s = src.act
+        self.conv = c = ConvLayer([bc.conv for bc in bcs], f, A, B, s.H, s.W, cin_stored=s.C, concat=True)
+        self.stats = A.zeroed((1, NREP, 2, c.Co), torch.float64)
+        self.y = new_act(A, 1, B, c.Ho, c.Wo, c.Co)
+        self.dy = new_act(A, 1, B, c.Ho, c.Wo, c.Co)
+        self.dx = new_act(A, 1, B, s.H, s.W, s.C, GRAD_DT) if src.needs_grad else None
+        self.members: List[CBR] = []  # filled by InceptionProgram._hconv
+
+    def forward(self, prog, ph: Phase, training: bool):
+        # the members' BNs share the combined replica buffer: any member's layer names it (offset 0 = base)
+        prog._conv_fwd(ph, self.conv, src_dict(self.src.act), self.y, self.members[0].bn, training)
+
+    def backward(self, prog, ph: Phase):
+        prog._conv_bwd(ph, self.conv, src_dict(self.src.act), self.dy, self.dx)
         if self.dx is not None:
             self.src.grads.append(self.dx)
 
@@ -207,6 +253,37 @@ class InceptionProgram(LoweredProgram):
         self._push(Pool(self, is_max, src, out))
         return out
 
+    def hfuse_enabled(self) -> bool:
+        """Horizontal fusion of sibling 1x1 convs (HConv; MDA_HFUSE=0 lowers every BasicConv2d on its own)."""
+        import os
+        return os.environ.get("MDA_HFUSE", "1") == "1"
+
+    def _hconv(self, bcs: List[BasicConv2d], src: Val, outs: List[Optional[Val]], branches: List[int]) -> List[Val]:
+        """Sibling 1x1 convs ``bcs`` of ``src`` (member i on branch ``branches[i]``, writing ``outs[i]`` or a new
+        value): one fused conv (stream 0, before the block's branches fork; in the backward after they join)
+        plus per-member BN + ReLU ops on the branches.  Returns the members' output values."""
+        if not self.hfuse_enabled():
+            vals = []
+            for bc, out, b in zip(bcs, outs, branches):
+                self._at(b)
+                vals.append(self._cbr(bc, src, out))
+            return vals
+        blk = self._cur
+        self._cur = None
+        hc = HConv(self, bcs, src)
+        self._push(hc)
+        vals = []
+        for (bc, out, b), (_, n0) in zip(zip(bcs, outs, branches), hc.conv.members):
+            if out is None:
+                out = self._val(hc.conv.Ho, hc.conv.Wo, bc.conv.out_channels)
+            self._at(b)
+            m = CBR(self, bc, src, out, fused=(hc, n0))
+            hc.members.append(m)
+            self._push(m)
+            vals.append(out)
+        self._cur = blk
+        return vals
+
     def _concat(self, H, W, widths) -> tuple:
         cat = self._val(H, W, sum(widths))
         parts, o = [], 0
@@ -221,9 +298,9 @@ class InceptionProgram(LoweredProgram):
         if isinstance(blk, InceptionA):
             pf = blk.branch_pool.conv.out_channels
             cat, (o1, o5, o3, op) = self._concat(H, W, [64, 64, 96, pf])
-            self._at(0); self._cbr(blk.branch1x1, x, o1)
-            self._at(1); self._cbr(blk.branch5x5_2, self._cbr(blk.branch5x5_1, x), o5)
-            self._at(2); self._cbr(blk.branch3x3dbl_3, self._cbr(blk.branch3x3dbl_2, self._cbr(blk.branch3x3dbl_1, x)), o3)
+            _, h5, h3 = self._hconv([blk.branch1x1, blk.branch5x5_1, blk.branch3x3dbl_1], x, [o1, None, None], [0, 1, 2])
+            self._at(1); self._cbr(blk.branch5x5_2, h5, o5)
+            self._at(2); self._cbr(blk.branch3x3dbl_3, self._cbr(blk.branch3x3dbl_2, h3), o3)
             self._at(3); self._cbr(blk.branch_pool, self._pool(False, x), op)
         elif isinstance(blk, InceptionB):
             Ho, Wo = (H - 3) // 2 + 1, (W - 3) // 2 + 1
@@ -233,33 +310,33 @@ class InceptionProgram(LoweredProgram):
             self._at(2); self._pool(True, x, om)
         elif isinstance(blk, InceptionC):
             cat, (o1, o7, od, op) = self._concat(H, W, [192, 192, 192, 192])
-            self._at(0); self._cbr(blk.branch1x1, x, o1)
-            self._at(1); self._cbr(blk.branch7x7_3, self._cbr(blk.branch7x7_2, self._cbr(blk.branch7x7_1, x)), o7)
+            _, h7, hd = self._hconv([blk.branch1x1, blk.branch7x7_1, blk.branch7x7dbl_1], x, [o1, None, None], [0, 1, 2])
+            self._at(1); self._cbr(blk.branch7x7_3, self._cbr(blk.branch7x7_2, h7), o7)
             self._at(2)
-            v = x
-            for i in range(1, 5):
+            v = hd
+            for i in range(2, 5):
                 v = self._cbr(getattr(blk, f"branch7x7dbl_{i}"), v)
             self._cbr(blk.branch7x7dbl_5, v, od)
             self._at(3); self._cbr(blk.branch_pool, self._pool(False, x), op)
         elif isinstance(blk, InceptionD):
             Ho, Wo = (H - 3) // 2 + 1, (W - 3) // 2 + 1
             cat, (o3, o7, om) = self._concat(Ho, Wo, [320, 192, x.act.C])
-            self._at(0); self._cbr(blk.branch3x3_2, self._cbr(blk.branch3x3_1, x), o3)
+            h3, h7 = self._hconv([blk.branch3x3_1, blk.branch7x7x3_1], x, [None, None], [0, 1])
+            self._at(0); self._cbr(blk.branch3x3_2, h3, o3)
             self._at(1)
-            v = x
-            for i in range(1, 4):
+            v = h7
+            for i in range(2, 4):
                 v = self._cbr(getattr(blk, f"branch7x7x3_{i}"), v)
             self._cbr(blk.branch7x7x3_4, v, o7)
             self._at(2); self._pool(True, x, om)
         elif isinstance(blk, InceptionE):
             cat, (o1, o3a, o3b, oda, odb, op) = self._concat(H, W, [320, 384, 384, 384, 384, 192])
-            self._at(0); self._cbr(blk.branch1x1, x, o1)
+            _, s, d1 = self._hconv([blk.branch1x1, blk.branch3x3_1, blk.branch3x3dbl_1], x, [o1, None, None], [0, 1, 2])
             self._at(1)
-            s = self._cbr(blk.branch3x3_1, x)
             self._cbr(blk.branch3x3_2a, s, o3a)
             self._cbr(blk.branch3x3_2b, s, o3b)
             self._at(2)
-            d = self._cbr(blk.branch3x3dbl_2, self._cbr(blk.branch3x3dbl_1, x))
+            d = self._cbr(blk.branch3x3dbl_2, d1)
             self._cbr(blk.branch3x3dbl_3a, d, oda)
             self._cbr(blk.branch3x3dbl_3b, d, odb)
             self._at(3); self._cbr(blk.branch_pool, self._pool(False, x), op)
@@ -306,7 +383,7 @@ class InceptionProgram(LoweredProgram):
         self.metrics = guard.alloc((3, 4), torch.float32, self.device, zero=True, label="metrics")
         self.confusion = guard.alloc((2, 16, 16), torch.int32, self.device, zero=True, label="confusion")
         self.nvalid = torch.full((1,), B, device=self.device, dtype=torch.int64)
-        self.convs: List[ConvLayer] = [op.conv for op in self.ops if isinstance(op, CBR)]
+        self.convs: List[ConvLayer] = [op.conv for op in self.ops if getattr(op, "conv", None) is not None]
         self._plan_nol()
 
     def set_rng_stream(self, seed: int, rank: int = 0):
@@ -329,13 +406,14 @@ class InceptionProgram(LoweredProgram):
         max_px = self.NOL_MAX_PX
         consumers = {}
         for op in self.ops:
-            consumers[id(op.src)] = consumers.get(id(op.src), 0) + 1
+            if getattr(op, "fused", None) is None:  # fused members read nothing: their HConv reads the input
+                consumers[id(op.src)] = consumers.get(id(op.src), 0) + 1
         consumers[id(self.feat)] = consumers.get(id(self.feat), 0) + 1
         producer = {id(op.out): op for op in self.ops if isinstance(op, CBR)}
         for op in self.ops:
             p = producer.get(id(op.src))
-            if (isinstance(op, CBR) and p is not None and op.src.parent is None
-                    and consumers[id(op.src)] == 1 and op.conv.Cs == p.conv.Co and op.conv.M_out <= max_px):
+            if (isinstance(op, CBR) and op.conv is not None and p is not None and op.src.parent is None
+                    and consumers[id(op.src)] == 1 and op.conv.Cs == p.out.act.C and op.conv.M_out <= max_px):
                 op.nol_from = p
                 p.skip_tail = True
                 self.n_nol += 1
@@ -399,11 +477,16 @@ class InceptionProgram(LoweredProgram):
                 owed0 = []
             st = meta[1] % 4
             ph.cur_stream = st
-            if st not in used:
-                used.add(st)
-                if st != 0:
-                    ph.pending_waits.append(f"{ph.name}_f{blk}")
+            first = st not in used
+            fork = f"{ph.name}_f{blk}"
+            if first and st != 0:
+                ph.pending_waits.append(fork)
+            n_before = len(ph.launches)
             run(self.ops[i])
+            if len(ph.launches) > n_before:
+                used.add(st)
+            elif first and st != 0:  # the op launched nothing (a fused member whose tail its consumer folded):
+                ph.pending_waits.remove(fork)  # the stream's first real launch waits for the fork instead
         if cur_block is not None:
             close_block()
         ph.cur_stream = 0

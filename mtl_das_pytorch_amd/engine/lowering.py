@@ -328,7 +328,7 @@ class LoweredProgram:
         return ph
 
     def _wgfin_args(self, convs=None):
-        t, nd, nblocks = build_wgfin_table([c.finalize_desc() for c in (self.convs if convs is None else convs)],
+        t, nd, nblocks = build_wgfin_table([d for c in (self.convs if convs is None else convs) for d in c.finalize_descs()],
                                            self.device)
         if convs is None:
             self.wgfin_table = t

@@ -44,12 +44,14 @@ def _no_miopen_references():
 @pytest.fixture(autouse=True)
 def _guard_bands_intact():
     """With MDA_GUARD=1 every engine buffer sits between canary bands (engine/guard.py); after each test none
-    of the live ones may have been written (the registry holds weak references: buffers a test's programs
-    freed drop out, so a full-suite guard run does not accumulate device memory)."""
+    of them may have been written.  The registry is then cleared: it holds the buffers (strongly) only until
+    the end of the test that allocated them, so a full-suite guard run does not accumulate device memory
+    (buffers of module-scoped fixtures are checked after the first test that used them)."""
     yield
     from mtl_das_pytorch_amd.engine import guard
     if guard.enabled() and guard.count():
         import torch
         torch.cuda.synchronize()
         bad = guard.check()
+        guard.reset()
         assert not bad, bad

@@ -226,8 +226,10 @@ def test_pack_images_match_layouts(model_name):
     torch.cuda.synchronize()
     n = 0
     for c in prog.convs:
-        for g, m in enumerate(c.mods):
-            w = m.weight.detach().float()
+        # a horizontally fused group (Model C's sibling 1x1 heads) is ONE conv over the concatenated weights
+        groups = [torch.cat([m.weight for m in c.mods])] if c.concat else [m.weight for m in c.mods]
+        for g, w in enumerate(groups):
+            w = w.detach().float()
             if c.KH * c.KW == w.shape[2] * w.shape[3]:  # the packed-tap stem has its own (virtual) layout
                 ef = pack_weight_fwd(w, c.Cs)
                 got = c.wf[g]

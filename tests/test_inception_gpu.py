@@ -152,7 +152,7 @@ def test_inception_backward_layer_local(cin):
     concat-slice gradient routing, multi-consumer source lists, pool backward) and every kernel at
     bf16-rounding precision, independent of the network's error amplification.  ``cin`` = 2: the 2-channel
     input of BASELINE's north star (unpacked 3x3/s2 stem over 8 stored channels)."""
-    from mtl_das_pytorch_amd.engine.inception import CBR
+    from mtl_das_pytorch_amd.engine.inception import CBR, HConv
     model, ref, prog, X, labels = _setup(p_drop=0.5, in_channels=cin)
     assert (prog.stem_pack[0] > 0) == (cin == 1)
     idx = torch.arange(prog.B, device="cuda")
@@ -161,6 +161,16 @@ def test_inception_backward_layer_local(cin):
     q = lambda t: t.bfloat16().float()
     worst = {}
     for op in prog.ops:
+        if isinstance(op, HConv):
+            # horizontally fused sibling 1x1 heads: ONE data gradient over the members' concatenated dy (each
+            # member's weight gradient and BN backward are checked with the member below)
+            x = _nchw(op.src.act).contiguous().requires_grad_(True)
+            w = torch.cat([q(m.weight.detach()) for m, _ in op.conv.members])
+            F.conv2d(x, w).backward(_nchw(op.dy))
+            err = rel(_nchw(op.dx), x.grad)
+            worst["hconv_dx"] = max(worst.get("hconv_dx", 0.0), err)
+            assert err < 2e-2, ("hconv dx", err)
+            continue
         g = sum(_nchw(a) for a in op.out.grad_sources())
         if getattr(op, "nol_from", None) is not None:
             # normalise-on-load: the input is never materialised; rebuild relu(BN(y)) of the producer from
@@ -171,7 +181,7 @@ def test_inception_backward_layer_local(cin):
         else:
             x = _nchw(op.src.act).contiguous()  # (torch's channels-last max-pool breaks ties differently)
         if isinstance(op, CBR):
-            conv, bn = op.conv.mods[0], op.bn.mods[0]
+            conv, bn = op.module.conv, op.bn.mods[0]
             x = x[:, :conv.in_channels].clone().requires_grad_(op.dx is not None)
             w = q(conv.weight.detach()).requires_grad_(True)
             gam, bet = bn.weight.detach(), bn.bias.detach()
@@ -201,8 +211,7 @@ def test_inception_backward_layer_local(cin):
         for k, (e, r) in checks.items():
             err = rel(e, r)
             worst[k] = max(worst.get(k, 0.0), err)
-            assert err < 2e-2, (k, err, [n for n, mm in model.named_modules() if getattr(op, "conv", None)
-                                        and mm is op.conv.mods[0]])
+            assert err < 2e-2, (k, err, [n for n, mm in model.named_modules() if mm is getattr(op, "module", None)])
     print("worst layer-local errors", {k: f"{v:.2e}" for k, v in worst.items()})
     # the classifier: d(fc) from the post-dropout features and the softmax gradient
     dl = torch.softmax(prog.logp, 1)

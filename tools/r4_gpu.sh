@@ -3,7 +3,7 @@
 source tools/gpu_round.sh
 what=${1:-all}
 if [ "$what" = tests ] || [ "$what" = all ]; then
-  step gputests timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread || exit $?
+  step gputests timeout -k 10 600 python -u -m pytest tests -m gpu --maxfail=10 -v --timeout 120 --timeout-method thread || exit $?
 fi
 if [ "$what" = bench ] || [ "$what" = all ]; then
   step benchA timeout -k 10 200 python bench.py --steps 300 --warmup 30 && \
