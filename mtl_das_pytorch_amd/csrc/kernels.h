@@ -218,6 +218,11 @@ struct OptSeg {
   bf16_t* wf;
   bf16_t* wd;
   int Co, Ci, KH, KW, Cs, Kpad_f, Kpad_d;
+  // members of a horizontally fused conv (engine/core.py ConvLayer concat): the member's image is a window of
+  // the group's -- kext_f = forward-image columns this member writes per row (its own taps, embedded at the
+  // group's tap offset by the wf pointer; 0 = Kpad_f), tap_ld = data-gradient-image column stride between taps
+  // (the group's Cout; 0 = Co)
+  int kext_f, tap_ld;
   int64_t block0;
 };
 

@@ -70,7 +70,7 @@ DEV void pack_dgrad_tile(const float* __restrict__ W, const OptSeg& S, int tile,
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       w4[j] = (uint32_t)f2bf(s_t[r][ch * 8 + 2 * j]) | ((uint32_t)f2bf(s_t[r][ch * 8 + 2 * j + 1]) << 16);
-    *reinterpret_cast<uint4*>(S.wd + (int64_t)ci * S.Kpad_d + tap * S.Co + co0 + ch * 8) =
+    *reinterpret_cast<uint4*>(S.wd + (int64_t)ci * S.Kpad_d + tap * (S.tap_ld ? S.tap_ld : S.Co) + co0 + ch * 8) =
         make_uint4(w4[0], w4[1], w4[2], w4[3]);
   }
 }
@@ -87,7 +87,7 @@ DEV void pack_fwd_rows_block(const float* __restrict__ W, const OptSeg& S, int b
   const float* src = W + (int64_t)co0 * row;
   for (int e = threadIdx.x; e < nr * row; e += 256) s_w[e] = src[e];
   __syncthreads();
-  const int K8 = S.Kpad_f >> 3;
+  const int K8 = (S.kext_f ? S.kext_f : S.Kpad_f) >> 3;
   for (int item = threadIdx.x; item < nr * K8; item += 256) {
     const int r = item / K8, k0 = (item - r * K8) * 8;
     const int tap = k0 / S.Cs, ci0 = k0 - tap * S.Cs;

@@ -358,24 +358,34 @@ class ConvLayer:
 
     def __init__(self, mods: Sequence[nn.Conv2d], flat: FlatState, arena: Arena, B: int, Hi: int, Wi: int,
                  cin_stored: Optional[int] = None, geom: Optional[dict] = None, concat: bool = False):
-        """``concat``: the modules are SIBLING 1x1 convolutions of one input (Inception branches), lowered as ONE
-        conv whose output channels are their concatenation (horizontal fusion: one GEMM with N = sum of Co, one
-        data gradient over the concatenated dy, one weight-gradient job); ``members`` = [(module, channel
-        offset)].  Otherwise the modules are G identically shaped per-task copies (grid.z groups)."""
+        """``concat``: the modules are SIBLING convolutions of one input, lowered as ONE conv whose output
+        channels are their concatenation (horizontal fusion: one GEMM with N = sum of Co, one data gradient over
+        the concatenated dy, one weight-gradient job) -- Inception's 1x1 branch heads, or Model A's 3x3/s2
+        residual conv with its 1x1/s2 projection shortcut.  The first module sets the kernel; every other one
+        has the same kernel or is a 1x1 whose window is the kernel's centre tap (same stride, padding reduced
+        by the offset: its weights occupy that tap of the packed images, the other taps stay zero).
+        ``members`` = [(module, channel offset, tap offset)].  Otherwise the modules are G identically shaped
+        per-task copies (grid.z groups)."""
         self.mods = list(mods)
         self.concat = concat
         self.G = 1 if concat else len(mods)
         m = mods[0]
         self.flat = flat
         self.Co, self.Ci = m.out_channels, m.in_channels
-        self.members = [(m, 0)]
+        self.members = [(m, 0, 0)]
         if concat:
             self.members, n0 = [], 0
+            KH, KW = m.kernel_size
             for x in self.mods:
-                if (x.in_channels, x.kernel_size, x.stride, x.padding, x.groups, x.dilation) != \
-                        (m.in_channels, (1, 1), m.stride, m.padding, 1, (1, 1)) or x.bias is not None or x.out_channels % 8:
-                    raise ValueError("horizontal fusion needs bias-free 1x1 siblings of one input with Cout % 8 == 0")
-                self.members.append((x, n0))
+                dh, dw = (KH - x.kernel_size[0]) // 2, (KW - x.kernel_size[1]) // 2
+                centre = x.kernel_size == (1, 1) and KH % 2 == 1 and KW % 2 == 1
+                if (x.in_channels != m.in_channels or x.stride != m.stride or x.groups != 1 or x.dilation != (1, 1)
+                        or x.bias is not None or x.out_channels % 8 or m.groups != 1
+                        or not (x.kernel_size == m.kernel_size or centre)
+                        or (x.padding[0] + dh, x.padding[1] + dw) != tuple(m.padding)):
+                    raise ValueError("horizontal fusion needs bias-free siblings of one input with Cout % 8 == 0 and "
+                                     "the first one's kernel, or 1x1 at its centre tap (same stride, aligned padding)")
+                self.members.append((x, n0, dh * KW + dw))
                 n0 += x.out_channels
             self.Co = n0
         self.KH, self.KW = m.kernel_size
@@ -469,12 +479,17 @@ class ConvLayer:
         """Pack jobs (csrc/optim.hip pack_kernel): the forward and data-gradient bf16 images of every
         group member, rebuilt from the fp32 masters after each optimizer step."""
         segs = []
-        if self.concat:  # member rows [n0, n0 + Co) of the forward image; its columns n0.. of the 1x1 dgrad image
-            for m, n0 in self.members:
-                common = {"off": self.flat.off(m.weight), "Co": m.out_channels, "Ci": self.Ci, "KH": 1, "KW": 1,
-                          "Cs": self.Cs, "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d}
-                segs.append(dict(common, kind=1, n=m.out_channels * self.Kpad, wf=P(self.wf, n0 * self.Kpad)))
-                segs.append(dict(common, kind=2, n=self.Npad_d * self.Kpad_d, wd=P(self.wd, n0)))
+        if self.concat:
+            # member rows [n0, n0 + Co) of the forward image, its taps at the group's tap offset t0 (a centre-tap
+            # 1x1 writes the Cs columns of that tap only); its columns n0.. of each tap of the data-gradient image
+            # (tap stride = the group's Co)
+            for m, n0, t0 in self.members:
+                kh, kw = m.kernel_size
+                common = {"off": self.flat.off(m.weight), "Co": m.out_channels, "Ci": self.Ci, "KH": kh, "KW": kw,
+                          "Cs": self.Cs, "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d, "tap_ld": self.Co,
+                          "kext_f": kh * kw * self.Cs if t0 else 0}
+                segs.append(dict(common, kind=1, n=m.out_channels * self.Kpad, wf=P(self.wf, n0 * self.Kpad + t0 * self.Cs)))
+                segs.append(dict(common, kind=2, n=self.Npad_d * self.Kpad_d, wd=P(self.wd, t0 * self.Co + n0)))
             return segs
         for g, m in enumerate(self.mods):
             common = {"off": self.flat.off(m.weight), "Co": self.Co, "Ci": self.Ci, "KH": self.KH, "KW": self.KW,
@@ -489,10 +504,11 @@ class ConvLayer:
         own weight's gradient), else the conv's one."""
         if not self.concat:
             return [self.finalize_desc()]
-        return [{"slab": P(self.slab, n0 * self.Kpad_w), "grad": P(self.flat.grads, self.flat.off(m.weight)), "ggs": 0,
-                 "G": 1, "splits": self.splits, "Npad": self.Npad, "Kpad": self.Kpad_w, "Co": m.out_channels,
-                 "Ci": self.Ci, "Cs": self.Cs, "KH": 1, "KW": 1, "elems": m.out_channels * self.Ci}
-                for m, n0 in self.members]
+        return [{"slab": P(self.slab, n0 * self.Kpad_w + t0 * self.Cs), "grad": P(self.flat.grads, self.flat.off(m.weight)),
+                 "ggs": 0, "G": 1, "splits": self.splits, "Npad": self.Npad, "Kpad": self.Kpad_w, "Co": m.out_channels,
+                 "Ci": self.Ci, "Cs": self.Cs, "KH": m.kernel_size[0], "KW": m.kernel_size[1],
+                 "elems": m.out_channels * self.Ci * m.kernel_size[0] * m.kernel_size[1]}
+                for m, n0, t0 in self.members]
 
     def finalize_desc(self) -> dict:
         m0 = self.mods[0]
@@ -578,7 +594,7 @@ PACK_FWD_FLOATS = 4096  # csrc/kernels.h
 def build_optseg_table(segs: List[dict], device) -> tuple:
     dt = np.dtype([("off", "<i8"), ("n", "<i8"), ("kind", "<i4"), ("_pad0", "<i4"), ("wf", "<u8"), ("wd", "<u8"),
                    ("Co", "<i4"), ("Ci", "<i4"), ("KH", "<i4"), ("KW", "<i4"), ("Cs", "<i4"), ("Kpad_f", "<i4"),
-                   ("Kpad_d", "<i4"), ("_pad1", "<i4"), ("block0", "<i8")])
+                   ("Kpad_d", "<i4"), ("kext_f", "<i4"), ("tap_ld", "<i4"), ("_pad1", "<i4"), ("block0", "<i8")])
     assert dt.itemsize == lib().SIZEOF_OPTSEG, (dt.itemsize, lib().SIZEOF_OPTSEG)
     arr = np.zeros(len(segs), dtype=dt)
     b0 = 0

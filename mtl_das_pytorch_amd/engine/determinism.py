@@ -84,7 +84,7 @@ def _written_buffers(prog):
 
 
 def first_divergent_launch(prog, X: torch.Tensor, labels: torch.Tensor, idx: torch.Tensor) -> Optional[dict]:
-    """Race bisection: execute the forward + backward twice from the same state, eagerly and one launch at a
+    """Race bisection: execute the forward + backward twice (after a warm-up) from the same state, eagerly and one launch at a
     time (serialised on one stream), snapshot every buffer each launch writes, and return the first launch
     whose output bytes differ between the two executions -- ``{"phase", "index", "launch", "arg"}`` -- or
     None when the step is bitwise reproducible.  The first divergence is the racing kernel (later launches
@@ -130,6 +130,10 @@ def first_divergent_launch(prog, X: torch.Tensor, labels: torch.Tensor, idx: tor
             snaps.append(out)
         return snaps
 
+    # three executions, the first discarded: a buffer several launches write in parts (a fused conv's combined
+    # dy, written slice by slice) holds the previous execution's bytes in its unwritten parts at a snapshot --
+    # after a warm-up execution those are the same in both compared runs
+    execute()
     a, b = execute(), execute()
     for t, s in zip(state, saved):
         t.copy_(s)

@@ -273,7 +273,7 @@ class InceptionProgram(LoweredProgram):
         hc = HConv(self, bcs, src)
         self._push(hc)
         vals = []
-        for (bc, out, b), (_, n0) in zip(zip(bcs, outs, branches), hc.conv.members):
+        for (bc, out, b), (_, n0, _) in zip(zip(bcs, outs, branches), hc.conv.members):
             if out is None:
                 out = self._val(hc.conv.Ho, hc.conv.Wo, bc.conv.out_channels)
             self._at(b)

@@ -104,23 +104,40 @@ class MTLProgram(LoweredProgram):
         prev = self.f0
         for rb in m.resblocks:
             L = {}
-            ca = ConvLayer([rb.left[0]], f, A, B, prev.H, prev.W)
-            Ho, Wo, C = ca.Ho, ca.Wo, ca.Co
-            L["ca"], L["bna"] = ca, BNLayer([rb.left[1]], f, A, B * Ho * Wo)
-            L["cb"], L["bnb"] = ConvLayer([rb.left[3]], f, A, B, Ho, Wo), BNLayer([rb.left[4]], f, A, B * Ho * Wo)
             L["proj"] = rb.has_projection
-            if rb.has_projection:
+            L["fused"] = rb.has_projection and self.hfuse_enabled()
+            if L["fused"]:
+                # horizontal fusion: conv a (3x3/s2) and the projection shortcut (1x1/s2, the centre tap of conv
+                # a's window) read the same input -- ONE conv with N = 2C writes [ya | ys], its epilogue the BN sums
+                # of both BNs into one combined replica buffer; one data gradient over [dya | dys]
+                cas = ConvLayer([rb.left[0], rb.shortcut[0]], f, A, B, prev.H, prev.W, concat=True)
+                Ho, Wo, C = cas.Ho, cas.Wo, cas.Co // 2
+                st = A.zeroed((1, NREP, 2, 2 * C), torch.float64)
+                L["cas"], L["stats"] = cas, st
+                L["bna"] = BNLayer([rb.left[1]], f, A, B * Ho * Wo, stats_share=(st, 0, 2 * C))
+                L["bns"] = BNLayer([rb.shortcut[1]], f, A, B * Ho * Wo, stats_share=(st, C, 2 * C))
+                yas, dyas = new_act(A, 1, B, Ho, Wo, 2 * C), new_act(A, 1, B, Ho, Wo, 2 * C)
+                L["yas"], L["dyas"] = yas, dyas
+                L["ya"], L["ys"] = yas.slice(0, C), yas.slice(C, C)
+                L["dya"], L["dys"] = dyas.slice(0, C), dyas.slice(C, C)
+            else:
+                ca = ConvLayer([rb.left[0]], f, A, B, prev.H, prev.W)
+                Ho, Wo, C = ca.Ho, ca.Wo, ca.Co
+                L["ca"], L["bna"] = ca, BNLayer([rb.left[1]], f, A, B * Ho * Wo)
+                L["ya"], L["dya"] = new_act(A, 1, B, Ho, Wo, C), new_act(A, 1, B, Ho, Wo, C)
+            L["cb"], L["bnb"] = ConvLayer([rb.left[3]], f, A, B, Ho, Wo), BNLayer([rb.left[4]], f, A, B * Ho * Wo)
+            if rb.has_projection and not L["fused"]:
                 L["cs"] = ConvLayer([rb.shortcut[0]], f, A, B, prev.H, prev.W)
                 L["bns"] = BNLayer([rb.shortcut[1]], f, A, B * Ho * Wo)
                 L["ys"] = new_act(A, 1, B, Ho, Wo, C)
                 L["dys"] = new_act(A, 1, B, Ho, Wo, C)
                 L["dxs"] = new_act(A, 1, B, prev.H, prev.W, prev.C, GRAD_DT)
-            else:
+            elif not rb.has_projection:
                 L["side"] = new_act(A, 1, B, Ho, Wo, C, GRAD_DT)
             L["in"] = prev
-            L["ya"], L["ha"], L["yb"] = (new_act(A, 1, B, Ho, Wo, C) for _ in range(3))
+            L["ha"], L["yb"] = (new_act(A, 1, B, Ho, Wo, C) for _ in range(2))
             L["out"] = new_act(A, 1, B, Ho, Wo, C)
-            L["dyb"], L["dya"] = new_act(A, 1, B, Ho, Wo, C), new_act(A, 1, B, Ho, Wo, C)
+            L["dyb"] = new_act(A, 1, B, Ho, Wo, C)
             L["dha"] = new_act(A, 1, B, Ho, Wo, C, GRAD_DT)
             L["dxa"] = new_act(A, 1, B, prev.H, prev.W, prev.C, GRAD_DT)
             self.rbs.append(L)
@@ -168,8 +185,14 @@ class MTLProgram(LoweredProgram):
         self.metrics = guard.alloc((T, 4), torch.float32, self.device, zero=True, label="metrics")
         self.confusion = guard.alloc((T, 16, 16), torch.int32, self.device, zero=True, label="confusion")
         self.nvalid = torch.full((1,), B, device=self.device, dtype=torch.int64)
-        self.convs: List[ConvLayer] = [c1] + [L[k] for L in self.rbs for k in ("ca", "cb", "cs") if k in L] + \
+        self.convs: List[ConvLayer] = self._backbone_convs() + \
                                       [L[k] for L in self.levels for k in ("c0", "c3", "co") if k in L]
+
+    @staticmethod
+    def hfuse_enabled() -> bool:
+        """Horizontal fusion of each projection block's conv a with its shortcut (MDA_HFUSE=0: separate convs)."""
+        import os
+        return os.environ.get("MDA_HFUSE", "1") == "1"
 
     def _emit(self):
         self.nol = self.nol_enabled()
@@ -188,13 +211,16 @@ class MTLProgram(LoweredProgram):
         ph.cur_stream = 0
         for ri, L in enumerate(self.rbs):
             s = src_dict(L["in"])
-            self._conv_fwd(ph, L["ca"], s, L["ya"], L["bna"], training)
+            if L["fused"]:  # [ya | ys] and both BNs' sums in one launch (bna names the combined replica rows)
+                self._conv_fwd(ph, L["cas"], s, L["yas"], L["bna"], training)
+            else:
+                self._conv_fwd(ph, L["ca"], s, L["ya"], L["bna"], training)
             if self.nol_for(L["cb"]):  # conv b normalises ya on load: no BN+ReLU tail, ha never materialised
                 self._conv_fwd(ph, L["cb"], src_dict(L["ya"]), L["yb"], L["bnb"], training, nol=(L["bna"], ACT_RELU))
             else:
                 self._tail(ph, ACT_RELU, 1, L["ya"], L["bna"], L["ha"], training)
                 self._conv_fwd(ph, L["cb"], src_dict(L["ha"]), L["yb"], L["bnb"], training)
-            if L["proj"]:
+            if L["proj"] and not L["fused"]:
                 self._conv_fwd(ph, L["cs"], s, L["ys"], L["bns"], training)
             if L["proj"]:
                 self._tail(ph, ADD_RELU, 1, L["yb"], L["bnb"], L["out"], training, r=L["ys"], bn2=L["bns"])
@@ -250,7 +276,7 @@ class MTLProgram(LoweredProgram):
         return [(self._rb1_anchor, 0, hi)]
 
     def _backbone_convs(self) -> list:
-        return [self.conv1] + [L[k] for L in self.rbs for k in ("ca", "cb", "cs") if k in L]
+        return [self.conv1] + [L[k] for L in self.rbs for k in ("ca", "cas", "cb", "cs") if k in L]
 
     def _emit_backward(self) -> Phase:
         ph = Phase("backward")
@@ -291,9 +317,9 @@ class MTLProgram(LoweredProgram):
             if k < 8:
                 R = self.rbs[k]  # resblock k+1 consumes F_k (or f0 when k == 0)
                 src.append((R["dxa"].p, 0, R["dxa"].ld))
-                if R["proj"]:
+                if R["proj"] and not R["fused"]:  # (fused: the one data gradient covers the shortcut too)
                     src.append((R["dxs"].p, 0, R["dxs"].ld))
-                else:
+                elif not R["proj"]:
                     src.append((R["side"].p, 0, R["side"].ld))
             return src
         for i in range(7, -1, -1):
@@ -314,8 +340,11 @@ class MTLProgram(LoweredProgram):
             else:
                 self._conv_bwd(ph, R["cb"], src_dict(R["ha"]), R["dyb"], R["dha"])
             self._tail_bwd(ph, ACT_RELU, 1, R["ya"], R["bna"], [(R["dha"].p, 0, R["dha"].ld)], R["dya"])
-            self._conv_bwd(ph, R["ca"], src_dict(R["in"]), R["dya"], R["dxa"])
-            if R["proj"]:
+            if R["fused"]:
+                self._conv_bwd(ph, R["cas"], src_dict(R["in"]), R["dyas"], R["dxa"])
+            else:
+                self._conv_bwd(ph, R["ca"], src_dict(R["in"]), R["dya"], R["dxa"])
+            if R["proj"] and not R["fused"]:
                 self._conv_bwd(ph, R["cs"], src_dict(R["in"]), R["dys"], R["dxs"])
         self.dy0 = new_act(self.arena, 1, self.B, self.y0.H, self.y0.W, self.y0.C)
         self._tail_bwd(ph, ACT_RELU, 1, self.y0, self.bn1, sources(0), self.dy0)

@@ -327,7 +327,9 @@ class Trainer:
         out = {"acc": {m.names[t]: m.acc(t) for t in range(len(m.names))},
                "loss": {m.names[t]: float(batch_means[t] / n) for t in range(len(m.names))}}
         if "distance" in m.names:
-            out["mae_m"] = mae_from_confusion(m.cm[m.names.index("distance")])
+            cm = m.cm[m.names.index("distance")]
+            out["mae_m"] = mae_from_confusion(cm)
+            out["distance_cm"] = cm.tolist()
         return out
 
     @torch.no_grad()

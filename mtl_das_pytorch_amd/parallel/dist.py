@@ -134,7 +134,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[int] = N
             kw = dict(backend=backend, store=dist.HashStore(), rank=0, world_size=1,
                       timeout=datetime.timedelta(seconds=timeout_s))
             if backend == "nccl":
-                kw["device_id"] = device
+                kw.update(device_id=device, pg_options=_rccl_options())
             dist.init_process_group(**kw)
         return _with_capture_group(DistContext(0, 1, 0, device, backend))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -147,9 +147,20 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[int] = N
     if not dist.is_initialized():
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
-            kw["device_id"] = device
+            kw.update(device_id=device, pg_options=_rccl_options())
         dist.init_process_group(**kw)
     return _with_capture_group(DistContext(rank, world, local_rank, device, backend))
+
+
+def _rccl_options():
+    """RCCL communicators run on HIGH-priority pool streams.  PyTorch hands out the normal-priority pool's 32
+    streams round robin to every ``torch.cuda.Stream()`` -- the engine's phase streams and the graph-capture
+    stream among them -- and to the process group's communication stream alike; once the pool wraps, a
+    communicator's stream can BE a stream the step graph captures on, and the watchdog's poll of an eager
+    collective's event recorded there fails during the capture ("event last recorded in a capturing stream",
+    seen on Model C's 4-stream step).  A separate pool keeps them apart; priority also puts the collectives'
+    kernels ahead of compute in the queues, as wanted for overlapped gradient buckets."""
+    return dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
 
 
 def _with_capture_group(ctx: DistContext) -> DistContext:
@@ -158,7 +169,7 @@ def _with_capture_group(ctx: DistContext) -> DistContext:
     call (new_group is collective); the default group is bound to the device, so the new communicator is
     initialised eagerly here -- never lazily inside a capture."""
     if ctx.backend == "nccl" and (ctx.world == 1 or os.environ.get("MDA_CAPTURE_COLLECTIVES") == "1"):
-        ctx.capture_group = dist.new_group(backend="nccl")
+        ctx.capture_group = dist.new_group(backend="nccl", pg_options=_rccl_options())
     return ctx
 
 

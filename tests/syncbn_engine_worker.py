@@ -66,7 +66,9 @@ def local_syncbn_check(prog, world):
                 if key in R and any(l.name == "conv_dgrad" and l.args[3].get("add") and l.args[3]["out"] == R[key].p
                                     for l in prog.bwd.launches):
                     return nchw(R[key])
-            g = g + nchw(R["dxa"]) + (nchw(R["dxs"]) if R["proj"] else nchw(R["side"]))
+            g = g + nchw(R["dxa"])
+            if not R.get("fused"):  # (a fused conv a + shortcut: "dxa" is the block input's one data gradient)
+                g = g + (nchw(R["dxs"]) if R["proj"] else nchw(R["side"]))
         return g
 
     def sync_dy(dz, y, bn):

@@ -226,8 +226,14 @@ def test_pack_images_match_layouts(model_name):
     torch.cuda.synchronize()
     n = 0
     for c in prog.convs:
-        # a horizontally fused group (Model C's sibling 1x1 heads) is ONE conv over the concatenated weights
-        groups = [torch.cat([m.weight for m in c.mods])] if c.concat else [m.weight for m in c.mods]
+        # a horizontally fused group (Model C's sibling 1x1 heads, Model A's conv a + centre-tap 1x1 shortcut) is
+        # ONE conv over the concatenated weights, a 1x1 member zero-padded to the group's kernel at its centre
+        def embed(w):
+            out = torch.zeros(w.shape[0], w.shape[1], c.KH, c.KW, device=w.device)
+            dh, dw = (c.KH - w.shape[2]) // 2, (c.KW - w.shape[3]) // 2
+            out[:, :, dh:dh + w.shape[2], dw:dw + w.shape[3]] = w
+            return out
+        groups = [torch.cat([embed(m.weight) for m in c.mods])] if c.concat else [m.weight for m in c.mods]
         for g, w in enumerate(groups):
             w = w.detach().float()
             if c.KH * c.KW == w.shape[2] * w.shape[3]:  # the packed-tap stem has its own (virtual) layout
@@ -245,3 +251,55 @@ def test_pack_images_match_layouts(model_name):
     assert n > 10
 
 
+
+
+def test_training_trajectory_matches_fp32_oracle():
+    """Three full training steps of Model A (forward, backward, Adam with the reference's lr 1e-3 / coupled
+    weight decay 1e-5 as torch.optim.Adam applies them) on the engine and on the fp32 reference module from
+    the same bf16-rounded weights and batches.  Tolerances are the oracle's own sensitivity: a copy of the
+    fp32 reference whose weights carry one bf16 ulp of relative noise (4e-3) is stepped alongside, and the
+    engine must stay within 1.5x that copy's distance from the oracle (plus a small floor) -- per step for
+    both task losses, and for the accumulated parameter update after the last step."""
+    from mtl_das_pytorch_amd.engine.step import StepRunner
+    from mtl_das_pytorch_amd.models import MTL_Net
+    model, ref, prog, X, labels = _setup(MTL_Net, B=16)
+    B, steps, lr, wd = prog.B, 3, 1e-3, 1e-5
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_(p.bfloat16().float())
+        prog.flat.params.copy_(prog.flat.params.bfloat16().float())  # the same rounded masters
+    noisy = copy.deepcopy(ref)
+    torch.manual_seed(321)
+    with torch.no_grad():
+        for p in noisy.parameters():
+            p.mul_(1 + 4e-3 * torch.randn_like(p))
+    p0 = {n: p.detach().clone() for n, p in ref.named_parameters()}
+    pn0 = {n: p.detach().clone() for n, p in noisy.named_parameters()}
+    prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=wd)
+    runner = StepRunner(prog, X, labels, use_graph=False)
+    runner.set_lr(lr)
+    opts = [torch.optim.Adam(m.parameters(), lr=lr, weight_decay=wd, foreach=False) for m in (ref, noisy)]
+    for s in range(steps):
+        idx = torch.arange(s * B, (s + 1) * B, device="cuda") % X.shape[0]
+        runner.reset_metrics()
+        runner.train_step(idx)
+        torch.cuda.synchronize()
+        eng = [prog.metrics[t, 0].item() / B for t in range(2)]
+        losses = []
+        for m, opt in zip((ref, noisy), opts):
+            m.train()
+            opt.zero_grad()
+            outs = m(X[idx].bfloat16().float())
+            ls = [F.nll_loss(o, labels[idx, t]) for t, o in enumerate(outs)]
+            sum(ls).backward()
+            opt.step()
+            losses.append([l.item() for l in ls])
+        for t in range(2):
+            tol = 1.5 * abs(losses[1][t] - losses[0][t]) + 0.02 * abs(losses[0][t]) + 1e-3
+            assert abs(eng[t] - losses[0][t]) <= tol, (s, t, eng[t], losses[0][t], losses[1][t])
+    upd_e = torch.cat([(p.detach() - p0[n]).flatten() for n, p in model.named_parameters()])
+    upd_r = torch.cat([(p.detach() - p0[n]).flatten() for n, p in ref.named_parameters()])
+    upd_n = torch.cat([(p.detach() - pn0[n]).flatten() for n, p in noisy.named_parameters()])
+    e, bound = rel(upd_e, upd_r), 1.5 * rel(upd_n, upd_r) + 0.05
+    print(f"3-step update: engine vs oracle {e:.3f}, noisy oracle vs oracle {rel(upd_n, upd_r):.3f}")
+    assert e <= bound, (e, bound)

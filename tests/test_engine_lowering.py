@@ -16,8 +16,14 @@ def test_mtl_program_structure():
         assert torch.equal(v, sd_before[k]), k
     assert p.flat.numel >= sum(x.numel() for x in m.parameters())
     n = p.num_launches()
-    # forward: 12 BN+ReLU tails are folded into their consumer conv (normalise-on-load)
-    assert n["forward_train"] == 48 and n["backward"] == 90
+    # forward: 12 BN+ReLU tails are folded into their consumer conv (normalise-on-load), and RB3/5/7's conv a
+    # and projection shortcut are one fused conv each (one forward, one data gradient, one wgrad job)
+    assert n["forward_train"] == 45 and n["backward"] == 84
+    for R in (p.rbs[2], p.rbs[4], p.rbs[6]):
+        cas = R["cas"]
+        assert R["fused"] and cas.concat and cas.Co == 2 * R["ya"].C and [t for _, _, t in cas.members] == [0, 4]
+        assert R["ys"].off == R["ya"].C and R["ys"].ld == cas.Co and R["bns"].sld == cas.Co
+        assert "dxs" not in R and "cs" not in R
     # the residual tails have 2-4 gradient sources: the last producing dgrad sums them (fold_tail_sources)
     # and fuses the tail's statistics, so 7 of 8 run apply-only; RB8's tail has no dgrad before it
     tails = [l for l in p.bwd.launches if l.name == "tailbwd4"]
@@ -33,8 +39,8 @@ def test_mtl_program_structure():
     assert p.flat.off(g1) - p.flat.off(g0) == L["c0"].wstride
     # shared backbone input read with group stride 0, per-task prev level with stride > 0
     assert L["Fa"].gs == 0 and L["prevB"].gs > 0
-    assert p.wgfin_table.numel() == len(p.convs) * 88
-    assert p.optseg_table.numel() == 2 * sum(c.G for c in p.convs) * 80
+    assert p.wgfin_table.numel() == (len(p.convs) + 3) * 88  # one finalize descriptor per fused member
+    assert p.optseg_table.numel() == 2 * (sum(c.G for c in p.convs) + 3) * 88
 
 
 def test_single_task_program():

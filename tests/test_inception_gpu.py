@@ -165,7 +165,7 @@ def test_inception_backward_layer_local(cin):
             # horizontally fused sibling 1x1 heads: ONE data gradient over the members' concatenated dy (each
             # member's weight gradient and BN backward are checked with the member below)
             x = _nchw(op.src.act).contiguous().requires_grad_(True)
-            w = torch.cat([q(m.weight.detach()) for m, _ in op.conv.members])
+            w = torch.cat([q(m.weight.detach()) for m, _, _ in op.conv.members])
             F.conv2d(x, w).backward(_nchw(op.dy))
             err = rel(_nchw(op.dx), x.grad)
             worst["hconv_dx"] = max(worst.get("hconv_dx", 0.0), err)

@@ -136,6 +136,18 @@ def conv_check(chk, name, conv, z, x, dy, dx_act=None, x_requires=True, dx_extra
         chk("dx", f"{name} dx", dx_act, x.grad if dx_extra is None else x.grad + dx_extra)
 
 
+def fused_conv_check(chk, names, conv, x, dys, dx_act, dx_extra=None):
+    """A horizontally fused conv (engine ConvLayer concat: RB3/5/7's conv a with its centre-tap 1x1 projection
+    shortcut): each member's weight gradient from its own dy slice, and the ONE data gradient against the sum
+    of the members' autograd input gradients."""
+    x = x.clone().requires_grad_(True)
+    for (m, _, _), name, dy in zip(conv.members, names, dys):
+        w = q(m.weight.detach()).requires_grad_(True)
+        F.conv2d(x, w, None, m.stride, m.padding).backward(dy)
+        chk("dW", f"{name}.weight", m.weight.grad, w.grad)
+    chk("dx", f"{names[0]}+shortcut dx", dx_act, x.grad if dx_extra is None else x.grad + dx_extra)
+
+
 def bn_grads_check(chk, name, bn, z, dgam, dbet):
     chk("dgamma", f"{name}.weight", bn.mods[z].weight.grad, dgam)
     chk("dbeta", f"{name}.bias", bn.mods[z].bias.grad, dbet)
@@ -147,6 +159,7 @@ def test_mtl_backward_layer_local(engine_step):
     T, lv, rbs = prog.T, prog.levels, prog.rbs
 
     def folded(R):  # which data gradient of block R summed all gradient sources of its input (or None)
+        # (a fused conv a + shortcut writes "dxa": the one data gradient of the block's input)
         for key in ("dxs", "dxa"):
             if key in R and any(l.name == "conv_dgrad" and l.args[3].get("add") and l.args[3]["out"] == R[key].p
                                 for l in prog.bwd.launches):
@@ -167,13 +180,17 @@ def test_mtl_backward_layer_local(engine_step):
             R = rbs[k]
             if folded(R):
                 return nchw(R[folded(R)])
-            g = g + nchw(R["dxa"]) + (nchw(R["dxs"]) if R["proj"] else nchw(R["side"]))
+            g = g + nchw(R["dxa"])
+            if not R.get("fused"):
+                g = g + (nchw(R["dxs"]) if R["proj"] else nchw(R["side"]))
         return g
 
     def folded_extra(i, key):  # what the folded dgrad of block i (consuming F_i) added to its own output
         R = rbs[i]
         if folded(R) != key:
             return None
+        if R.get("fused"):
+            return level_sources(i)
         return level_sources(i) + (nchw(R["dxa"]) if key == "dxs" else nchw(R["side"]))
 
     # ---- task levels (per task t, group z = t)
@@ -240,6 +257,10 @@ def test_mtl_backward_layer_local(engine_step):
         dya, dgam, dbet = bn_backward(nchw(R["dha"]) * ((ya * sca + sha) > 0), ya, R["bna"])
         chk("dy", f"{nm} inner tail dy", nchw(R["dya"]), dya)
         bn_grads_check(chk, f"{nm}.left.1", R["bna"], 0, dgam, dbet)
+        if R.get("fused"):
+            fused_conv_check(chk, [f"{nm}.left.0", f"{nm}.shortcut.0"], R["cas"], nchw(R["in"]),
+                             [nchw(R["dya"]), nchw(R["dys"])], nchw(R["dxa"]), dx_extra=folded_extra(i, "dxa"))
+            continue
         conv_check(chk, f"{nm}.left.0", R["ca"], 0, nchw(R["in"]), nchw(R["dya"]), nchw(R["dxa"]),
                    dx_extra=folded_extra(i, "dxa"))
         if R["proj"]:

@@ -42,7 +42,8 @@ def test_rccl_one_rank_dp_and_syncbn(model):
     assert "train_full" in s["graphs"]  # SyncBN stays on the single-graph step: collectives captured
     assert all(s["graph_eq_eager"].values()), s
     # one step vs plain BN: forward bitwise (BN statistics); backward summation order amplified by the chaotic
-    # network at init (measured: A 0 everywhere, C grads 1.1e-2)
+    # network at init -- with bf16 gradient storage an fp32 reordering flips the rounding of a few stored
+    # gradient elements by one ulp (measured: A grads 7.4e-3, params 1.3e-3 after one Adam step)
     r = s["rel_vs_plain"]
-    assert r["bn_mean"] == 0.0 and r["bn_var"] == 0.0 and r["grads"] < 5e-2 and r["params"] < 1e-3, s
+    assert r["bn_mean"] == 0.0 and r["bn_var"] == 0.0 and r["grads"] < 5e-2 and r["params"] < 5e-3, s
     assert res["misc"]["metrics_ok"] and res["misc"]["average_ok"]

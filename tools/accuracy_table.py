@@ -68,8 +68,28 @@ def run_one(name, model, backend, args, seed, test_sets, lab2, joint, out_dir):
         r = tr.evaluate(X, lab)
         row["test"][k] = {"acc": {t: round(v, 4) for t, v in r["acc"].items()},
                           "mae_m": None if r.get("mae_m") is None else round(r["mae_m"], 4)}
+        if r.get("distance_cm") is not None:
+            row["test"][k]["distance_cm"] = r["distance_cm"]
+            row["test"][k]["errors"] = error_profile(np.asarray(r["distance_cm"]))
     print(json.dumps(row), flush=True)
     return row
+
+
+def error_profile(cm: np.ndarray) -> dict:
+    """Where the distance errors go (rows = true class, columns = predicted; 1 m bins): the share of errors
+    within one bin of the truth, their mean |error| in metres, the share of all predictions that fall in the
+    most-predicted class, and the mean signed error (prediction - truth) -- tells an ordinal near-miss
+    localiser from one that collapses noisy samples onto a fixed class."""
+    n = cm.sum()
+    idx = np.arange(cm.shape[0])
+    dist = np.abs(idx[None, :] - idx[:, None])
+    err = cm * (dist > 0)
+    ne = err.sum()
+    top = int(cm.sum(0).argmax())
+    return {"near_miss_share": round(float((cm * (dist == 1)).sum() / max(ne, 1)), 4),
+            "mean_abs_err_of_errors_m": round(float((err * dist).sum() / max(ne, 1)), 3),
+            "top_pred_class": top, "top_pred_share": round(float(cm[:, top].sum() / max(n, 1)), 4),
+            "mean_signed_err_m": round(float((cm * (idx[None, :] - idx[:, None])).sum() / max(n, 1)), 3)}
 
 
 def _stat(vals, fmt):
@@ -106,6 +126,22 @@ def to_markdown(rows, args):
     for n in names:
         lines.append(f"| {n} | " + " | ".join(f"{cell(n, k, 'event')} / {cell(n, k, 'distance')} / {cell(n, k, 'mae')}"
                                            for k in keys[1:]) + " |")
+    lines += ["", "Distance errors (error_profile): share of errors within one bin / mean |error| of the errors (m) / "
+              "most-predicted class and its share of all predictions / mean signed error (m)", "",
+              "| Model | " + " | ".join(keys) + " |", "|---|" + "---|" * len(keys)]
+    for n in names:
+        rs = [r for r in rows if r["name"] == n]
+        if "errors" not in rs[0]["test"][keys[0]]:
+            continue
+
+        def prof(k):
+            e = [r["test"][k]["errors"] for r in rs]
+            tops = sorted({x["top_pred_class"] for x in e})
+            return (f"{_stat([x['near_miss_share'] for x in e], '%.2f')} / "
+                    f"{_stat([x['mean_abs_err_of_errors_m'] for x in e], '%.1f')} / "
+                    f"{','.join(str(t) for t in tops)}: {_stat([x['top_pred_share'] for x in e], '%.2f')} / "
+                    f"{_stat([x['mean_signed_err_m'] for x in e], '%+.1f')}")
+        lines.append(f"| {n} | " + " | ".join(prof(k) for k in keys) + " |")
     return "\n".join(lines) + "\n"
 
 
