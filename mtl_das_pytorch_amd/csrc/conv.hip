@@ -421,57 +421,23 @@ DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// Block: 256 threads, output tile TN (rows = cout) x TK (cols = k), MCH pixels staged per iteration.
-// Global loads of chunk c+1 are issued into registers before the MFMAs of chunk c (which read LDS), so
-// the load latency overlaps compute; one LDS image per operand, two barriers per chunk.
+// Staging of one im2col weight-gradient chunk (MCH pixels): dy [MCH][TN] and the im2col rows [MCH][TK] of
+// the forward input, loaded by 16-byte units into registers (so that the next chunk's loads are in flight
+// while this chunk's MFMAs run) and stored into pixel-major LDS images, with the normalise-on-load
+// transform applied on the way (the forward conv read act(BN(y)) on load: rebuild the operand the same way).
+struct WgCtx {
+  int n0, mend, HWo;
+  const bf16_t *base0, *base1, *dyz;
+};
+
 template <int TN, int TK, int MCH>
-DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const int z) {
-  // Row pitch 16 x odd elements (TN + 16 for even multiples of 16): with the row permutation below the 32
-  // lanes of one ds_read_b64_tr_b16 read rows 0-7 of a 16-row block, whose 8-bank windows then tile the 64
-  // banks exactly (the previous pitch TN + 8 with rows 0-3 and 8-11 per instruction left 2-way conflicts:
-  // SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.38)
-  constexpr int LDY = (TN / 16) % 2 ? TN : TN + 16, LDX = (TK / 16) % 2 ? TK : TK + 16;
-  __shared__ __attribute__((aligned(16))) bf16_t s_dy[MCH * LDY];
-  __shared__ __attribute__((aligned(16))) bf16_t s_x[MCH * LDX];
-  __shared__ int s_tab[TK / 8];
-  __shared__ float s_nsc[TK], s_nsh[TK];  // normalise-on-load constants of this tile's input channels
-  constexpr int FN = TN / 16, FK = TK / 16, NFR = FN * FK;
-  constexpr int FPW = (NFR + 3) / 4;  // fragments per wave
-  constexpr int VY = MCH * (TN / 8), VX = MCH * (TK / 8);
-  constexpr int NY = (VY + 255) / 256, NX = (VX + 255) / 256;
-
-  const int ntk = a.Kpad / TK;
-  const int tn = tile / ntk, tk = tile - tn * ntk;
-  const int n0 = tn * TN, k0 = tk * TK;
-  const int Ktot = a.KH * a.KW * a.Cs;
-  if (threadIdx.x < TK / 8) s_tab[threadIdx.x] = encode_kg(k0 / 8 + threadIdx.x, Ktot, a.Cs >> 3, a.KW, a.src.C0);
-  if (a.nol) {  // the forward conv read act(BN(y)) on load: rebuild the operand the same way
-    for (int t = threadIdx.x; t < TK; t += 256) {
-      const int e = encode_kg(k0 / 8 + t / 8, Ktot, a.Cs >> 3, a.KW, a.src.C0);
-      const int c = (e & 16383) + (t & 7);
-      const float* kz = a.nol_consts + (int64_t)z * 4 * a.Cs;
-      s_nsc[t] = ((e >> 29) & 1) ? kz[c] : 0.f;
-      s_nsh[t] = ((e >> 29) & 1) ? kz[a.Cs + c] : 0.f;
-    }
-  }
-
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int HWo = a.Ho * a.Wo;
-  const int M = a.B * HWo;
-  const int mbeg = split * a.m_per_split;
-  const int mend = min(M, mbeg + a.m_per_split);
-  const bf16_t* base0 = a.src.p[0] + a.src.gs[0] * z;
-  const bf16_t* base1 = a.src.p[1] ? a.src.p[1] + a.src.gs[1] * z : base0;
-  const bf16_t* dyz = a.dy + a.dgs * z;
-
-  f32x4 acc[FPW];
-#pragma unroll
-  for (int j = 0; j < FPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
-
+struct WgStage {
+  static constexpr int VY = MCH * (TN / 8), VX = MCH * (TK / 8);
+  static constexpr int NY = (VY + 255) / 256, NX = (VX + 255) / 256;
   uint4 ry[NY], rx[NX];
-  uint32_t rok = 0;  // which rx hold real input (not zero padding)
-  auto load_chunk = [&](int mc) {
+  uint32_t rok;  // which rx hold real input (not zero padding)
+
+  DEV void load(const WgradArgs& a, const WgCtx& c, int mc, const int* s_tab) {
     rok = 0;
 #pragma unroll
     for (int i = 0; i < NY; ++i) {
@@ -479,8 +445,8 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
       ry[i] = make_uint4(0, 0, 0, 0);
       if (v < VY) {
         const int p = v / (TN / 8), cg = v - p * (TN / 8);
-        const int m = mc + p, n = n0 + cg * 8;
-        if (m < mend && n < a.Co) ry[i] = *reinterpret_cast<const uint4*>(dyz + (int64_t)m * a.ldd + n);
+        const int m = mc + p, n = c.n0 + cg * 8;
+        if (m < c.mend && n < a.Co) ry[i] = *reinterpret_cast<const uint4*>(c.dyz + (int64_t)m * a.ldd + n);
       }
     }
 #pragma unroll
@@ -491,29 +457,30 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
         const int p = v / (TK / 8), g = v - p * (TK / 8);
         const int m = mc + p;
         const int e = s_tab[g];
-        if (m < mend && ((e >> 29) & 1)) {
-          const int b = m / HWo, r = m - b * HWo;
+        if (m < c.mend && ((e >> 29) & 1)) {
+          const int b = m / c.HWo, r = m - b * c.HWo;
           const int oh = r / a.Wo, ow = r - oh * a.Wo;
           const int ih = oh * a.sh - a.ph + ((e >> 21) & 127);
           const int iw = ow * a.sw - a.pw + ((e >> 14) & 127);
           if (ih >= 0 && ih < a.Hi && iw >= 0 && iw < a.Wi) {
             const int seg = (e >> 28) & 1;
-            const bf16_t* sb = seg ? base1 : base0;
+            const bf16_t* sb = seg ? c.base1 : c.base0;
             rx[i] = *reinterpret_cast<const uint4*>(sb + ((int64_t)(b * a.Hi + ih) * a.Wi + iw) * a.src.ld[seg] + (e & 16383));
             rok |= 1u << i;
           }
         }
       }
     }
-  };
-  auto store_chunk = [&]() {
+  }
+
+  DEV void store(const WgradArgs& a, bf16_t* s_dy, int ldy, bf16_t* s_x, int ldx, const float* s_nsc,
+                 const float* s_nsh) const {
 #pragma unroll
     for (int i = 0; i < NY; ++i) {
       const int v = threadIdx.x + 256 * i;
       if (v < VY) {
         const int p = v / (TN / 8), cg = v - p * (TN / 8);
-        const uint4 u = ry[i];
-        *reinterpret_cast<uint4*>(&s_dy[p * LDY + cg * 8]) = u;
+        *reinterpret_cast<uint4*>(&s_dy[p * ldy + cg * 8]) = ry[i];
       }
     }
 #pragma unroll
@@ -533,16 +500,74 @@ DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const 
           }
           u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
         }
-        *reinterpret_cast<uint4*>(&s_x[p * LDX + g * 8]) = u;
+        *reinterpret_cast<uint4*>(&s_x[p * ldx + g * 8]) = u;
       }
     }
-  };
+  }
+};
 
-  if (mbeg < mend) load_chunk(mbeg);
+// Per-tile setup shared by the im2col weight-gradient kernels: the tap / channel table of the TK columns
+// starting at k0 (columns past the reduction encode as invalid and stage zeros), the normalise-on-load
+// constants of those columns, and the chunk context.
+template <int TK>
+DEV WgCtx wgrad_tile_setup(const WgradArgs& a, int n0, int k0, int split, int z, int* s_tab, float* s_nsc,
+                           float* s_nsh) {
+  const int Ktot = a.KH * a.KW * a.Cs;
+  if (threadIdx.x < TK / 8) s_tab[threadIdx.x] = encode_kg(k0 / 8 + threadIdx.x, Ktot, a.Cs >> 3, a.KW, a.src.C0);
+  if (a.nol) {
+    for (int t = threadIdx.x; t < TK; t += 256) {
+      const int e = encode_kg(k0 / 8 + t / 8, Ktot, a.Cs >> 3, a.KW, a.src.C0);
+      const int c = (e & 16383) + (t & 7);
+      const float* kz = a.nol_consts + (int64_t)z * 4 * a.Cs;
+      s_nsc[t] = ((e >> 29) & 1) ? kz[c] : 0.f;
+      s_nsh[t] = ((e >> 29) & 1) ? kz[a.Cs + c] : 0.f;
+    }
+  }
+  WgCtx c;
+  c.n0 = n0;
+  c.HWo = a.Ho * a.Wo;
+  c.mend = min(a.B * c.HWo, (split + 1) * a.m_per_split);
+  c.base0 = a.src.p[0] + a.src.gs[0] * z;
+  c.base1 = a.src.p[1] ? a.src.p[1] + a.src.gs[1] * z : c.base0;
+  c.dyz = a.dy + a.dgs * z;
+  return c;
+}
+
+// Block: 256 threads, output tile TN (rows = cout) x TK (cols = k), MCH pixels staged per iteration.
+// Global loads of chunk c+1 are issued into registers before the MFMAs of chunk c (which read LDS), so
+// the load latency overlaps compute; one LDS image per operand, two barriers per chunk.
+template <int TN, int TK, int MCH>
+DEV void wgrad_block(const WgradArgs& a, const int tile, const int split, const int z) {
+  // Row pitch 16 x odd elements (TN + 16 for even multiples of 16): with the row permutation below the 32
+  // lanes of one ds_read_b64_tr_b16 read rows 0-7 of a 16-row block, whose 8-bank windows then tile the 64
+  // banks exactly (the previous pitch TN + 8 with rows 0-3 and 8-11 per instruction left 2-way conflicts:
+  // SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.38)
+  constexpr int LDY = (TN / 16) % 2 ? TN : TN + 16, LDX = (TK / 16) % 2 ? TK : TK + 16;
+  __shared__ __attribute__((aligned(16))) bf16_t s_dy[MCH * LDY];
+  __shared__ __attribute__((aligned(16))) bf16_t s_x[MCH * LDX];
+  __shared__ int s_tab[TK / 8];
+  __shared__ float s_nsc[TK], s_nsh[TK];  // normalise-on-load constants of this tile's input channels
+  constexpr int FN = TN / 16, FK = TK / 16, NFR = FN * FK;
+  constexpr int FPW = (NFR + 3) / 4;  // fragments per wave
+
+  const int ntk = a.Kpad / TK;
+  const int tn = tile / ntk, tk = tile - tn * ntk;
+  const int n0 = tn * TN, k0 = tk * TK;
+  const WgCtx c = wgrad_tile_setup<TK>(a, n0, k0, split, z, s_tab, s_nsc, s_nsh);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int mbeg = split * a.m_per_split, mend = c.mend;
+
+  f32x4 acc[FPW];
+#pragma unroll
+  for (int j = 0; j < FPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  WgStage<TN, TK, MCH> st;
+  if (mbeg < mend) st.load(a, c, mbeg, s_tab);
   for (int mc = mbeg; mc < mend; mc += MCH) {
-    store_chunk();
+    st.store(a, s_dy, LDY, s_x, LDX, s_nsc, s_nsh);
     __syncthreads();
-    if (mc + MCH < mend) load_chunk(mc + MCH);  // in flight during this chunk's MFMAs
+    if (mc + MCH < mend) st.load(a, c, mc + MCH, s_tab);  // in flight during this chunk's MFMAs
 #pragma unroll
     for (int kk = 0; kk < MCH / 32; ++kk) {
       // the MFMA's k index (pixel) of lane group g = lane >> 4 is any fixed permutation of the chunk's
@@ -595,6 +620,107 @@ __global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob*
   const int per_z = J.ntiles * J.a.splits;
   const int z = local / per_z, r = local - z * per_z;
   wgrad_block<TN, TK, MCH>(J.a, r % J.ntiles, r / J.ntiles, z);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Large-tile weight gradient on the 32x32x16 MFMA (configs WGRAD_BIG_CFG0 + i).  The 16-32-wide tiles of
+// wgrad_block re-stage dy and the im2col operand once per tile: Model C's wide 1x7 / 7x1 layers staged
+// ~1.2 GB per step through LDS for ~50 GFLOP, at one 16x16x32 MFMA per two transposed reads.  Here a
+// block owns a TN x TK tile of 64 or 128 rows / columns, its 4 waves a (TN/2) x (TK/2) quarter each, a
+// grid of 32x32 accumulators: every k-step of 16 pixels costs (TN + TK)/64 read pairs for TN*TK/4096
+// MFMAs of 16K MACs, and the operands are staged 2-4x less often.  Chunks of 64 pixels; the pitch of the
+// pixel-major LDS images (width + 32 elements) puts the 4 rows of a transposed read (32 columns each) on
+// disjoint bank quarters.  K tiles may run past Kpad (their columns stage zeros and are not stored).
+DEV bf16x8 tr_read32(const bf16_t* lds_row0, int ld, int col0, int lane) {
+  // lane l receives column col0 + (l & 31) of rows 8 (l >> 5) .. 8 (l >> 5) + 7: the A (row = l & 31) or
+  // B (column = l & 31) operand of a 32x32x16 MFMA whose k index is the row
+  const int i = lane & 15, g = lane >> 4;
+  const bf16_t* a0 = lds_row0 + (8 * (g >> 1) + (i >> 2)) * ld + col0 + 16 * (g & 1) + 4 * (i & 3);
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + 4 * ld));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int TN, int TK>
+DEV void wgrad_big_block(const WgradArgs& a, const int tile, const int split, const int z) {
+  constexpr int MCH = 64;
+  constexpr int LDY = TN + 32, LDX = TK + 32;
+  constexpr int FA = TN / 64, FB = TK / 64;  // 32x32 accumulators of a wave along n / k
+  __shared__ __attribute__((aligned(16))) bf16_t s_dy[MCH * LDY];
+  __shared__ __attribute__((aligned(16))) bf16_t s_x[MCH * LDX];
+  __shared__ int s_tab[TK / 8];
+  __shared__ float s_nsc[TK], s_nsh[TK];
+
+  const int ntk = (a.Kpad + TK - 1) / TK;
+  const int tn = tile / ntk, tk = tile - tn * ntk;
+  const int n0 = tn * TN, k0 = tk * TK;
+  const WgCtx c = wgrad_tile_setup<TK>(a, n0, k0, split, z, s_tab, s_nsc, s_nsh);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wn = (wid & 1) * (TN / 2), wk = (wid >> 1) * (TK / 2);
+  const int mbeg = split * a.m_per_split, mend = c.mend;
+
+  f32x16 acc[FA][FB];
+#pragma unroll
+  for (int i = 0; i < FA; ++i)
+#pragma unroll
+    for (int j = 0; j < FB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  __syncthreads();
+
+  WgStage<TN, TK, MCH> st;
+  if (mbeg < mend) st.load(a, c, mbeg, s_tab);
+  for (int mc = mbeg; mc < mend; mc += MCH) {
+    st.store(a, s_dy, LDY, s_x, LDX, s_nsc, s_nsh);
+    __syncthreads();
+    if (mc + MCH < mend) st.load(a, c, mc + MCH, s_tab);
+#pragma unroll
+    for (int ks = 0; ks < MCH / 16; ++ks) {
+      bf16x8 av[FA], bv[FB];
+#pragma unroll
+      for (int i = 0; i < FA; ++i) av[i] = tr_read32(&s_dy[ks * 16 * LDY], LDY, wn + 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < FB; ++j) bv[j] = tr_read32(&s_x[ks * 16 * LDX], LDX, wk + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < FA; ++i)
+#pragma unroll
+        for (int j = 0; j < FB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  float* slab = a.slab + (((int64_t)z * a.splits + split) * a.Npad) * a.Kpad;
+#pragma unroll
+  for (int i = 0; i < FA; ++i)
+#pragma unroll
+    for (int j = 0; j < FB; ++j) {
+      const int col = k0 + wk + 32 * j + (lane & 31);
+      const int row0 = n0 + wn + 32 * i + 4 * (lane >> 5);
+      if (col < a.Kpad) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = row0 + (r & 3) + 8 * (r >> 2);
+          if (row < a.Npad) slab[(int64_t)row * a.Kpad + col] = acc[i][j][r];
+        }
+      }
+    }
+}
+
+template <int TN, int TK>
+__global__ __launch_bounds__(256) void conv_wgrad_big_kernel(WgradArgs a) {
+  wgrad_big_block<TN, TK>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+template <int TN, int TK>
+__global__ __launch_bounds__(256) void conv_wgrad_big_batched_kernel(const WgradJob* __restrict__ jobs, int nj) {
+  int lo = 0, hi = nj - 1;
+  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
+  const WgradJob& J = jobs[lo];
+  const int local = (int)((int64_t)blockIdx.x - J.block0);
+  const int per_z = J.ntiles * J.a.splits;
+  const int z = local / per_z, r = local - z * per_z;
+  wgrad_big_block<TN, TK>(J.a, r % J.ntiles, r / J.ntiles, z);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -936,6 +1062,17 @@ int launch_conv(int mode, const ConvArgs& a0, int G, int cfg, hipStream_t st) {
   case 12: X(16, 16, 88, 4) case 13: X(32, 16, 88, 4) case 14: X(32, 32, 48, 4) case 15: X(64, 32, 24, 4) \
   case 16: X(32, 32, 128, 2) case 17: X(64, 32, 128, 2) case 18: X(64, 16, 128, 2) case 19: X(32, 16, 128, 2)
 
+// Large-tile configs 32-35 (TN, TK; 64-pixel chunks); keep in sync with ops/functional.py WGRAD_BIG.
+#define WGRAD_BIG_CASES(X) case 32: X(64, 64) case 33: X(64, 128) case 34: X(128, 64) case 35: X(128, 128)
+
+int wgrad_big_shape(int cfg, int& TN, int& TK) {
+  if (cfg < WGRAD_BIG_CFG0 || cfg >= WGRAD_BIG_CFG0 + WGRAD_BIG_NCFG) return -1;
+  const int k = cfg - WGRAD_BIG_CFG0;
+  TN = (k & 2) ? 128 : 64;
+  TK = (k & 1) ? 128 : 64;
+  return 0;
+}
+
 int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8, int& R) {
   static const int tn[] = {16, 32, 32, 64, 32, 64, 64, 32}, cb[] = {16, 16, 32, 32, 32, 32, 16, 16};
   static const int w8[] = {88, 88, 48, 24, 128, 128, 128, 128}, rr[] = {4, 4, 4, 4, 2, 2, 2, 2};
@@ -956,11 +1093,25 @@ int wgrad_ntiles(int cfg, const WgradArgs& a) {
       return -2;
     return ((a.Npad + TN - 1) / TN) * (a.Cs / CB);
   }
+  if (!wgrad_big_shape(cfg, TN, TK)) return ((a.Npad + TN - 1) / TN) * ((a.Kpad + TK - 1) / TK);
   if (wgrad_tile_shape(cfg, TN, TK) || a.Kpad % TK) return -2;  // the K tiles must cover Kpad exactly
   return ((a.Npad + TN - 1) / TN) * (a.Kpad / TK);
 }
 
 int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st) {
+  if (cfg >= WGRAD_BIG_CFG0) {
+    const int nt = wgrad_ntiles(cfg, a);
+    if (nt < 0) return nt;
+#define LAUNCH_WGBIG(TN, TK)                                                                            \
+  hipLaunchKernelGGL((conv_wgrad_big_kernel<TN, TK>), dim3(nt, a.splits, G), dim3(256), 0, st, a); \
+  break;
+    switch (cfg) {
+      WGRAD_BIG_CASES(LAUNCH_WGBIG)
+      default: return -1;
+    }
+#undef LAUNCH_WGBIG
+    return (int)hipGetLastError();
+  }
   if (cfg >= WGRAD_PATCH_CFG0) {
     const int nt = wgrad_ntiles(cfg, a);
     if (nt < 0) return nt;
@@ -1001,6 +1152,17 @@ int wgrad_tile_shape(int cfg, int& TN, int& TK) {
 int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st) {
   if (nblocks <= 0) return 0;
   dim3 grid((unsigned)nblocks);
+  if (cfg >= WGRAD_BIG_CFG0) {
+#define LAUNCH_WGBIGB(TN, TK)                                                                                 \
+  hipLaunchKernelGGL((conv_wgrad_big_batched_kernel<TN, TK>), grid, dim3(256), 0, st, d_jobs, nj); \
+  break;
+    switch (cfg) {
+      WGRAD_BIG_CASES(LAUNCH_WGBIGB)
+      default: return -1;
+    }
+#undef LAUNCH_WGBIGB
+    return (int)hipGetLastError();
+  }
   if (cfg >= WGRAD_PATCH_CFG0) {
 #define LAUNCH_WGPB(TN, CB, W8, R)                                                                              \
   hipLaunchKernelGGL((conv_wgrad_patch_batched_kernel<TN, CB, W8, R>), grid, dim3(256), 0, st, d_jobs, nj); \

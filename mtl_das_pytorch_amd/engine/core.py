@@ -23,7 +23,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..ops.functional import WGRAD_PATCH, WGRAD_TILES, bnb_plan, patch_plan, patch_valid, wgrad_cfg
+from ..ops.functional import (WGRAD_BIG0, WGRAD_PATCH, WGRAD_TILES, bnb_plan, patch_plan, patch_valid, wgrad_cfg,
+                              wgrad_ktiles)
 from ..ops.hip import lib, ptr
 from . import guard
 
@@ -432,15 +433,17 @@ class ConvLayer:
     # finalize (Model C: ~0.9 GB/step of slab traffic with grid-filling splits)
     # (512 / 2048 / 4096 measured within noise on A, C 7.10k at 1024 vs 6.83k at 2048)
     MIN_SPLIT_PX = 1024
+    MIN_SPLIT_PX_BIG = 256
 
     def wgrad_valid(self, cfg: int) -> bool:
-        """The K tiles of ``cfg`` cover this conv's padded reduction exactly (patch configs: a 3x3 / s1 /
-        p1 conv whose input channels split into whole CB slices and whose rows fit the tile width)."""
+        """The K tiles of ``cfg`` cover this conv's padded reduction (exactly, except for the large-tile
+        configs; patch configs: a 3x3 / s1 / p1 conv whose input channels split into whole CB slices and
+        whose rows fit the tile width)."""
         if cfg in WGRAD_PATCH:
             return self.stem_geom is None and patch_valid(cfg, self.Cs, self.KH, self.KW, (self.sh, self.sw),
                                                           (self.ph, self.pw), self.Hi, self.Wi, self.Ho, self.Wo,
                                                           self.src_C0, self.src_C1)
-        return self.Kpad_w % WGRAD_TILES[cfg][1] == 0
+        return wgrad_ktiles(cfg, self.Kpad_w) > 0
 
     def wgrad_plan(self, cfg: int):
         if cfg in WGRAD_PATCH:
@@ -450,10 +453,14 @@ class ConvLayer:
             wide = WGRAD_PATCH[cfg][2] >= 128
             return patch_plan(cfg, self.B, self.Ho, self.Npad, self.Cs, self.G, 512 if wide else 128)
         TN, TK, MCH = WGRAD_TILES[cfg]
-        tiles = math.ceil(self.Npad / TN) * (self.Kpad_w // TK) * self.G
+        tiles = math.ceil(self.Npad / TN) * wgrad_ktiles(cfg, self.Kpad_w) * self.G
         # whole-reduction tiles (TK >= 128) have one tile per channel block: shorter per-block pixel
-        # ranges keep enough blocks in flight (the finalize sums the extra splits with several lanes)
-        min_px = self.MIN_SPLIT_PX // 2 if TK >= 128 else self.MIN_SPLIT_PX
+        # ranges keep enough blocks in flight (the finalize sums the extra splits with several lanes);
+        # the large tiles stage 2-4x fewer bytes per output and can afford more splits still
+        if cfg >= WGRAD_BIG0:
+            min_px = self.MIN_SPLIT_PX_BIG
+        else:
+            min_px = self.MIN_SPLIT_PX // 2 if TK >= 128 else self.MIN_SPLIT_PX
         splits = max(1, min(math.ceil(self.M_out / MCH), math.ceil(512 / tiles),
                             math.ceil(self.M_out / min_px)))
         mps = pad_to(math.ceil(self.M_out / splits), MCH)

@@ -7,10 +7,10 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ..ops.functional import WGRAD_PATCH, WGRAD_TILES
+from ..ops.functional import WGRAD_PATCH, WGRAD_TILES, wgrad_ktiles
 from ..ops.hip import lib
 from .core import GRAD_DT, Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, pad_to
-from .program import (COMM_STREAM, Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad,
+from .program import (COMM_STREAM, SPILL_STREAM, Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad,
                       k_wgrad_batched)
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
@@ -23,7 +23,7 @@ def _wgrad_cost(cfg: int, G: int, d: dict) -> int:
         px = d["splits"] * d["m_per_split"] * R * pad_to(d["Wo"], 8)
         return px * G * math.ceil(d["Npad"] / TN) * TN * 9 * d["Cs"]
     TN, TK, MCH = WGRAD_TILES[cfg]
-    return d["splits"] * d["m_per_split"] * G * TN * TK * math.ceil(d["Npad"] / TN) * (d["Kpad"] // TK)
+    return d["splits"] * d["m_per_split"] * G * TN * TK * math.ceil(d["Npad"] / TN) * wgrad_ktiles(cfg, d["Kpad"])
 
 
 _GRAD_KEYS = ("dgamma", "dbeta", "dgamma2", "dbeta2", "dW", "db")
@@ -132,7 +132,7 @@ class LoweredProgram:
             new.append(l)
             bn = by_stats.get(l.args[3].get("stats") or 0) if l.name == "conv_fwd" else None
             if bn is not None:
-                new += self._collective(allreduce, bn.stats, l.stream, l.bucket, l.record)
+                new += self._collective(allreduce, self._used_replicas(bn.stats, bn.nrep), l.stream, l.bucket, l.record)
                 l.record = None
                 n += 1
         self.fwd_train.launches = new
@@ -153,13 +153,13 @@ class LoweredProgram:
                                                                 "dy2", "d2gs", "ldd2", "pgs")}
                 red["fused"] = 3
                 l.name, l.args = f"tailpart{kind}", (kind, G, nchunk, red)
-                new += [l] + self._collective(allreduce, bn.part, l.stream, l.bucket)
+                new += [l] + self._collective(allreduce, self._used_replicas(bn.part, bn.pnrep), l.stream, l.bucket)
             elif l.stream < self.COLLECTIVE_STREAMS:  # statistics from the producing dgrad's epilogue
-                l.name, l.fn, l.args = "allreduce_bn", k_allreduce, (allreduce, bn.part)
+                l.name, l.fn, l.args = "allreduce_bn", k_allreduce, (allreduce, self._used_replicas(bn.part, bn.pnrep))
                 new.append(l)
             else:  # (the launch keeps its waits as a kernel-free fork point in front of the collective)
                 l.name, l.fn, l.args = f"fork:{l.name}", None, ()
-                new += [l] + self._collective(allreduce, bn.part, l.stream, l.bucket)
+                new += [l] + self._collective(allreduce, self._used_replicas(bn.part, bn.pnrep), l.stream, l.bucket)
             d = {k: v for k, v in d.items() if k not in ("dzbuf", "dzgs", "lddz")}
             d["fused"], d["gscale"] = 2, 1.0 / world
             new.append(Launch(name, k_tail_bwd, kind, G, nchunk, d, owner=l.owner, stream=l.stream, record=record,
@@ -168,6 +168,14 @@ class LoweredProgram:
         self.bwd.launches = new
         self.sync_bn_world = world
         return n
+
+    @staticmethod
+    def _used_replicas(buf, nrep: int):
+        """The part of a BN replica buffer ([G][NREP][rows][C], arena-bound) that holds data: its first ``nrep``
+        replicas when there is one group (a contiguous slice -- small maps use few replicas, and Model C's 1x6
+        layers would otherwise all-reduce 32x the bytes), the whole buffer for grouped (per-task) BNs."""
+        t = buf.t if hasattr(buf, "bind") else buf
+        return t[0, :nrep] if t.shape[0] == 1 else t
 
     # Collectives captured into the step graph from at most these streams (0 and 1: Model A's backbone and
     # level branches); a collective of a BN on a later stream (Model C's Inception branches) runs on stream 0
@@ -507,6 +515,41 @@ class LoweredProgram:
         self.n_wgrad_merged = moved
         return moved
 
+    def spill_wgrads(self, frac: float) -> int:
+        """Move the weight gradients of stream 0's EARLIEST convs (in backward order; about ``frac`` of stream
+        0's weight-gradient work) to their own batches on the spill stream, which start as soon as the last
+        of them has its dy -- while stream 0 still runs the rest of its data-gradient chain.
+
+        batch_wgrads otherwise puts every stream-0 weight gradient after stream 0's last kernel, and stream
+        0 ends the backward (the stem / first residual blocks, serial dgrads of a few us each that leave most
+        of the GPU idle).  Measured: Model C +1-2 % at frac 0.7 (the stem's wide-map weight gradients stay
+        at the end, the Inception blocks' move); Model A -2..-8 % at any fraction, also with the spilled
+        blocks capped at one per CU -- its stream-0 chain of small dgrads slows by more than the ~110 us of
+        batches it sheds (tools/timeline.py: +150 us).  Chosen per model in the step by tune_in_context
+        (table entry wgspill|..., percent; 0 = off).  Must run before merge_wgrad_cfgs / batch_wgrads; a
+        backward cut into gradient-bucket pieces is left alone.  Returns the number of convs moved."""
+        ls = self.bwd.launches
+        if frac <= 0 or any(l.name == "cut" for l in ls):
+            return 0
+        wg0 = [l for l in ls if l.name == "conv_wgrad" and l.stream == 0]
+        # a launch recording an event (other than the per-conv "wgrads" tag) ends the movable prefix
+        cut = next((i for i, l in enumerate(wg0) if l.record not in (None, "wgrads")), len(wg0))
+        wg0 = wg0[:cut]
+        cost = [_wgrad_cost(l.args[0], l.args[1], l.args[2]) for l in wg0]
+        total, acc, n = sum(cost), 0, 0
+        while n < len(wg0) and acc + cost[n] <= frac * total:
+            acc += cost[n]
+            n += 1
+        if n == 0:
+            return 0
+        last = next(i for i, l in enumerate(ls) if l is wg0[n - 1])
+        ls.insert(last + 1, Launch("fork:wgspill", None, stream=0, record="wgspill"))
+        for l in wg0[:n]:
+            l.stream = SPILL_STREAM
+            l.waits = tuple(l.waits) + ("wgspill",)
+        self.n_wgrad_spilled = n
+        return n
+
     def batch_wgrads(self):
         """Replace the per-conv weight-gradient launches by batched launches, one per (stream, tile
         config) (csrc/conv.hip conv_wgrad_batched_kernel).  Each stream's batch goes after that stream's
@@ -541,7 +584,13 @@ class LoweredProgram:
             for cfg in sorted({l.args[0] for l in wg if l.stream == st}):
                 group = [l for l in wg if l.stream == st and l.args[0] == cfg]
                 batched.append(self._wgrad_batch_launch(cfg, group, st))
-            pos = max((i for i, k in enumerate(keep) if k.stream == st), default=len(keep) - 1) + 1
+            # the jobs' own waits (spilled weight gradients: the spill point) go on the stream's first batch
+            batched[0].waits = tuple(dict.fromkeys(w for l in wg if l.stream == st for w in l.waits))
+            # list position = capture order, which the graph executor follows when it dispatches: a batch
+            # goes right after its stream's last kernel or the launch recording what it waits for (a spilled
+            # batch appended at the end of the list started after stream 0's whole chain)
+            pos = max([i for i, k in enumerate(keep) if k.stream == st or (k.record and k.record in batched[0].waits)],
+                      default=len(keep) - 1) + 1
             batched[-1].record = f"wgrads_s{st}"
             tags.append(batched[-1].record)
             inserts.append((pos, batched))

@@ -29,6 +29,9 @@ MAX_STREAMS = 4
 # logical id of the communication stream: data-parallel gradient all-reduces embedded in the backward
 # (LoweredProgram.backward_with_allreduce) run there, beside the compute streams, never folded onto them
 COMM_STREAM = 7
+# logical id of the weight-gradient spill stream (LoweredProgram.spill_wgrads): the early stream-0 weight
+# gradients run there while stream 0 continues its data-gradient chain
+SPILL_STREAM = 6
 
 
 class Launch:
@@ -99,9 +102,10 @@ class Phase:
             return
         main = torch.cuda.current_stream()
         if self._streams is None or self._streams[0].device != main.device:
-            self._streams = [torch.cuda.Stream(device=main.device) for _ in range(MAX_STREAMS)]
-        streams = [main] + self._streams  # [MAX_STREAMS] is the communication stream
-        sid_of = lambda l: MAX_STREAMS if l.stream == COMM_STREAM else min(l.stream, MAX_STREAMS - 1)
+            self._streams = [torch.cuda.Stream(device=main.device) for _ in range(MAX_STREAMS + 1)]
+        streams = [main] + self._streams  # [MAX_STREAMS] communication, [MAX_STREAMS + 1] spill stream
+        sid_of = lambda l: (MAX_STREAMS if l.stream == COMM_STREAM else MAX_STREAMS + 1 if l.stream == SPILL_STREAM  # noqa: E731
+                            else min(l.stream, MAX_STREAMS - 1))
         used = {sid_of(l) for l in self.launches}
         start = main.record_event()
         for sid in used - {0}:

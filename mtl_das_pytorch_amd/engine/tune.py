@@ -17,7 +17,8 @@ import torch
 
 from ..ops.functional import (CONV_DEEP_CFG0, CONV_DEEP_NCFG, CONV_GLDS_CFG0, CONV_GLDS_NCFG, CONV_LDS_CFG0,
                               CONV_LDS_NCFG, CONV_PATCH_CFG0, CONV_PATCH_NCFG, CONV_PATCHP_CFG0, CONV_PATCHP_NCFG,
-                              CONV_XCD, GDEEP_TILES, WGRAD_PATCH, WGRAD_TILES, conv_workspace, glds_cfg)
+                              CONV_XCD, GDEEP_TILES, WGRAD_BIG0, WGRAD_PATCH, WGRAD_TILES, conv_workspace,
+                              glds_cfg)
 from ..ops.hip import lib
 
 # conv.hip register-pipelined tiles 0-13 (pipeline depth 2, and 4 at CONV_DEEP_CFG0 + tile), then
@@ -44,6 +45,10 @@ def conv_signature(mode: int, G: int, d: dict) -> str:
     sig = f"conv{mode}|G{G}|" + ",".join(str(d[k]) for k in keys) + f"|seg{int(src.get('C1', 0) > 0)}" + \
           f"|st{int(bool(d.get('stats')))}"
     return sig
+
+
+def wgrad_signature(G: int, d: dict) -> str:
+    return "wgrad|" + conv_signature(0, G, dict(d, N=d["Co"], Hs=d["Hi"], Ws=d["Wi"], stats=0))
 
 
 def load_cache(path: Optional[str] = None) -> Dict[str, int]:
@@ -136,7 +141,7 @@ def autotune_phases(phases: Iterable, cache: Optional[Dict[str, int]] = None, ve
                 continue
             cfg, G, d = launch.args
             conv = launch.owner
-            sig = "wgrad|" + conv_signature(0, G, dict(d, N=d["Co"], Hs=d["Hi"], Ws=d["Wi"], stats=0))
+            sig = wgrad_signature(G, d)
             if sig not in cache and not measure:
                 continue
             if sig not in cache:
@@ -182,6 +187,19 @@ def tail_bwd_signature(kind: int, G: int, d: dict) -> str:
             f"|bn2{int('bn2' in d)}|side{int(bool(d.get('side')))}")
 
 
+def spill_signature(prog) -> str:
+    return f"wgspill|{type(prog).__name__}|B{prog.B}|convs{len(prog.convs)}"
+
+
+def wgrad_spill_frac(prog, cache: Dict[str, int]) -> float:
+    """Share of stream 0's weight-gradient work moved to the spill stream (LoweredProgram.spill_wgrads), in
+    percent in the table (chosen in the captured step by tune_in_context); MDA_WGSPILL overrides."""
+    env = os.environ.get("MDA_WGSPILL")
+    if env is not None:
+        return float(env)
+    return cache.get(spill_signature(prog), 0) / 100.0
+
+
 def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False, measure: bool = True,
                      batch_wgrads: bool = True, cache: Optional[Dict[str, int]] = None) -> Dict[str, int]:
     """Tune every conv launch of a lowered program (train forward, eval forward, backward), then batch the
@@ -194,12 +212,158 @@ def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False
     n0 = len(cache)
     autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose, measure)
     if batch_wgrads:
+        prog.spill_wgrads(wgrad_spill_frac(prog, cache))
         prog.merge_wgrad_cfgs()
     prog.refresh_wgrad_finalize()
     if batch_wgrads:
         prog.batch_wgrads()
     if out_path and len(cache) != n0:
         save_cache(cache, out_path)
+    return cache
+
+
+def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passes: int = 1) -> Dict[str, int]:
+    """Choose the weight-gradient configs by the time of the BATCHED launches they end up in.
+
+    A conv's weight gradient never runs alone: it is a job of one batched launch per (stream, config)
+    (engine/lowering.py batch_wgrads) beside dozens of others, so what counts is the aggregate -- bytes
+    staged through LDS, blocks in flight, the finalize's split-slab reads -- not one job's latency, which
+    is what the isolated timing of autotune_phases ranks (it favours small tiles with many blocks; in the
+    batch the large 32x32x16 tiles, 2-4x fewer staged bytes per output, win on the big layers).  Greedy
+    coordinate descent over the wgrad signatures (costliest first): each candidate -- the current config
+    and every valid large tile -- is applied, the per-stream config cap (merge_wgrad_cfgs) and the finalize
+    refresh run as the bench runs them, and the sum of the batched launches' and the finalize's isolated
+    graph-replay times decides.  Must run before batch_wgrads (on the per-conv launches).  Updates and
+    returns ``cache``."""
+    L = lib()
+    wg = [l for l in prog.bwd.launches if l.name == "conv_wgrad" and l.owner is not None]
+    if not wg:
+        return cache
+    groups: Dict[str, list] = {}
+    for l in wg:
+        groups.setdefault(wgrad_signature(l.args[1], l.args[2]), []).append(l)
+    assign = {sig: ls[0].args[0] for sig, ls in groups.items()}
+    start = dict(assign)
+    fin = [l for l in prog.bwd.launches if l.name == "wgrad_finalize"]
+
+    def cost() -> float:
+        for sig, ls in groups.items():
+            for l in ls:
+                l.owner.set_wgrad_cfg(assign[sig])
+                l.args = (assign[sig],) + tuple(l.args[1:])
+        prog.merge_wgrad_cfgs()
+        prog.refresh_wgrad_finalize()
+        total, tables = 0.0, []
+        for key in sorted({(l.bucket, l.stream, l.args[0]) for l in wg}):
+            job = [l for l in wg if (l.bucket, l.stream, l.args[0]) == key]
+            raw, nblocks = L.wgrad_table(key[2], [l.args[2] for l in job], [l.args[1] for l in job])
+            t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(prog.device)
+            tables.append(t)
+            total += _time(lambda c=key[2], t=t, n=len(job), nb=nblocks:
+                           L.wgrad_batched(c, t.data_ptr(), n, nb, torch.cuda.current_stream().cuda_stream))
+        for f in fin:
+            total += _time(lambda f=f: f.fn(*f.args, torch.cuda.current_stream().cuda_stream))
+        return total
+
+    def weight(sig):
+        d = groups[sig][0].args[2]
+        return len(groups[sig]) * d["B"] * d["Ho"] * d["Wo"] * d["Npad"] * d["Kpad"]
+
+    best = cost()
+    t0 = best
+    for _ in range(passes):
+        changed = False
+        for sig in sorted(groups, key=weight, reverse=True):
+            cur = assign[sig]
+            for c in [start[sig]] + [c for c in WGRAD_CFGS if c >= WGRAD_BIG0]:
+                if c == assign[sig] or not all(l.owner.wgrad_valid(c) for l in groups[sig]):
+                    continue
+                prev = assign[sig]
+                assign[sig] = c
+                t = cost()
+                if t < best * 0.995:
+                    best = t
+                    changed = True
+                else:
+                    assign[sig] = prev
+            if assign[sig] != cur and verbose:
+                print(f"  {sig}: wgrad cfg {cur} -> {assign[sig]} (batches + finalize {best * 1e3:.1f} us)",
+                      flush=True)
+        if not changed:
+            break
+    cost()  # leave the launches on the chosen assignment
+    cache.update(assign)
+    if verbose:
+        print(f"wgrad batches + finalize: {t0 * 1e3:.1f} -> {best * 1e3:.1f} us", flush=True)
+    return cache
+
+
+def step_time_us(prog, X: torch.Tensor, labels: torch.Tensor, reps: int = 100, rounds: int = 3) -> float:
+    """Best-of-``rounds`` mean time of the training step (gather, forward, backward, Adam + re-pack at
+    learning rate 0) captured as one HIP graph; the program's mutable state is restored afterwards."""
+    from .step import StateSnapshot
+    f = prog.flat
+    snap = StateSnapshot([f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step,
+                          f.lr, prog.metrics, prog.confusion, prog.logp] + list(getattr(prog, "extra_state", [])))
+    f.lr.zero_()
+    prog.opt["pack"].run()
+    idx = torch.arange(prog.B, device=prog.device) % X.shape[0]
+    gather = prog.gather_phase(X, labels, idx)
+    fns = [prog.arena.clear, gather.run, prog.fwd_train.run, prog.bwd.run, prog.opt["adam"].run]
+    for fn_ in fns:
+        fn_()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for fn_ in fns:
+            fn_()
+    for _ in range(10):
+        g.replay()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            g.replay()
+        e.record()
+        torch.cuda.synchronize()
+        best = min(best, 1e3 * s.elapsed_time(e) / reps)
+    g.reset()
+    del g
+    snap.restore()
+    prog.opt["pack"].run()
+    torch.cuda.synchronize()
+    return best
+
+
+def tune_spill(make_prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str, int],
+               fracs=(0, 50, 70, 90), margin: float = 0.005, verbose: bool = True) -> Dict[str, int]:
+    """Choose the weight-gradient spill fraction (LoweredProgram.spill_wgrads; table entry in percent) by
+    the captured step's time.  ``make_prog()`` builds a fresh, un-tuned program of the model (the spill
+    rewrites the per-conv launches, which batching removes, so every candidate needs its own lowering).
+    Candidates are timed in two alternating rounds and a fraction must beat 0 (off) by ``margin`` in
+    both."""
+    times: Dict[int, list] = {fr: [] for fr in fracs}
+    key = None
+    for _ in range(2):
+        for fr in fracs:
+            prog = make_prog()
+            key = spill_signature(prog)
+            cache[key] = fr
+            autotune_program(prog, cache=cache, measure=False)
+            times[fr].append(step_time_us(prog, X, labels))
+            del prog
+            torch.cuda.empty_cache()
+    best = 0
+    for fr in fracs:
+        if fr and all(t < b * (1.0 - margin) for t, b in zip(times[fr], times[0])):
+            if best == 0 or sum(times[fr]) < sum(times[best]):
+                best = fr
+    cache[key] = best
+    if verbose:
+        print("spill fractions: " + ", ".join(f"{fr}%: {' / '.join(f'{t:.1f}' for t in times[fr])} us"
+                                              for fr in fracs) + f" -> {best}%", flush=True)
     return cache
 
 

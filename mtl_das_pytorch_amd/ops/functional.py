@@ -226,7 +226,20 @@ def conv2d_dgrad(dy: torch.Tensor, w: torch.Tensor, in_hw: Tuple[int, int], stri
 WGRAD_TILES = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 64), 4: (16, 64, 128),
                5: (16, 32, 256), 6: (32, 32, 256), 7: (64, 32, 64),
                # whole-reduction tiles for small-Cout layers (csrc/conv.hip WGRAD_CFG_CASES)
-               8: (16, 192, 64), 9: (16, 128, 64), 10: (32, 192, 64), 11: (32, 320, 32)}  # (TN, TK, MCH)
+               8: (16, 192, 64), 9: (16, 128, 64), 10: (32, 192, 64), 11: (32, 320, 32),  # (TN, TK, MCH)
+               # large tiles on the 32x32x16 MFMA (csrc/conv.hip wgrad_big_block); their last K tile may be
+               # partial
+               32: (64, 64, 64), 33: (64, 128, 64), 34: (128, 64, 64), 35: (128, 128, 64)}
+WGRAD_BIG0 = 32
+
+
+def wgrad_ktiles(cfg: int, Kpad: int) -> int:
+    """K tiles of an im2col weight-gradient config over a padded reduction of ``Kpad`` columns; 0 if the
+    config cannot cover it (the small-tile kernels need TK | Kpad)."""
+    TK = WGRAD_TILES[cfg][1]
+    if cfg >= WGRAD_BIG0:
+        return math.ceil(Kpad / TK)
+    return 0 if Kpad % TK else Kpad // TK
 
 
 # 3x3 / stride-1 patch kernels, padding 1 or 0 (csrc/conv.hip wgrad_patch_block):
@@ -245,7 +258,9 @@ def patch_valid(cfg, Cs, KH, KW, stride, padding, Hi, Wi, Ho, Wo, C0=None, C1=0)
 
 
 def patch_plan(cfg, B, Ho, Npad, Cs, G=1, target=512):
-    """(splits, units per split) of a patch wgrad: unit = (image, strip of R output rows)."""
+    """(splits, units per split) of a patch wgrad: unit = (image, strip of R output rows).  (Capping the
+    units per block at 3 to even out the blocks of a batched launch measured 4 % slower on Model A: the
+    extra splits cost more slab traffic in the finalize than the shorter blocks saved.)"""
     TN, CB, _, R = WGRAD_PATCH[cfg]
     U = B * math.ceil(Ho / R)
     tiles = math.ceil(Npad / TN) * (Cs // CB) * G
@@ -278,10 +293,10 @@ def prepare_conv2d_wgrad(x, dy, w_shape, stride=1, padding=0, x2=None, splits=No
         splits, mps = patch_plan(cfg, B, Ho, Npad, Cs)
     else:
         TN, TK, MCH = WGRAD_TILES[cfg]
-        if Kpad % TK:
+        if not wgrad_ktiles(cfg, Kpad):
             raise ValueError(f"wgrad config {cfg} (TK={TK}) does not tile the padded reduction {Kpad}")
         M = B * Ho * Wo
-        tiles = math.ceil(Npad / TN) * (Kpad // TK)
+        tiles = math.ceil(Npad / TN) * wgrad_ktiles(cfg, Kpad)
         if splits is None:
             splits = max(1, min(math.ceil(M / MCH), math.ceil(512 / tiles)))
         mps = _pad(math.ceil(M / splits), MCH)

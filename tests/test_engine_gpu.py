@@ -185,9 +185,24 @@ def test_graph_replay_matches_eager():
     assert torch.equal(params[2][0], params[0][0]) and torch.equal(params[1][0], params[0][0])
 
 
+def _force_big_wgrad(prog):
+    """Every conv whose reduction allows it on a large-tile weight-gradient config (32-35, rotating)."""
+    i = 0
+    for l in prog.bwd.launches:
+        if l.name == "conv_wgrad":
+            c = 32 + i % 4
+            i += 1
+            if l.owner.wgrad_valid(c):
+                l.owner.set_wgrad_cfg(c)
+                l.args = (c,) + tuple(l.args[1:])
+    return i
+
+
 @pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
-def test_batched_wgrad_bitwise_equal(model_name):
-    """One launch per tile config computes exactly what the per-conv launches compute."""
+@pytest.mark.parametrize("big", [False, True])
+def test_batched_wgrad_bitwise_equal(model_name, big):
+    """One launch per tile config computes exactly what the per-conv launches compute (also with every
+    conv on the large-tile configs, whose gradients must match the default configs' to fp32 order)."""
     from mtl_das_pytorch_amd.models import build_model, encode_joint
     from mtl_das_pytorch_amd.data.synthetic import generate
     grads = []
@@ -200,6 +215,8 @@ def test_batched_wgrad_bitwise_equal(model_name):
         else:
             from mtl_das_pytorch_amd.engine.mtl import MTLProgram
             prog = MTLProgram(m, 8, "cuda")
+        if big:
+            assert _force_big_wgrad(prog) > 0
         if batched:
             prog.batch_wgrads()
         X, d, e = generate(16, seed=1, device="cuda")

@@ -262,3 +262,30 @@ def test_backward_with_allreduce_structure(nb):
         covered += t.numel()
         assert ph.launches.index(a) > ph.launches.index(f)
     assert covered == p.flat.numel
+
+
+@pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
+def test_spill_wgrads(model):
+    """The earliest stream-0 weight gradients move to the spill stream: their batch waits for the spill
+    point, sits right after it in capture order, and the finalize waits for it."""
+    from mtl_das_pytorch_amd.engine.program import SPILL_STREAM
+    from mtl_das_pytorch_amd.models import build_model
+    m = build_model(model)
+    if model == "multi_classifier":
+        from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+        p = InceptionProgram(m, 32, "cpu")
+    else:
+        p = MTLProgram(m, 32, "cpu")
+    n0 = sum(1 for l in p.bwd.launches if l.name == "conv_wgrad" and l.stream == 0)
+    n = p.spill_wgrads(0.7)
+    assert 0 < n < n0
+    p.merge_wgrad_cfgs()
+    p.batch_wgrads()
+    _check_event_order(p.bwd)
+    ls = p.bwd.launches
+    fork = next(i for i, l in enumerate(ls) if l.record == "wgspill")
+    sp = [i for i, l in enumerate(ls) if l.stream == SPILL_STREAM]
+    assert sp and sp[0] == fork + 1 and ls[sp[0]].waits == ("wgspill",)
+    assert all(l.name == "wgrad_batched" for l in (ls[i] for i in sp))
+    fin = next(l for l in ls if l.name == "wgrad_finalize")
+    assert f"wgrads_s{SPILL_STREAM}" in fin.waits

@@ -39,3 +39,77 @@ if [ "$what" = prof ]; then
   step kernels_C python tools/prof_summary.py gpurun_out/prof_C 6 && \
   step timelineA timeout -k 10 200 python tools/timeline.py MTL
 fi
+if [ "$what" = wgbig ]; then
+  # large-tile weight-gradient kernels: numerics, then re-time every wgrad choice and bench before / after
+  step wgtests timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_engine_gpu.py \
+      -k "big or batched_wgrad" -v --timeout 120 --timeout-method thread && \
+  step benchA0 timeout -k 10 200 python bench.py --steps 300 --warmup 30 && \
+  step benchC0 timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 && \
+  step retune_wg timeout -k 10 900 python -u tools/retune.py --keep --drop wgrad \
+      --models MTL,single_event,single_distance,multi_classifier --out gpurun_out/tuned_wg.json && \
+  cp gpurun_out/tuned_wg.json mtl_das_pytorch_amd/engine/tuned_cfgs.json && \
+  step benchA_wg timeout -k 10 200 python bench.py --steps 300 --warmup 30 && \
+  step benchC_wg timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 && \
+  step phaseC_wg timeout -k 10 300 python tools/phase_times.py multi_classifier && \
+  step benchA_upb0 env MDA_PATCH_UPB=0 timeout -k 10 200 python bench.py --steps 300 --warmup 30
+fi
+if [ "$what" = upb ]; then
+  # same-box A/B of the patch wgrad unit cap (ops/functional.py PATCH_MAX_UNITS)
+  for r in 1 2; do
+    for u in 3 0; do
+      step benchA_upb${u}_$r env MDA_PATCH_UPB=$u timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 || exit $?
+    done
+  done
+  for u in 3 0; do
+    step benchC_upb${u} env MDA_PATCH_UPB=$u timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
+  done
+fi
+if [ "$what" = wgassign ]; then
+  step wgassignC timeout -k 10 400 python -u tools/wgrad_assign.py multi_classifier table,big,table,big --min-px 256,1024 && \
+  step wgassignA timeout -k 10 300 python -u tools/wgrad_assign.py MTL table,big,bigall --min-px 256
+fi
+if [ "$what" = wgtune ]; then
+  # weight-gradient configs chosen by their batched launches' time, then A / C benches on the new table
+  step benchA_pre timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+  step benchC_pre timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 && \
+  step wgtune timeout -k 10 900 python -u tools/retune.py --keep --wgrad-batches \
+      --models MTL,multi_classifier --out gpurun_out/tuned_wgb.json && \
+  cp gpurun_out/tuned_wgb.json mtl_das_pytorch_amd/engine/tuned_cfgs.json && \
+  step benchA_wgb timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+  step benchC_wgb timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 && \
+  step wgjobsC timeout -k 10 300 python tools/wgrad_assign.py multi_classifier table --min-px 256
+fi
+if [ "$what" = spill ]; then
+  # share of stream 0's weight gradients moved to the spill stream (engine/lowering.py spill_wgrads)
+  for f in 0 0.3 0.5 0.7 0.85 0; do
+    step benchA_spill$f env MDA_WGSPILL=$f timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 || exit $?
+  done
+  for f in 0 0.5 0.7 0.9 0; do
+    step benchC_spill$f env MDA_WGSPILL=$f timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
+  done
+fi
+if [ "$what" = spill2 ]; then
+  # spilled weight gradients with their blocks per CU capped by extra LDS (MDA_SPILL_LDS bytes)
+  for cfg in "0 0" "0.5 98304" "0.85 98304" "0.85 65536" "0.5 65536" "0.85 0" "0 0"; do
+    set -- $cfg
+    step benchA_spill$1_lds$2 env MDA_WGSPILL=$1 MDA_SPILL_LDS=$2 timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 || exit $?
+  done
+fi
+if [ "$what" = spill3 ]; then
+  for f in 0 0.5 0.7 0.85 0; do
+    step benchA_sp$f env MDA_WGSPILL=$f MDA_SPILL_LDS=0 timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 || exit $?
+  done
+  step benchA_sp0.7_lds env MDA_WGSPILL=0.7 timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+  MDA_WGSPILL=0.7 MDA_SPILL_LDS=0 step tl_sp70 timeout -k 10 200 python tools/timeline.py MTL bwd,adam && \
+  for f in 0 0.7 0.9; do
+    step benchC_sp$f env MDA_WGSPILL=$f MDA_SPILL_LDS=0 timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
+  done
+fi
+if [ "$what" = wg0 ]; then
+  for v in 0 1 0 1; do
+    step benchA_wg0_$v env MDA_WG_STREAM0=$v timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 || exit $?
+  done
+  for v in 0 1; do
+    step benchC_wg0_$v env MDA_WG_STREAM0=$v timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
+  done
+fi
