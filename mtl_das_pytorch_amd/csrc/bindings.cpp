@@ -258,6 +258,30 @@ TailArgs parse_tail(const py::dict& d) {
 void tail_fwd(int kind, int G, int blocks, int64_t stream, py::dict d) {
   check(launch_tail_fwd(kind, parse_tail(d), G, blocks, S(stream)), "tail_fwd");
 }
+
+// Packs the TailJob table of a batched forward-tail launch; returns (bytes, total blocks, largest C).
+py::tuple tail_table(py::list dicts, py::list blocks) {
+  std::vector<TailJob> jobs(dicts.size());
+  int64_t b0 = 0;
+  int maxC = 0;
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    TailJob& j = jobs[i];
+    j = TailJob{};
+    j.a = parse_tail(dicts[i].cast<py::dict>());
+    j.blocks = blocks[i].cast<int>();
+    if (j.blocks <= 0 || j.a.C % 8 || j.a.r || j.a.r_bn) throw std::runtime_error("tail_table: unsupported tail");
+    j.block0 = (int)b0;
+    b0 += j.blocks;
+    maxC = std::max(maxC, j.a.C);
+  }
+  if (b0 >= (1ll << 31)) throw std::runtime_error("tail_table: too many blocks");
+  return py::make_tuple(py::bytes(reinterpret_cast<const char*>(jobs.data()), jobs.size() * sizeof(TailJob)), b0, maxC);
+}
+
+void tail_fwd_batched(int kind, int64_t table, int nj, int64_t nblocks, int maxC, int64_t stream) {
+  check(launch_tail_fwd_batched(kind, reinterpret_cast<const TailJob*>(static_cast<intptr_t>(table)), nj, (int)nblocks,
+                                maxC, S(stream)), "tail_fwd_batched");
+}
 void tail_bwd(int kind, int G, int blocks, int64_t stream, py::dict d) {
   check(launch_tail_bwd(kind, parse_tail(d), G, blocks, (int)I(d, "fused", 0), S(stream)), "tail_bwd");
 }
@@ -371,6 +395,8 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("wgrad", &wgrad);
   m.def("wgrad_finalize", &wgrad_finalize);
   m.def("tail_fwd", &tail_fwd);
+  m.def("tail_table", &tail_table);
+  m.def("tail_fwd_batched", &tail_fwd_batched);
   m.def("tail_bwd", &tail_bwd);
   m.def("mtl_head", &mtl_head);
   m.def("cls_head", &cls_head);

@@ -56,15 +56,16 @@ struct Lanes {
   }
 };
 
+// bx / nbx: this block's index among the tail's blocks and their count (the grid's x, or a job's share of a
+// batched launch)
 template <int KIND>
-DEV void tail_fwd_impl(const TailArgs& a) {
+DEV void tail_fwd_impl(const TailArgs& a, const int bx, const int nbx, const int z) {
   extern __shared__ float sm[];
   float* s_sc = sm;
   float* s_sh = sm + a.C;
   float* s_sc2 = sm + 2 * a.C;
   float* s_sh2 = sm + 3 * a.C;
-  const int z = blockIdx.z;
-  const bool upd = blockIdx.x == 0;
+  const bool upd = bx == 0;
   bn_prepare(a.bn, z, s_sc, s_sh, nullptr, nullptr, upd);
   if (KIND == ADD_RELU2) bn_prepare(a.bn2, z, s_sc2, s_sh2, nullptr, nullptr, upd);
   __syncthreads();
@@ -80,7 +81,7 @@ DEV void tail_fwd_impl(const TailArgs& a) {
   if (KIND == POOL_RELU) {
     const int Hp = (a.H + 1) >> 1, Wp = (a.W + 1) >> 1;
     const int Mp = a.B * Hp * Wp;
-    for (int p = blockIdx.x * L.PL + L.pl; p < Mp; p += gridDim.x * L.PL) {
+    for (int p = bx * L.PL + L.pl; p < Mp; p += nbx * L.PL) {
       int b = p / (Hp * Wp), r = p - b * Hp * Wp;
       int hp = r / Wp, wp = r - hp * Wp;
       float mx[8];
@@ -114,8 +115,8 @@ DEV void tail_fwd_impl(const TailArgs& a) {
   // inputs as far as the compiler knows, so a one-pixel loop keeps one pixel's loads in flight per thread
   // (the large maps -- Model C's 47x122 stem -- then ran at ~2 TB/s)
   constexpr bool RES = KIND == SIGMUL || is_add<KIND>();
-  const int step = gridDim.x * L.PL;
-  for (int p = blockIdx.x * L.PL + L.pl; p < M; p += 2 * step) {
+  const int step = nbx * L.PL;
+  for (int p = bx * L.PL + L.pl; p < M; p += 2 * step) {
     const int p2 = p + step;
     const bool has2 = p2 < M;
     const int q2 = has2 ? p2 : p;
@@ -164,7 +165,19 @@ DEV void tail_fwd_impl(const TailArgs& a) {
 // (round 3), 8 waves +170 us on Model A's forward (round 2; docs/PERF.md).
 template <int KIND>
 __global__ __launch_bounds__(256) void tail_fwd_kernel(TailArgs a) {
-  tail_fwd_impl<KIND>(a);
+  tail_fwd_impl<KIND>(a, blockIdx.x, gridDim.x, blockIdx.z);
+}
+
+// Several tails of one kind in one launch (engine/inception.py: the BN+ReLU tails of an Inception block's
+// branch outputs, which all land in the block's concat buffer and are only read by the next block): block ->
+// job by binary search over the jobs' first blocks.  The branch streams each ended in their own small tail
+// (Model C: 44 launches of 4-8 us on 4x13 / 1x6 maps); one launch after the block's join does them all.
+template <int KIND>
+__global__ __launch_bounds__(256) void tail_fwd_batched_kernel(const TailJob* __restrict__ jobs, int nj) {
+  int lo = 0, hi = nj - 1;
+  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= (int)blockIdx.x) lo = mid; else hi = mid - 1; }
+  const TailJob& J = jobs[lo];
+  tail_fwd_impl<KIND>(J.a, (int)blockIdx.x - J.block0, J.blocks, 0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -576,6 +589,18 @@ int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t 
     K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID) K(SIGMUL) K(POOL_RELU) K(ADD_RELU) K(ADD_RELU2)
 #undef K
     default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_tail_fwd_batched(int kind, const TailJob* d_jobs, int nj, int nblocks, int maxC, hipStream_t st) {
+  if (nblocks <= 0) return 0;
+  const size_t lds = (size_t)4 * maxC * sizeof(float);
+#define K(X) case X: hipLaunchKernelGGL(tail_fwd_batched_kernel<X>, dim3(nblocks), dim3(256), lds, st, d_jobs, nj); break;
+  switch (kind) {
+    K(ACT_NONE) K(ACT_RELU) K(ACT_SIGMOID)
+#undef K
+    default: return -1;  // kinds with a second operand or a pooled grid are not batched
   }
   return (int)hipGetLastError();
 }

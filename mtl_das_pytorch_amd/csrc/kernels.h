@@ -170,6 +170,12 @@ struct TailArgs {
   float gscale;                     // factor on the d(gamma), d(beta) the apply writes (SyncBN: 1 / world)
 };
 
+struct TailJob {  // one tail of a batched forward-tail launch (bn.hip tail_fwd_batched_kernel)
+  TailArgs a;
+  int blocks;      // blocks of this tail (its grid x), one group (z = 0)
+  int block0;      // first block of this tail in the batched grid
+};
+
 struct HeadArgs {
   const bf16_t* feat; int64_t fgs; int ldf;  // per task [B*HW][C] (+ t * fgs)
   const int64_t* labels; int lab_stride, lab_off;  // label of (b, t) = labels[b*lab_stride + lab_off + t]
@@ -214,7 +220,7 @@ struct PoolArgs {
 
 struct OptSeg {
   int64_t off, n;
-  int kind;  // 1 = forward image of a conv weight, 2 = data-gradient image (pack_kernel)
+  int kind;  // 0 = plain flat range, 3 = conv weight with both images (optim.hip adam_pack_kernel)
   bf16_t* wf;
   bf16_t* wd;
   int Co, Ci, KH, KW, Cs, Kpad_f, Kpad_d;
@@ -226,16 +232,11 @@ struct OptSeg {
   int64_t block0;
 };
 
-// Data-gradient image pack tiles (optim.hip pack_dgrad_tile): 64 co x cit ci, cit*taps <= PACK_ROWS LDS rows;
-// keep in sync with engine/core.py build_optseg_table.
-constexpr int PACK_ROWS = 72;
-__host__ __device__ inline int pack_dgrad_cit(int taps) { return std::min(32, PACK_ROWS / taps); }
-// Forward image pack (optim.hip pack_fwd_rows): a block stages up to PACK_FWD_FLOATS contiguous master
-// floats = whole co rows (at least one) in LDS; rows of more than PACK_FWD_FLOATS floats are not supported.
-constexpr int PACK_FWD_FLOATS = 4096;
-__host__ __device__ inline int pack_fwd_rows(int Ci, int taps, int Co) {
-  return std::max(1, std::min(Co, PACK_FWD_FLOATS / (Ci * taps)));
-}
+// Conv-weight tiles of the fused Adam + pack (optim.hip adam_pack_kernel): PACK_TCO co x pack_tile_ci(taps) ci x
+// all taps (~2K elements: 256 ci of a 1x1, 24 of a 3x3, 8 of a 7x7), staged in LDS rows of at most
+// PACK_TILE_FLOATS floats; keep in sync with engine/core.py build_optseg_table.
+constexpr int PACK_TCO = 8, PACK_TILE_FLOATS = 512;
+__host__ __device__ inline int pack_tile_ci(int taps) { return std::max(8, (256 / taps) & ~7); }
 
 struct AdamArgs {
   float* p; const float* g; float* m; float* v;
@@ -273,6 +274,7 @@ int wgrad_ntiles(int cfg, const WgradArgs& a);  // tiles per group of a wgrad la
 int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st);
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);
+int launch_tail_fwd_batched(int kind, const TailJob* d_jobs, int nj, int nblocks, int maxC, hipStream_t st);
 int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, int fused, hipStream_t st);
 int launch_mtl_head(const HeadArgs& a, hipStream_t st);
 int launch_cls_head(const ClsArgs& a, int64_t* seed_mut, hipStream_t st);

@@ -483,8 +483,8 @@ class ConvLayer:
 
     # ---- packed weight images / optimizer descriptors ------------------------------------------
     def opt_segments(self) -> List[dict]:
-        """Pack jobs (csrc/optim.hip pack_kernel): the forward and data-gradient bf16 images of every
-        group member, rebuilt from the fp32 masters after each optimizer step."""
+        """Optimizer jobs (csrc/optim.hip adam_pack_kernel, kind 3): every member weight's Adam update and
+        its forward and data-gradient bf16 images, rebuilt from the updated fp32 masters each step."""
         segs = []
         if self.concat:
             # member rows [n0, n0 + Co) of the forward image, its taps at the group's tap offset t0 (a centre-tap
@@ -492,18 +492,15 @@ class ConvLayer:
             # (tap stride = the group's Co)
             for m, n0, t0 in self.members:
                 kh, kw = m.kernel_size
-                common = {"off": self.flat.off(m.weight), "Co": m.out_channels, "Ci": self.Ci, "KH": kh, "KW": kw,
-                          "Cs": self.Cs, "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d, "tap_ld": self.Co,
-                          "kext_f": kh * kw * self.Cs if t0 else 0}
-                segs.append(dict(common, kind=1, n=m.out_channels * self.Kpad, wf=P(self.wf, n0 * self.Kpad + t0 * self.Cs)))
-                segs.append(dict(common, kind=2, n=self.Npad_d * self.Kpad_d, wd=P(self.wd, t0 * self.Co + n0)))
+                segs.append({"kind": 3, "off": self.flat.off(m.weight), "n": m.weight.numel(), "Co": m.out_channels,
+                             "Ci": self.Ci, "KH": kh, "KW": kw, "Cs": self.Cs, "Kpad_f": self.Kpad,
+                             "Kpad_d": self.Kpad_d, "tap_ld": self.Co, "kext_f": kh * kw * self.Cs if t0 else 0,
+                             "wf": P(self.wf, n0 * self.Kpad + t0 * self.Cs), "wd": P(self.wd, t0 * self.Co + n0)})
             return segs
         for g, m in enumerate(self.mods):
-            common = {"off": self.flat.off(m.weight), "Co": self.Co, "Ci": self.Ci, "KH": self.KH, "KW": self.KW,
-                      "Cs": self.Cs, "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d}
-            segs.append(dict(common, kind=1, n=self.Npad * self.Kpad, wf=P(self.wf, g * self.Npad * self.Kpad)))
-            segs.append(dict(common, kind=2, n=self.Npad_d * self.Kpad_d,
-                             wd=P(self.wd, g * self.Npad_d * self.Kpad_d)))
+            segs.append({"kind": 3, "off": self.flat.off(m.weight), "n": m.weight.numel(), "Co": self.Co, "Ci": self.Ci,
+                         "KH": self.KH, "KW": self.KW, "Cs": self.Cs, "Kpad_f": self.Kpad, "Kpad_d": self.Kpad_d,
+                         "wf": P(self.wf, g * self.Npad * self.Kpad), "wd": P(self.wd, g * self.Npad_d * self.Kpad_d)})
         return segs
 
     def finalize_descs(self) -> List[dict]:
@@ -594,8 +591,29 @@ def build_wgfin_table(descs: List[dict], device) -> tuple:
     return t, len(descs), b0
 
 
-PACK_ROWS = 72  # csrc/kernels.h
-PACK_FWD_FLOATS = 4096  # csrc/kernels.h
+PACK_TCO, PACK_TILE_FLOATS = 8, 512  # csrc/kernels.h
+
+
+def pack_tile_ci(taps: int) -> int:
+    return max(8, (256 // taps) & ~7)
+
+
+def optimizer_segments(conv_segs: List[dict], numel: int) -> List[dict]:
+    """The fused optimizer's segments: the conv weights' tiles (kind 3) plus plain Adam ranges (kind 0)
+    covering every other element of the flat buffer, each element exactly once, in flat order."""
+    segs, pos = [], 0
+    for s in sorted(conv_segs, key=lambda s: s["off"]):
+        if s["off"] < pos:
+            raise ValueError(f"optimizer segments overlap at flat offset {s['off']}")
+        if s["off"] > pos:
+            segs.append({"kind": 0, "off": pos, "n": s["off"] - pos})
+        segs.append(s)
+        pos = s["off"] + s["n"]
+    if pos > numel:
+        raise ValueError("optimizer segments run past the flat buffer")
+    if pos < numel:
+        segs.append({"kind": 0, "off": pos, "n": numel - pos})
+    return segs
 
 
 def build_optseg_table(segs: List[dict], device) -> tuple:
@@ -611,17 +629,12 @@ def build_optseg_table(segs: List[dict], device) -> tuple:
         arr[i]["block0"] = b0
         if s["kind"] == 0:  # plain Adam range, 1024 elements per block
             b0 += math.ceil(s["n"] / 1024)
-        elif s["kind"] == 2:  # LDS-transposed tiles of 64 co x cit ci (csrc/optim.hip pack_dgrad_tile)
+        else:  # (8 co) x (ci tile) x all taps through LDS (csrc/optim.hip adam_pack_kernel)
             taps = s["KH"] * s["KW"]
-            if taps > PACK_ROWS:
-                raise ValueError(f"pack: {taps} taps exceed the {PACK_ROWS} LDS rows of a tile")
-            cit = min(32, PACK_ROWS // taps)
-            b0 += math.ceil(s["Co"] / 64) * math.ceil(s["Ci"] / cit)
-        else:  # whole co rows staged in LDS (csrc/optim.hip pack_fwd_rows_block)
-            row = s["Ci"] * s["KH"] * s["KW"]
-            if row > PACK_FWD_FLOATS:
-                raise ValueError(f"pack: a {row}-float weight row exceeds the {PACK_FWD_FLOATS}-float LDS stage")
-            rb = max(1, min(s["Co"], PACK_FWD_FLOATS // row))
-            b0 += math.ceil(s["Co"] / rb)
+            if 8 * taps > PACK_TILE_FLOATS:
+                raise ValueError(f"pack: {taps} taps exceed the {PACK_TILE_FLOATS}-float LDS tile")
+            if s["n"] != s["Co"] * s["Ci"] * taps:
+                raise ValueError("pack: a conv segment must cover its whole weight")
+            b0 += math.ceil(s["Co"] / PACK_TCO) * math.ceil(s["Ci"] / pack_tile_ci(taps))
     t = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
     return t, len(segs), b0

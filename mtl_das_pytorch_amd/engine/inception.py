@@ -18,6 +18,7 @@ Launch counts per training step (B fixed): forward 94 conv + 94 tails + 13 pools
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -80,6 +81,7 @@ class CBR:
                              f"destination {(out.act.H, out.act.W, out.act.C)}")
         self.nol_from: Optional["CBR"] = None  # producer whose BN+ReLU this conv applies on load
         self.skip_tail = False                 # the (single) consumer normalises self.y on load
+        self.defer_tail = False                # the tail joins its block's batched tail launch
 
     def _src(self):
         if self.nol_from is not None:
@@ -90,7 +92,9 @@ class CBR:
         if self.conv is not None:
             src, nol = self._src()
             prog._conv_fwd(ph, self.conv, src, self.y, self.bn, training, nol=nol)
-        if not self.skip_tail:
+        if self.defer_tail:
+            prog._pending_tails.append(prog._tail_args(self.y, self.bn, self.out.act, training))
+        elif not self.skip_tail:
             prog._tail(ph, ACT_RELU, 1, self.y, self.bn, self.out.act, training)
 
     def backward(self, prog, ph: Phase):
@@ -255,7 +259,6 @@ class InceptionProgram(LoweredProgram):
 
     def hfuse_enabled(self) -> bool:
         """Horizontal fusion of sibling 1x1 convs (HConv; MDA_HFUSE=0 lowers every BasicConv2d on its own)."""
-        import os
         return os.environ.get("MDA_HFUSE", "1") == "1"
 
     def _hconv(self, bcs: List[BasicConv2d], src: Val, outs: List[Optional[Val]], branches: List[int]) -> List[Val]:
@@ -385,6 +388,7 @@ class InceptionProgram(LoweredProgram):
         self.nvalid = torch.full((1,), B, device=self.device, dtype=torch.int64)
         self.convs: List[ConvLayer] = [op.conv for op in self.ops if getattr(op, "conv", None) is not None]
         self._plan_nol()
+        self._plan_tail_batches()
 
     def set_rng_stream(self, seed: int, rank: int = 0):
         """Select the dropout RNG stream (high word of the device counter; the low word counts training
@@ -395,6 +399,24 @@ class InceptionProgram(LoweredProgram):
     # the stem's 47x122 and 21x58 convs keep their BN+ReLU tails (C at bs 32: 7.55k -> 7.66k samples/s,
     # three runs each of a limit of all / 1e5 / 3e4 output pixels)
     NOL_MAX_PX = 30000
+
+    def tail_batch_enabled(self) -> bool:
+        """One batched BN+ReLU tail launch per Inception block (MDA_TAIL_BATCH=0: a tail per branch output)."""
+        return os.environ.get("MDA_TAIL_BATCH", "1") == "1"
+
+    def _plan_tail_batches(self):
+        """The BN+ReLU tails of an Inception block's branch outputs -- channel slices of the block's concat
+        buffer, read only by the next block -- run as ONE launch after the block's branches join
+        (_emit_streamed) instead of one per branch at the end of each branch stream."""
+        self._pending_tails: List[tuple] = []
+        self.n_tail_batched = 0
+        if not self.tail_batch_enabled():
+            return
+        for i, op in enumerate(self.ops):
+            if (isinstance(op, CBR) and not op.skip_tail and op.out.parent is not None
+                    and self.op_meta[i] is not None):
+                op.defer_tail = True
+                self.n_tail_batched += 1
 
     def _plan_nol(self):
         """Normalise-on-load: a BasicConv2d output consumed by exactly one other BasicConv2d (and not a
@@ -456,6 +478,12 @@ class InceptionProgram(LoweredProgram):
                 tag = f"{ph.name}_e{cur_block}_{st}"
                 ph.mark(tag)
                 owed0.append(tag)
+            if self._pending_tails:  # the block's deferred branch-output tails, after the join, on stream 0
+                ph.cur_stream = 0
+                ph.pending_waits.extend(owed0)
+                owed0 = []
+                self._tail_batch(ph, ACT_RELU, self._pending_tails)
+                self._pending_tails = []
             cur_block, used = None, set()
 
         for i in order:

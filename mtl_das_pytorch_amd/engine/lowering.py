@@ -9,8 +9,10 @@ import torch
 
 from ..ops.functional import WGRAD_PATCH, WGRAD_TILES, wgrad_ktiles
 from ..ops.hip import lib
-from .core import GRAD_DT, Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, pad_to
-from .program import (COMM_STREAM, SPILL_STREAM, Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd, k_wgfin, k_wgrad,
+from .core import (GRAD_DT, Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, optimizer_segments,
+                   pad_to)
+from .program import (COMM_STREAM, SPILL_STREAM, Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd,
+                      k_tail_fwd_batched, k_wgfin, k_wgrad,
                       k_wgrad_batched)
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, SIGMUL, ADD_RELU, POOL_RELU = range(6)
@@ -71,6 +73,20 @@ class LoweredProgram:
         return 1 if world <= 1 else int(os.environ.get("MDA_BUCKETS", str(self.default_buckets)))
 
     # -------------------------------------------------------------------------------------------
+    def _tail_args(self, y: Act, bn: BNLayer, out: Act, training: bool, H=None, W=None) -> tuple:
+        d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(training), "out": out.p, "ogs": out.gs, "ldo": out.ld,
+             "B": self.B, "H": y.H if H is None else H, "W": y.W if W is None else W, "C": y.C}
+        return d, _blocks(self.B * d["H"] * d["W"], y.C, per_thread=2)
+
+    def _tail_batch(self, ph: Phase, kind: int, jobs: List[tuple]):
+        """One launch for several single-group forward tails of one kind (``jobs``: (args, blocks) from
+        _tail_args; csrc/bn.hip tail_fwd_batched_kernel)."""
+        raw, nblocks, max_c = lib().tail_table([d for d, _ in jobs], [b for _, b in jobs])
+        table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+        self._tail_tables = getattr(self, "_tail_tables", [])
+        self._tail_tables.append(table)  # alive as long as the program (captured graphs point at it)
+        ph.add(f"tailbatch{kind}", k_tail_fwd_batched, kind, table, len(jobs), nblocks, max_c, owner=jobs)
+
     def _tail(self, ph: Phase, kind: int, G: int, y: Act, bn: BNLayer, out: Act, training: bool, r: Act = None,
               bn2: BNLayer = None, H=None, W=None):
         d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(training), "out": out.p, "ogs": out.gs, "ldo": out.ld,
@@ -669,9 +685,10 @@ class LoweredProgram:
         self.wgrads_batched = True
 
     def _emit_optimizer(self, grad_scale: float = 1.0) -> Dict[str, Phase]:
-        segs = [s for c in self.convs for s in c.opt_segments()]
-        self.optseg_table, ns, nblocks = build_optseg_table(segs, self.device)
         f = self.flat
+        segs = optimizer_segments([s for c in self.convs for s in c.opt_segments()], f.numel)
+        self.opt_segs = segs
+        self.optseg_table, ns, nblocks = build_optseg_table(segs, self.device)
         base = {"p": P(f.params), "g": P(f.grads), "m": P(f.exp_avg), "v": P(f.exp_avg_sq), "n": f.numel,
                 "lr": P(f.lr), "step": P(f.step), "segs": P(self.optseg_table), "nsegs": ns, "nblocks": nblocks}
         self._opt_base = base

@@ -170,6 +170,10 @@ def k_tail_fwd(kind, G, blocks, d, st):
     lib().tail_fwd(kind, G, blocks, st, d)
 
 
+def k_tail_fwd_batched(kind, table, nj, nblocks, max_c, st):
+    lib().tail_fwd_batched(kind, table.data_ptr(), nj, nblocks, max_c, st)
+
+
 def k_tail_bwd(kind, G, blocks, d, st):
     lib().tail_bwd(kind, G, blocks, st, d)
 

@@ -159,7 +159,15 @@ def _rccl_options():
     communicator's stream can BE a stream the step graph captures on, and the watchdog's poll of an eager
     collective's event recorded there fails during the capture ("event last recorded in a capturing stream",
     seen on Model C's 4-stream step).  A separate pool keeps them apart; priority also puts the collectives'
-    kernels ahead of compute in the queues, as wanted for overlapped gradient buckets."""
+    kernels ahead of compute in the queues, as wanted for overlapped gradient buckets.
+
+    Also turns off ProcessGroupNCCL's process-wide event cache (TORCH_NCCL_CUDA_EVENT_CACHE=0, read when a
+    group is constructed): it recycles the start / end events of finished works across ALL groups, so an
+    event the capture group recorded inside a graph capture could come back as an eager work's event of the
+    default group, and the watchdog's query of an event of that work that was not re-recorded (the start
+    event is only recorded with timing on) fails with the same "event last recorded in a capturing stream"
+    -- an intermittent abort of the 1-rank DP test, depending on which cached event a work drew."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
     return dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
 
 

@@ -40,7 +40,10 @@ def test_mtl_program_structure():
     # shared backbone input read with group stride 0, per-task prev level with stride > 0
     assert L["Fa"].gs == 0 and L["prevB"].gs > 0
     assert p.wgfin_table.numel() == (len(p.convs) + 3) * 88  # one finalize descriptor per fused member
-    assert p.optseg_table.numel() == 2 * (sum(c.G for c in p.convs) + 3) * 88
+    # fused optimizer: one segment per conv weight (both images), plain ranges for the rest; exact cover
+    assert sum(s["kind"] == 3 for s in p.opt_segs) == sum(c.G for c in p.convs) + 3
+    assert sum(s["n"] for s in p.opt_segs) == p.flat.numel and p.optseg_table.numel() == len(p.opt_segs) * 88
+    assert all(a["off"] + a["n"] == b["off"] for a, b in zip(p.opt_segs, p.opt_segs[1:]))
 
 
 def test_single_task_program():
@@ -81,7 +84,8 @@ def test_inception_program_structure():
     n_conv = 94 - sum(len(h.members) - 1 for h in hcs)  # conv launches: one per fused group
     assert n_conv == 94 - 19 == len(p.convs)
     kernels = lambda ph: sum(1 for l in ph.launches if l.fn is not None)  # not the fork points
-    assert kernels(p.fwd_train) == n_conv + 94 + 13 + 1 - p.n_nol  # tails folded into their consumer conv
+    # tails folded into their consumer conv; the blocks' branch-output tails batched one launch per block
+    assert kernels(p.fwd_train) == n_conv + 94 + 13 + 1 - p.n_nol - p.n_tail_batched + 11
     assert kernels(p.bwd) == 94 + 2 * n_conv - 1 + 13 + 1   # the stem conv has no data gradient
     # Mixed_5b's 1x1 branch writes channels [0, 64) of the 256-wide block buffer in place; its pre-BN y is a
     # slice of the fused group's output, its BN sums a slice of the group's combined replica rows
@@ -289,3 +293,36 @@ def test_spill_wgrads(model):
     assert all(l.name == "wgrad_batched" for l in (ls[i] for i in sp))
     fin = next(l for l in ls if l.name == "wgrad_finalize")
     assert f"wgrads_s{SPILL_STREAM}" in fin.waits
+
+
+def test_inception_tail_batches_structure():
+    """Model C's forward: every Inception block's branch-output tails in one launch after the join."""
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.models import build_model
+    p = InceptionProgram(build_model("multi_classifier"), 32, "cpu")
+    names = [l.name for l in p.fwd_train.launches]
+    assert names.count("tailbatch1") == 11 and names.count("tail1") + names.count("tailbatch1") <= 30
+    assert sum(len(l.owner) for l in p.fwd_train.launches if l.name == "tailbatch1") == p.n_tail_batched == 44
+    for ph in (p.fwd_train, p.fwd_eval):
+        _check_event_order(ph)
+        for l in ph.launches:
+            if l.name == "tailbatch1":
+                assert l.stream == 0
+
+
+@pytest.mark.parametrize("model", ["single_event", "multi_classifier"])
+def test_optimizer_segments_cover_flat(model):
+    """The fused Adam + pack covers every flat element exactly once: one tile segment per conv weight
+    (both of its bf16 images), plain ranges in between."""
+    from mtl_das_pytorch_amd.models import build_model
+    m = build_model(model)
+    if model == "multi_classifier":
+        from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+        p = InceptionProgram(m, 8, "cpu")
+    else:
+        p = MTLProgram(m, 8, "cpu")
+    segs = p.opt_segs
+    assert segs[0]["off"] == 0 and sum(s["n"] for s in segs) == p.flat.numel
+    assert all(a["off"] + a["n"] == b["off"] for a, b in zip(segs, segs[1:]))
+    convw = {p.flat.off(mod.weight) for c in p.convs for mod in c.mods}
+    assert {s["off"] for s in segs if s["kind"] == 3} == convw

@@ -274,3 +274,18 @@ def test_inception_graph_learns_fixed_batch():
     print("losses", [round(l, 3) for l in losses])
     assert all(map(lambda v: v == v, losses))
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+def test_inception_tail_batches_bitwise(monkeypatch):
+    """One batched BN+ReLU tail launch per Inception block (engine/inception.py _plan_tail_batches) computes
+    exactly what the per-branch tails compute: forward outputs, running statistics and gradients bitwise."""
+    out = []
+    for batched in ("0", "1"):
+        monkeypatch.setenv("MDA_TAIL_BATCH", batched)
+        model, ref, prog, X, labels = _setup(B=8, seed=3)
+        assert (prog.n_tail_batched > 0) == (batched == "1")
+        _engine_step(prog, X, labels, torch.arange(8, device="cuda"))
+        f = prog.flat
+        out.append((prog.logp.clone(), f.grads.clone(), f.bn_mean.clone(), f.bn_var.clone()))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)

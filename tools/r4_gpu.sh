@@ -113,3 +113,28 @@ if [ "$what" = wg0 ]; then
     step benchC_wg0_$v env MDA_WG_STREAM0=$v timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
   done
 fi
+if [ "$what" = opt ]; then
+  step opttests timeout -k 10 500 python -u -m pytest tests/test_engine_gpu.py tests/test_rccl_gpu.py tests/test_mtl_layer_local_gpu.py \
+      -x -v --timeout 120 --timeout-method thread && \
+  step benchA timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+  step phaseA timeout -k 10 200 python tools/phase_times.py MTL && \
+  step benchC timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 && \
+  step phaseC timeout -k 10 300 python tools/phase_times.py multi_classifier
+fi
+if [ "$what" = scratch ]; then
+  # verdict item 7: the whole table re-derived from an EMPTY table (isolated, then in-context for A and C)
+  step scratch timeout -k 10 1100 python -u tools/retune.py --models MTL,single_event,single_distance,multi_classifier \
+      --in-context --topk 3 --passes cfg,tail --out gpurun_out/tuned_scratch.json
+fi
+if [ "$what" = scratch_ab ]; then
+  # shipped table vs the from-scratch one, interleaved on one box
+  for r in 1 2; do
+    step benchA_ship$r timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+    step benchA_scr$r env MDA_TUNED_CFGS=gpurun_out/tuned_scratch.json timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+    step benchC_ship$r timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 && \
+    step benchC_scr$r env MDA_TUNED_CFGS=gpurun_out/tuned_scratch.json timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
+  done
+fi
+if [ "$what" = acc ]; then
+  step accuracy timeout -k 10 1100 python -u tools/accuracy_table.py --out gpurun_out/accuracy
+fi

@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--in-context", action="store_true")
     ap.add_argument("--topk", type=int, default=3)
+    ap.add_argument("--in-context-models", default="MTL,multi_classifier",
+                    help="models whose conv choices --in-context refines (Model B shares A's signatures)")
     ap.add_argument("--margin", type=float, default=0.002, help="in-context: relative step-time gain to keep a config")
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--drop", default="", help="with --keep: comma-separated key prefixes to re-measure (e.g. wgrad)")
@@ -87,7 +89,7 @@ def main():
             X, d, e = generate(4 * args.batch, seed=3, device="cuda")
             labels = encode_joint(d, e) if name == "multi_classifier" else torch.stack([d, e], 1)
             tune_spill(lambda: _make(name, args.batch), X, labels, cache)
-        if args.in_context:
+        if args.in_context and name in args.in_context_models.split(","):
             autotune_program(prog, cache=cache, measure=False)  # batch the weight gradients as the bench does
             X, d, e = generate(4 * args.batch, seed=3, device="cuda")
             labels = encode_joint(d, e) if name == "multi_classifier" else torch.stack([d, e], 1)
