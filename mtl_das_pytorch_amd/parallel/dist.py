@@ -80,8 +80,17 @@ class DistContext:
         if not self.enabled:
             return t
         if self.backend == "nccl":
-            # under capture: the capture-only communicator (see ``capture_group``)
-            dist.all_reduce(t, group=self.capture_group if torch.cuda.is_current_stream_capturing() else None)
+            if torch.cuda.is_current_stream_capturing():  # the capture-only communicator (see ``capture_group``)
+                dist.all_reduce(t, group=self.capture_group)
+            else:
+                # eager (the warm-up run before a capture among others): async on the group's own stream, the
+                # current stream waits for it.  A synchronous all_reduce runs on -- and records its work's
+                # events on -- the CURRENT stream, here an engine phase stream; the graph captured right after
+                # the warm-up captures on those same phase streams, and the watchdog's poll of the not yet
+                # retired eager work then queries an event of a stream that is capturing: "operation not
+                # permitted on an event last recorded in a capturing stream", an abort whose timing depended on
+                # the watchdog's 100 ms poll (the round-3 0.5 s sleep hid it; the 1-rank RCCL test failed ~1 in 3)
+                dist.all_reduce(t, async_op=True).wait()
             return t
         if t.device.type != "cuda":
             dist.all_reduce(t)
@@ -159,15 +168,7 @@ def _rccl_options():
     communicator's stream can BE a stream the step graph captures on, and the watchdog's poll of an eager
     collective's event recorded there fails during the capture ("event last recorded in a capturing stream",
     seen on Model C's 4-stream step).  A separate pool keeps them apart; priority also puts the collectives'
-    kernels ahead of compute in the queues, as wanted for overlapped gradient buckets.
-
-    Also turns off ProcessGroupNCCL's process-wide event cache (TORCH_NCCL_CUDA_EVENT_CACHE=0, read when a
-    group is constructed): it recycles the start / end events of finished works across ALL groups, so an
-    event the capture group recorded inside a graph capture could come back as an eager work's event of the
-    default group, and the watchdog's query of an event of that work that was not re-recorded (the start
-    event is only recorded with timing on) fails with the same "event last recorded in a capturing stream"
-    -- an intermittent abort of the 1-rank DP test, depending on which cached event a work drew."""
-    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    kernels ahead of compute in the queues, as wanted for overlapped gradient buckets."""
     return dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
 
 

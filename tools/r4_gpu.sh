@@ -116,6 +116,9 @@ fi
 if [ "$what" = opt ]; then
   step opttests timeout -k 10 500 python -u -m pytest tests/test_engine_gpu.py tests/test_rccl_gpu.py tests/test_mtl_layer_local_gpu.py \
       -x -v --timeout 120 --timeout-method thread && \
+  step rccl2 timeout -k 10 300 python -u -m pytest tests/test_rccl_gpu.py -x -v --timeout 120 --timeout-method thread && \
+  step rccl3 timeout -k 10 300 python -u -m pytest tests/test_rccl_gpu.py -x -v --timeout 120 --timeout-method thread && \
+  step inc timeout -k 10 300 python -u -m pytest tests/test_inception_gpu.py -x -v --timeout 120 --timeout-method thread && \
   step benchA timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
   step phaseA timeout -k 10 200 python tools/phase_times.py MTL && \
   step benchC timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 && \
