@@ -24,8 +24,10 @@ from ..ops.hip import lib, stream
 # (join-then-fork points, wgrads on their producer's stream): denser event patterns crashed
 # hipStreamEndCapture on ROCm 7.
 MULTI_STREAM = os.environ.get("MDA_STREAMS", "1") == "1"
-# streams used at most (ids above are folded onto the last one -- still a valid schedule)
-MAX_STREAMS = 4
+# streams used at most (ids above are folded onto the last one -- still a valid schedule); never more than
+# the process's hardware queues: with GPU_MAX_HW_QUEUES=2 a 4-stream graph segfaults inside the HIP runtime
+# at replay, engine-free repro in tools/hwq_repro.py (profiles/r4_runtime_faults.txt)
+MAX_STREAMS = max(1, min(4, int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))))
 # logical id of the communication stream: data-parallel gradient all-reduces embedded in the backward
 # (LoweredProgram.backward_with_allreduce) run there, beside the compute streams, never folded onto them
 COMM_STREAM = 7

@@ -18,7 +18,7 @@ if [ "$what" = faults ]; then
   step hwq_default timeout -k 10 120 python -X faulthandler tools/hwq_repro.py --streams 4 && \
   step exitA timeout -k 10 200 python -X faulthandler bench.py --steps 50 --warmup 10 --heldout 0 && \
   step exitC timeout -k 10 300 python -X faulthandler bench.py --model multi_classifier --steps 20 --warmup 5 --heldout 0 && \
-  step hwq2_repro env GPU_MAX_HW_QUEUES=2 timeout -k 10 120 python -X faulthandler tools/hwq_repro.py --streams 4 && \
+  step hwq2_repro2 env GPU_MAX_HW_QUEUES=2 timeout -k 10 120 python -X faulthandler tools/hwq_repro.py --streams 2 && \
   step hwq2_benchA env GPU_MAX_HW_QUEUES=2 timeout -k 10 200 python -X faulthandler bench.py --steps 50 --warmup 10 --heldout 0 && \
   step hwq2_benchC env GPU_MAX_HW_QUEUES=2 timeout -k 10 300 python -X faulthandler bench.py --model multi_classifier --steps 20 --warmup 5 --heldout 0
 fi
@@ -140,4 +140,14 @@ if [ "$what" = scratch_ab ]; then
 fi
 if [ "$what" = acc ]; then
   step accuracy timeout -k 10 1100 python -u tools/accuracy_table.py --out gpurun_out/accuracy
+fi
+if [ "$what" = tailab ]; then
+  for r in 1 2 3; do
+    for v in 0 1; do
+      step benchC_tb${v}_$r env MDA_TAIL_BATCH=$v timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
+    done
+  done
+  for v in 0 1; do
+    step phaseC_tb$v env MDA_TAIL_BATCH=$v timeout -k 10 300 python tools/phase_times.py multi_classifier || exit $?
+  done
 fi
