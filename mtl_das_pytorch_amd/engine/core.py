@@ -433,7 +433,9 @@ class ConvLayer:
     # finalize (Model C: ~0.9 GB/step of slab traffic with grid-filling splits)
     # (512 / 2048 / 4096 measured within noise on A, C 7.10k at 1024 vs 6.83k at 2048)
     MIN_SPLIT_PX = 1024
-    MIN_SPLIT_PX_BIG = 256
+    # the large 32x32x16 tiles (configs 32-35) at 256 pixels per split: Model C's batches 624 -> 440 us but
+    # the finalize's split slabs 102 -> 197 us; at 1024: 515 us and 103 us (tools/wgrad_assign.py)
+    MIN_SPLIT_PX_BIG = 1024
 
     def wgrad_valid(self, cfg: int) -> bool:
         """The K tiles of ``cfg`` cover this conv's padded reduction (exactly, except for the large-tile
@@ -455,8 +457,7 @@ class ConvLayer:
         TN, TK, MCH = WGRAD_TILES[cfg]
         tiles = math.ceil(self.Npad / TN) * wgrad_ktiles(cfg, self.Kpad_w) * self.G
         # whole-reduction tiles (TK >= 128) have one tile per channel block: shorter per-block pixel
-        # ranges keep enough blocks in flight (the finalize sums the extra splits with several lanes);
-        # the large tiles stage 2-4x fewer bytes per output and can afford more splits still
+        # ranges keep enough blocks in flight (the finalize sums the extra splits with several lanes)
         if cfg >= WGRAD_BIG0:
             min_px = self.MIN_SPLIT_PX_BIG
         else:

@@ -17,8 +17,7 @@ import torch
 
 from ..ops.functional import (CONV_DEEP_CFG0, CONV_DEEP_NCFG, CONV_GLDS_CFG0, CONV_GLDS_NCFG, CONV_LDS_CFG0,
                               CONV_LDS_NCFG, CONV_PATCH_CFG0, CONV_PATCH_NCFG, CONV_PATCHP_CFG0, CONV_PATCHP_NCFG,
-                              CONV_XCD, GDEEP_TILES, WGRAD_BIG0, WGRAD_PATCH, WGRAD_TILES, conv_workspace,
-                              glds_cfg)
+                              CONV_XCD, GDEEP_TILES, WGRAD_PATCH, WGRAD_TILES, conv_workspace, glds_cfg)
 from ..ops.hip import lib
 
 # conv.hip register-pipelined tiles 0-13 (pipeline depth 2, and 4 at CONV_DEEP_CFG0 + tile), then
@@ -230,8 +229,7 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
     staged through LDS, blocks in flight, the finalize's split-slab reads -- not one job's latency, which
     is what the isolated timing of autotune_phases ranks (it favours small tiles with many blocks; in the
     batch the large 32x32x16 tiles, 2-4x fewer staged bytes per output, win on the big layers).  Greedy
-    coordinate descent over the wgrad signatures (costliest first): each candidate -- the current config
-    and every valid large tile -- is applied, the per-stream config cap (merge_wgrad_cfgs) and the finalize
+    coordinate descent over the wgrad signatures (costliest first): each valid config is applied, the per-stream config cap (merge_wgrad_cfgs) and the finalize
     refresh run as the bench runs them, and the sum of the batched launches' and the finalize's isolated
     graph-replay times decides.  Must run before batch_wgrads (on the per-conv launches).  Updates and
     returns ``cache``."""
@@ -243,7 +241,6 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
     for l in wg:
         groups.setdefault(wgrad_signature(l.args[1], l.args[2]), []).append(l)
     assign = {sig: ls[0].args[0] for sig, ls in groups.items()}
-    start = dict(assign)
     fin = [l for l in prog.bwd.launches if l.name == "wgrad_finalize"]
 
     def cost() -> float:
@@ -275,7 +272,7 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
         changed = False
         for sig in sorted(groups, key=weight, reverse=True):
             cur = assign[sig]
-            for c in [start[sig]] + [c for c in WGRAD_CFGS if c >= WGRAD_BIG0]:
+            for c in WGRAD_CFGS:
                 if c == assign[sig] or not all(l.owner.wgrad_valid(c) for l in groups[sig]):
                     continue
                 prev = assign[sig]

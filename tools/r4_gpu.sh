@@ -127,7 +127,12 @@ fi
 if [ "$what" = scratch ]; then
   # verdict item 7: the whole table re-derived from an EMPTY table (isolated, then in-context for A and C)
   step scratch timeout -k 10 1100 python -u tools/retune.py --models MTL,single_event,single_distance,multi_classifier \
-      --in-context --topk 3 --passes cfg,tail --out gpurun_out/tuned_scratch.json
+      --in-context --topk 3 --passes cfg,tail --out gpurun_out/tuned_scratch.json && \
+  cp gpurun_out/tuned_scratch.json mtl_das_pytorch_amd/engine/tuned_scratch.json && \
+  for r in 1 2; do
+    step benchA_ship$r timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+    step benchA_scr$r env MDA_TUNED_CFGS=mtl_das_pytorch_amd/engine/tuned_scratch.json timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 || exit $?
+  done
 fi
 if [ "$what" = scratch_ab ]; then
   # shipped table vs the from-scratch one, interleaved on one box
@@ -149,5 +154,29 @@ if [ "$what" = tailab ]; then
   done
   for v in 0 1; do
     step phaseC_tb$v env MDA_TAIL_BATCH=$v timeout -k 10 300 python tools/phase_times.py multi_classifier || exit $?
+  done
+fi
+if [ "$what" = scratch2 ]; then
+  # second from-scratch stage: batch-level weight-gradient configs and a wider in-context search on top of
+  # the isolated-only scratch table (no shipped-table input)
+  step scratch2 env MDA_TUNED_CFGS=mtl_das_pytorch_amd/engine/tuned_scratch.json timeout -k 10 1000 python -u tools/retune.py \
+      --keep --wgrad-batches --in-context --topk 6 --margin 0.001 --reps 30 --passes cfg,xcd,tail \
+      --models MTL,single_event,single_distance,multi_classifier --out gpurun_out/tuned_scratch2.json && \
+  cp gpurun_out/tuned_scratch2.json mtl_das_pytorch_amd/engine/tuned_scratch2.json && \
+  for r in 1 2; do
+    step benchA_ship$r timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+    step benchA_scr2_$r env MDA_TUNED_CFGS=mtl_das_pytorch_amd/engine/tuned_scratch2.json timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 || exit $?
+  done
+fi
+if [ "$what" = wgb ]; then
+  # weight-gradient configs chosen by their batched launches' time on top of the shipped table, then A/B
+  step wgb timeout -k 10 600 python -u tools/retune.py --keep --wgrad-batches --models MTL,multi_classifier \
+      --out gpurun_out/tuned_wgb2.json && \
+  cp gpurun_out/tuned_wgb2.json mtl_das_pytorch_amd/engine/tuned_wgb2.json && \
+  for r in 1 2; do
+    step benchA_ship$r timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+    step benchA_wgb$r env MDA_TUNED_CFGS=mtl_das_pytorch_amd/engine/tuned_wgb2.json timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+    step benchC_ship$r timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 && \
+    step benchC_wgb$r env MDA_TUNED_CFGS=mtl_das_pytorch_amd/engine/tuned_wgb2.json timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
   done
 fi
