@@ -418,6 +418,24 @@ class InceptionProgram(LoweredProgram):
                 op.defer_tail = True
                 self.n_tail_batched += 1
 
+    def _patch_forward(self, conv: ConvLayer) -> bool:
+        """The conv's training forward runs a 3x3 patch config in the shipped table: its input strip is staged
+        once, so normalise-on-load transforms each element once instead of KH*KW times as the im2col does --
+        the reason for NOL_MAX_PX -- and the cap does not apply (the stem's 47x122 / 21x58 consumers)."""
+        from ..ops.functional import CONV_PATCH_CFG0, CONV_PATCH_NCFG, CONV_PATCHP_CFG0, CONV_PATCHP_NCFG, CONV_XCD
+        from .tune import conv_signature, load_cache
+        if not hasattr(self, "_table"):
+            self._table = load_cache()
+        d = {"B": conv.B, "Hs": conv.Hi, "Ws": conv.Wi, "Ho": conv.Ho, "Wo": conv.Wo, "N": conv.Co, "Cs": conv.Cs,
+             "KH": conv.KH, "KW": conv.KW, "sh": conv.sh, "sw": conv.sw, "ph": conv.ph, "pw": conv.pw,
+             "src": {"C1": conv.src_C1}, "stats": 1}
+        cfg = self._table.get(conv_signature(0, conv.G, d))
+        if cfg is None:
+            return False
+        cfg &= ~CONV_XCD
+        return (CONV_PATCH_CFG0 <= cfg < CONV_PATCH_CFG0 + CONV_PATCH_NCFG
+                or CONV_PATCHP_CFG0 <= cfg < CONV_PATCHP_CFG0 + CONV_PATCHP_NCFG)
+
     def _plan_nol(self):
         """Normalise-on-load: a BasicConv2d output consumed by exactly one other BasicConv2d (and not a
         slice of a block's concat buffer) is never materialised -- the consumer reads the producer's
@@ -435,7 +453,8 @@ class InceptionProgram(LoweredProgram):
         for op in self.ops:
             p = producer.get(id(op.src))
             if (isinstance(op, CBR) and op.conv is not None and p is not None and op.src.parent is None
-                    and consumers[id(op.src)] == 1 and op.conv.Cs == p.out.act.C and op.conv.M_out <= max_px):
+                    and consumers[id(op.src)] == 1 and op.conv.Cs == p.out.act.C
+                    and (op.conv.M_out <= max_px or self._patch_forward(op.conv))):
                 op.nol_from = p
                 p.skip_tail = True
                 self.n_nol += 1
