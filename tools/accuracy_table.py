@@ -48,10 +48,10 @@ def make_test_sets(per_class: int, seed: int, snrs, device):
         sets[f"snr={s:g}dB"] = torch.from_numpy(noisy.astype(np.float32))
     lab2 = torch.stack([d, e], 1)
     joint = d + N_DIST * e
-    return {k: v.to(device) for k, v in sets.items()}, lab2.to(device), joint.to(device)
+    return {k: v.to(device) for k, v in sets.items()}, lab2.to(device), joint.to(device), e.to(device)
 
 
-def run_one(name, model, backend, args, seed, test_sets, lab2, joint, out_dir):
+def run_one(name, model, backend, args, seed, test_sets, lab2, joint, ev, out_dir):
     from mtl_das_pytorch_amd.engine.trainer import Trainer
     from mtl_das_pytorch_amd.utils.config import TrainConfig
     cfg = TrainConfig(model=model, synthetic=args.per_class, synthetic_seed=args.data_seed, batch_size=32,
@@ -71,6 +71,16 @@ def run_one(name, model, backend, args, seed, test_sets, lab2, joint, out_dir):
         if r.get("distance_cm") is not None:
             row["test"][k]["distance_cm"] = r["distance_cm"]
             row["test"][k]["errors"] = error_profile(np.asarray(r["distance_cm"]))
+            # the distance task per event type (is a collapse tied to one event signature?)
+            by = []
+            for e_ in (0, 1):
+                sel = ev == e_
+                re_ = tr.evaluate(X[sel], lab[sel])
+                cm = np.asarray(re_["distance_cm"])
+                by.append({"acc": round(float(np.trace(cm) / cm.sum()), 4), "mae_m": round(re_["mae_m"], 3),
+                           "top_pred_class": int(cm.sum(0).argmax()),
+                           "top_pred_share": round(float(cm.sum(0).max() / cm.sum()), 3)})
+            row["test"][k]["distance_by_event"] = by
     print(json.dumps(row), flush=True)
     return row
 
@@ -142,6 +152,22 @@ def to_markdown(rows, args):
                     f"{','.join(str(t) for t in tops)}: {_stat([x['top_pred_share'] for x in e], '%.2f')} / "
                     f"{_stat([x['mean_signed_err_m'] for x in e], '%+.1f')}")
         lines.append(f"| {n} | " + " | ".join(prof(k) for k in keys) + " |")
+    lines += ["", "Distance accuracy per event type (striking / excavating test samples evaluated separately; most-"
+              "predicted class and its share)", "", "| Model | " + " | ".join(keys) + " |", "|---|" + "---|" * len(keys)]
+    for n in names:
+        rs = [r for r in rows if r["name"] == n]
+        if "distance_by_event" not in rs[0]["test"][keys[0]]:
+            continue
+
+        def byev(k):
+            out = []
+            for e_ in (0, 1):
+                b = [r["test"][k]["distance_by_event"][e_] for r in rs]
+                tops = sorted({x["top_pred_class"] for x in b})
+                out.append(f"{_stat([x['acc'] for x in b], '%.3f')} ({','.join(map(str, tops))}: "
+                           f"{_stat([x['top_pred_share'] for x in b], '%.2f')})")
+            return " / ".join(out)
+        lines.append(f"| {n} | " + " | ".join(byev(k) for k in keys) + " |")
     return "\n".join(lines) + "\n"
 
 
@@ -163,7 +189,7 @@ def main():
     runs = args.runs_dir or tempfile.mkdtemp(prefix="mda_acc_")
     dev = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
     snrs = [float(s) for s in args.snr.split(",") if s]
-    test_sets, lab2, joint = make_test_sets(args.test_per_class, 99991 + args.data_seed, snrs, dev)
+    test_sets, lab2, joint, ev = make_test_sets(args.test_per_class, 99991 + args.data_seed, snrs, dev)
     spec = {"A": ("A MTL_Net", "MTL", "engine"), "A_fp32": ("A MTL_Net (fp32 torch)", "MTL", "torch"),
             "B_distance": ("B Single_Task_Net distance", "single_distance", "engine"),
             "B_event": ("B Single_Task_Net event", "single_event", "engine"),
@@ -174,7 +200,7 @@ def main():
             name, model, backend = spec[key]
             if dev.type != "cuda":
                 backend = "torch"
-            rows.append(run_one(name, model, backend, args, seed, test_sets, lab2, joint, runs))
+            rows.append(run_one(name, model, backend, args, seed, test_sets, lab2, joint, ev, runs))
             with open(os.path.join(args.out, "accuracy.json"), "w") as f:
                 json.dump({"args": vars(args), "rows": rows}, f, indent=1)
     md = to_markdown(rows, args)

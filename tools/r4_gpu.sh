@@ -180,3 +180,12 @@ if [ "$what" = wgb ]; then
     step benchC_wgb$r env MDA_TUNED_CFGS=mtl_das_pytorch_amd/engine/tuned_wgb2.json timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
   done
 fi
+if [ "$what" = accev_prof ]; then
+  for sd in 0 1 2; do
+    step accuracy_ev$sd timeout -k 10 300 python -X faulthandler -u tools/accuracy_table.py --rows A,B_distance,C --seeds $sd \
+        --out gpurun_out/accuracy_ev$sd || exit $?
+  done
+
+  source tools/profile_round.sh && \
+  prof_model MTL A && prof_model multi_classifier C
+fi
