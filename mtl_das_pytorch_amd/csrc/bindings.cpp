@@ -316,10 +316,20 @@ void cls_head(int64_t stream, py::dict d) {
 }
 
 void gather_batch(int64_t X, int64_t idx, int64_t lab, int lab_w, int64_t out, int64_t lab_out, int B, int Cin, int H,
-                  int W, int64_t stream, int taps, int off) {
+                  int W, int64_t stream, int taps, int off, py::list zero) {
+  ZeroRanges z{};
+  if (zero.size() > 4) throw std::runtime_error("gather_batch: at most 4 zero ranges");
+  for (size_t i = 0; i < zero.size(); ++i) {
+    auto t = zero[i].cast<py::tuple>();
+    const int64_t ptr = t[0].cast<int64_t>(), bytes = t[1].cast<int64_t>();
+    if (ptr % 16 || bytes % 16 || bytes < 0) throw std::runtime_error("gather_batch: zero range not 16-byte aligned");
+    z.p[i] = reinterpret_cast<uint4*>(static_cast<intptr_t>(ptr));
+    z.n16[i] = bytes / 16;
+  }
+  z.n = (int)zero.size();
   check(launch_gather_batch(reinterpret_cast<const float*>(X), reinterpret_cast<const int64_t*>(idx),
                             reinterpret_cast<const int64_t*>(lab), lab_w, reinterpret_cast<bf16_t*>(out),
-                            reinterpret_cast<int64_t*>(lab_out), B, Cin, H, W, taps, off, S(stream)), "gather_batch");
+                            reinterpret_cast<int64_t*>(lab_out), B, Cin, H, W, taps, off, z, S(stream)), "gather_batch");
 }
 
 void pool3(int is_max, int backward, int64_t stream, py::dict d) {
@@ -402,7 +412,7 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("cls_head", &cls_head);
   m.def("gather_batch", &gather_batch, py::arg("X"), py::arg("idx"), py::arg("lab"), py::arg("lab_w"), py::arg("out"),
         py::arg("lab_out"), py::arg("B"), py::arg("Cin"), py::arg("H"), py::arg("W"), py::arg("stream"),
-        py::arg("taps") = 0, py::arg("off") = 0);
+        py::arg("taps") = 0, py::arg("off") = 0, py::arg("zero") = py::list());
   m.def("pool3", &pool3);
   m.def("wgrad_table", &wgrad_table);
   m.def("wgrad_batched", &wgrad_batched);

@@ -278,8 +278,14 @@ int launch_tail_fwd_batched(int kind, const TailJob* d_jobs, int nj, int nblocks
 int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, int fused, hipStream_t st);
 int launch_mtl_head(const HeadArgs& a, hipStream_t st);
 int launch_cls_head(const ClsArgs& a, int64_t* seed_mut, hipStream_t st);
+struct ZeroRanges {  // up to 4 16-byte-aligned regions a launch zeroes (gather_batch: the arena's zeroed buffers)
+  uint4* p[4];
+  int64_t n16[4];     // 16-byte units
+  int n;
+};
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
-                        int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, hipStream_t st);
+                        int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, const ZeroRanges& zero,
+                        hipStream_t st);
 int launch_pool3(int is_max, int backward, const PoolArgs& a, hipStream_t st);
 // synth.hip: on-device synthetic DAS samples (data/synthetic.py physical model, Philox noise)
 constexpr int SYNTH_NPARAM = 9;  // per sample: distance, event, x0, t0, jitter[4], snr_db

@@ -16,10 +16,18 @@ namespace mda {
 // holds x[h - off + j][w] (zero outside the image, j < taps), so a KHxKW stem over 1 channel runs as a
 // 1xKW conv over KH real channels (engine/core.py stem_pack_geom) instead of wasting 7/8 of its K on
 // zero padding channels.
+// zero: the arena's zeroed regions (BN statistic replicas, backward workspaces) cleared by the same launch
+// at the start of a training step -- one dependent launch instead of a gather plus a fill per dtype.
 __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restrict__ X, const int64_t* __restrict__ idx,
                                                            const int64_t* __restrict__ lab, int lab_w,
                                                            bf16_t* __restrict__ out, int64_t* __restrict__ lab_out,
-                                                           int B, int Cin, int H, int W, int taps, int off) {
+                                                           int B, int Cin, int H, int W, int taps, int off,
+                                                           ZeroRanges zero) {
+  {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, nt = (int64_t)gridDim.x * 256;
+    for (int r = 0; r < zero.n; ++r)
+      for (int64_t i = t; i < zero.n16[r]; i += nt) zero.p[r][i] = make_uint4(0, 0, 0, 0);
+  }
   const int64_t M = (int64_t)B * H * W;
   const int HW = H * W;
   for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < M; p += (int64_t)gridDim.x * 256) {
@@ -48,13 +56,14 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restri
 }
 
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
-                        int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, hipStream_t st) {
+                        int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, const ZeroRanges& zero,
+                        hipStream_t st) {
   if (Cin > 8 || taps > 8 || (taps > 0 && Cin != 1) || (int64_t)B * H * W >= (1ll << 31)) return -2;
   const int64_t M = (int64_t)B * H * W;
   // one pixel per thread (no grid-stride second round: the idx -> X -> store chain is latency-bound)
   int blocks = (int)std::min<int64_t>((M + 255) / 256, 65535);
   hipLaunchKernelGGL(gather_batch_kernel, dim3(blocks), dim3(256), 0, st, X, idx, lab, lab_w, out, lab_out, B, Cin, H, W,
-                     taps, off);
+                     taps, off, zero);
   return (int)hipGetLastError();
 }
 

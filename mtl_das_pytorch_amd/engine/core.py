@@ -190,6 +190,13 @@ class Arena:
                 v.bind(buf[o:o + n].view(v.shape))
                 o += pad_to(n, 64)
 
+    def zero_ranges(self):
+        """(pointer, bytes) of the zeroed backing buffers, for a kernel that clears them itself (the batch
+        gather); None under the guard allocator (banded per-view buffers: use clear())."""
+        if guard.enabled() or len(self._zero) > 4:
+            return None
+        return [(b.data_ptr(), b.numel() * b.element_size()) for b in self._zero.values()]
+
     def clear(self):
         if guard.enabled():
             for v in self._zero_specs:

@@ -343,12 +343,21 @@ class LoweredProgram:
 
     stem_pack = (0, 0)  # (taps, offset) of the gather's vertical tap packing (core.stem_pack_geom)
 
-    def gather_phase(self, X, labels, idx) -> Phase:
+    def gather_phase(self, X, labels, idx, clear: bool = False) -> Phase:
+        """The batch gather; ``clear``: the same launch also zeroes the arena's zeroed region (what
+        ``arena.clear`` does at the start of a training step), unless the guard allocator keeps every zeroed
+        view in its own banded buffer -- then ``arena.clear`` runs first."""
         ph = Phase("gather")
         if self.stem_pack[0] and X.shape[1] != 1:
             raise ValueError("stem tap packing needs a single-channel input")
+        zero = []
+        if clear:
+            zero = self.arena.zero_ranges()
+            if zero is None:
+                ph.add("clear", lambda st: self.arena.clear())
+                zero = []
         ph.add("gather", k_gather, X, idx, labels, self.label_width, self.x, self.labels, self.B, X.shape[1], self.H0,
-               self.W0, *self.stem_pack)
+               self.W0, *self.stem_pack, zero)
         return ph
 
     def _wgfin_args(self, convs=None):

@@ -211,6 +211,6 @@ def k_allreduce(fn, t, st):
     fn(t.t if hasattr(t, "bind") else t)  # arena LazyView -> its bound tensor
 
 
-def k_gather(X, idx, lab, lab_w, out, lab_out, B, Cin, H, W, taps, off, st):
+def k_gather(X, idx, lab, lab_w, out, lab_out, B, Cin, H, W, taps, off, zero, st):
     lib().gather_batch(X.data_ptr(), idx.data_ptr(), lab.data_ptr(), lab_w, out.data_ptr(), lab_out.data_ptr(),
-                       B, Cin, H, W, st, taps, off)
+                       B, Cin, H, W, st, taps, off, zero)

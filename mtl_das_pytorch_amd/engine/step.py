@@ -2,7 +2,7 @@
 
 A training step is
 
-    [memset zeroed arena] [gather batch] [forward] [backward]  ->  (DP: RCCL all-reduce of the flat
+    [gather batch + zero the arena's accumulators] [forward] [backward]  ->  (DP: RCCL all-reduce of the flat
     gradient buckets)  ->  [fused Adam + bf16 re-pack] [step++]
 
 Single GPU: the whole step is ONE captured HIP graph (``torch.cuda.CUDAGraph`` is a hipGraph on ROCm),
@@ -80,21 +80,22 @@ class StepRunner:
     def _phases(self, kind: str) -> List[Callable[[], None]]:
         p = self.p
         X, lab = self.sources["train" if kind.startswith("train") else "eval"]
-        gather = p.gather_phase(X, lab, self.idx)
+        # a training step's gather also zeroes the arena's accumulators (one launch; arena.clear otherwise)
+        gather = p.gather_phase(X, lab, self.idx, clear=kind.startswith("train"))
         if kind.startswith("train_piece"):
             k = int(kind[len("train_piece"):])
             pieces = self._pieces()
-            return ([p.arena.clear, gather.run, p.fwd_train.run] if k == 0 else []) + [pieces[k].run]
+            return ([gather.run, p.fwd_train.run] if k == 0 else []) + [pieces[k].run]
         if kind == "train_compute":
-            return [p.arena.clear, gather.run, p.fwd_train.run, p.bwd.run]
+            return [gather.run, p.fwd_train.run, p.bwd.run]
         if kind == "train_opt":
             return [p.opt["adam"].run]
         if kind == "train_full":
-            return [p.arena.clear, gather.run, p.fwd_train.run, p.bwd.run, p.opt["adam"].run]
+            return [gather.run, p.fwd_train.run, p.bwd.run, p.opt["adam"].run]
         if kind == "train_full_dp":
             if self._bwd_dp is None:
                 self._bwd_dp = p.backward_with_allreduce(self.allreduce.ordered)
-            return [p.arena.clear, gather.run, p.fwd_train.run, self._bwd_dp.run, p.opt["adam"].run]
+            return [gather.run, p.fwd_train.run, self._bwd_dp.run, p.opt["adam"].run]
         if kind == "eval":
             return [gather.run, p.fwd_eval.run]
         raise ValueError(kind)

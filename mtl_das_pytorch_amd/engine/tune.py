@@ -305,8 +305,8 @@ def step_time_us(prog, X: torch.Tensor, labels: torch.Tensor, reps: int = 100, r
     f.lr.zero_()
     prog.opt["pack"].run()
     idx = torch.arange(prog.B, device=prog.device) % X.shape[0]
-    gather = prog.gather_phase(X, labels, idx)
-    fns = [prog.arena.clear, gather.run, prog.fwd_train.run, prog.bwd.run, prog.opt["adam"].run]
+    gather = prog.gather_phase(X, labels, idx, clear=True)
+    fns = [gather.run, prog.fwd_train.run, prog.bwd.run, prog.opt["adam"].run]
     for fn_ in fns:
         fn_()
     torch.cuda.synchronize()
@@ -397,8 +397,8 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
                           f.lr, prog.metrics, prog.confusion, prog.logp] + list(getattr(prog, "extra_state", [])))
     f.lr.zero_()
     idx = torch.arange(prog.B, device=prog.device) % X.shape[0]
-    gather = prog.gather_phase(X, labels, idx)
-    fns = [prog.arena.clear, gather.run, prog.fwd_train.run, prog.bwd.run, prog.opt["adam"].run]
+    gather = prog.gather_phase(X, labels, idx, clear=True)
+    fns = [gather.run, prog.fwd_train.run, prog.bwd.run, prog.opt["adam"].run]
     keep = {}
     for ph in (prog.fwd_train, prog.bwd):
         ph.__dict__.setdefault("ws_keep", {})

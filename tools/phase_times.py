@@ -34,15 +34,15 @@ def main():
     idx = torch.arange(32, device="cuda")
     p.flat.lr.fill_(1e-3)
     p.opt["pack"].run()
-    gather = p.gather_phase(X, lab, idx)
+    gather = p.gather_phase(X, lab, idx, clear=True)  # with the arena clear, as the step runs it
     f = p.flat
     state = [f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step, p.metrics,
              p.confusion, p.logp] + list(getattr(p, "extra_state", []))
     prefixes = {
-        "gather": [p.arena.clear, gather.run],
-        "+fwd": [p.arena.clear, gather.run, p.fwd_train.run],
-        "+bwd": [p.arena.clear, gather.run, p.fwd_train.run, p.bwd.run],
-        "+adam (full step)": [p.arena.clear, gather.run, p.fwd_train.run, p.bwd.run, p.opt["adam"].run],
+        "gather": [gather.run],
+        "+fwd": [gather.run, p.fwd_train.run],
+        "+bwd": [gather.run, p.fwd_train.run, p.bwd.run],
+        "+adam (full step)": [gather.run, p.fwd_train.run, p.bwd.run, p.opt["adam"].run],
         "eval fwd": [gather.run, p.fwd_eval.run],
     }
     counts = {"fwd": len(p.fwd_train), "bwd": len(p.bwd), "adam": len(p.opt["adam"]), "eval": len(p.fwd_eval)}

@@ -189,3 +189,12 @@ if [ "$what" = accev_prof ]; then
   source tools/profile_round.sh && \
   prof_model MTL A && prof_model multi_classifier C
 fi
+if [ "$what" = gclear ]; then
+  step gctests timeout -k 10 500 python -u -m pytest tests/test_engine_gpu.py tests/test_inception_gpu.py tests/test_rccl_gpu.py \
+      tests/test_guard_gpu.py tests/test_mtl_layer_local_gpu.py tests/test_inference_gpu.py -x -v --timeout 120 --timeout-method thread && \
+  step benchA1 timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+  step benchA2 timeout -k 10 200 python bench.py --steps 300 --warmup 30 && \
+  step phaseA timeout -k 10 200 python tools/phase_times.py MTL && \
+  step benchC timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 && \
+  step phaseC timeout -k 10 300 python tools/phase_times.py multi_classifier
+fi
