@@ -259,8 +259,9 @@ void tail_fwd(int kind, int G, int blocks, int64_t stream, py::dict d) {
   check(launch_tail_fwd(kind, parse_tail(d), G, blocks, S(stream)), "tail_fwd");
 }
 
-// Packs the TailJob table of a batched forward-tail launch; returns (bytes, total blocks, largest C).
-py::tuple tail_table(py::list dicts, py::list blocks) {
+// Packs the TailJob table of a batched tail launch; returns (bytes, total blocks, largest C).  ``bwd``: backward
+// tails (residual-free ACT_RELU tails; the gradient sources, replica sums and outputs of parse_tail).
+py::tuple tail_table(py::list dicts, py::list blocks, bool bwd) {
   std::vector<TailJob> jobs(dicts.size());
   int64_t b0 = 0;
   int maxC = 0;
@@ -270,12 +271,19 @@ py::tuple tail_table(py::list dicts, py::list blocks) {
     j.a = parse_tail(dicts[i].cast<py::dict>());
     j.blocks = blocks[i].cast<int>();
     if (j.blocks <= 0 || j.a.C % 8 || j.a.r || j.a.r_bn) throw std::runtime_error("tail_table: unsupported tail");
+    if (bwd && (!j.a.part || j.a.chunk_px <= 0 || j.a.side || j.a.gscale != 1.f))
+      throw std::runtime_error("tail_table: unsupported backward tail");
     j.block0 = (int)b0;
     b0 += j.blocks;
     maxC = std::max(maxC, j.a.C);
   }
   if (b0 >= (1ll << 31)) throw std::runtime_error("tail_table: too many blocks");
   return py::make_tuple(py::bytes(reinterpret_cast<const char*>(jobs.data()), jobs.size() * sizeof(TailJob)), b0, maxC);
+}
+
+void tail_bwd_batched(int kind, int cgb, int reduce, int64_t table, int nj, int64_t nblocks, int64_t stream) {
+  check(launch_tail_bwd_batched(kind, cgb, reduce, reinterpret_cast<const TailJob*>(static_cast<intptr_t>(table)), nj,
+                                (int)nblocks, S(stream)), "tail_bwd_batched");
 }
 
 void tail_fwd_batched(int kind, int64_t table, int nj, int64_t nblocks, int maxC, int64_t stream) {
@@ -405,7 +413,8 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("wgrad", &wgrad);
   m.def("wgrad_finalize", &wgrad_finalize);
   m.def("tail_fwd", &tail_fwd);
-  m.def("tail_table", &tail_table);
+  m.def("tail_table", &tail_table, py::arg("dicts"), py::arg("blocks"), py::arg("bwd") = false);
+  m.def("tail_bwd_batched", &tail_bwd_batched);
   m.def("tail_fwd_batched", &tail_fwd_batched);
   m.def("tail_bwd", &tail_bwd);
   m.def("mtl_head", &mtl_head);

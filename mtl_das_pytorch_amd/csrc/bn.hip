@@ -324,14 +324,15 @@ DEV void bnb_ctx(const TailArgs& a, int z, int cblk, int cgl, BwdCtx& X, float (
   X.sc2 = &s_x[1][0][q]; X.sh2 = &s_x[1][1][q]; X.mean2 = &s_x[1][2][q]; X.inv2 = &s_x[1][3][q];
 }
 
+// chunk / cy / z: the block's pixel chunk, channel block and group (the grid's x / y / z, or a job's share
+// of a batched launch)
 template <int KIND, int CGB>
-DEV void bnb_reduce_impl(const TailArgs& a) {
+DEV void bnb_reduce_impl(const TailArgs& a, const int chunk, const int cy, const int z) {
   constexpr int PL = BNB_T / CGB, CB = 8 * CGB;
   __shared__ float s_x[2][5][CB];
   __shared__ float s_part[16][3][CB];  // 16 rows of 16 lanes per block
-  const int z = blockIdx.z, chunk = blockIdx.x;
   const int cgl = threadIdx.x % CGB, pl = threadIdx.x / CGB;
-  const int cblk = blockIdx.y * CB, c = cblk + cgl * 8;
+  const int cblk = cy * CB, c = cblk + cgl * 8;
   constexpr bool two = KIND == ADD_RELU2;
   BwdCtx X;
   bnb_ctx<KIND, CGB>(a, z, cblk, cgl, X, s_x);
@@ -373,14 +374,13 @@ DEV void bnb_reduce_impl(const TailArgs& a) {
 }
 
 template <int KIND, int CGB>
-DEV void bnb_apply_impl(const TailArgs& a) {
+DEV void bnb_apply_impl(const TailArgs& a, const int chunk, const int cy, const int z) {
   constexpr int PL = BNB_T / CGB, CB = 8 * CGB;
   __shared__ float s_x[2][5][CB];
   __shared__ float s_red[BNB_T];
   __shared__ float s_coef[2][3][CB];
-  const int z = blockIdx.z, chunk = blockIdx.x;
   const int cgl = threadIdx.x % CGB, pl = threadIdx.x / CGB;
-  const int cblk = blockIdx.y * CB, c = cblk + cgl * 8;
+  const int cblk = cy * CB, c = cblk + cgl * 8;
   constexpr bool two = KIND == ADD_RELU2;
   BwdCtx X;
   bnb_ctx<KIND, CGB>(a, z, cblk, cgl, X, s_x);
@@ -460,16 +460,37 @@ DEV void bnb_apply_impl(const TailArgs& a) {
 // These passes are latency-bound, and occupancy is what hides the latency (measured: forward tails at 4
 // instead of 6 waves per SIMD cost Model A 150 us per step).
 template <int KIND, int CGB>
-__global__ __launch_bounds__(BNB_T) void bnb_reduce_kernel(TailArgs a) { bnb_reduce_impl<KIND, CGB>(a); }
+__global__ __launch_bounds__(BNB_T) void bnb_reduce_kernel(TailArgs a) {
+  bnb_reduce_impl<KIND, CGB>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
 template <int KIND, int CGB, int W>
 __global__ __launch_bounds__(BNB_T) __attribute__((amdgpu_waves_per_eu(W))) void bnb_reduce_kernel_w(TailArgs a) {
-  bnb_reduce_impl<KIND, CGB>(a);
+  bnb_reduce_impl<KIND, CGB>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 template <int KIND, int CGB>
-__global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) { bnb_apply_impl<KIND, CGB>(a); }
+__global__ __launch_bounds__(BNB_T) void bnb_apply_kernel(TailArgs a) {
+  bnb_apply_impl<KIND, CGB>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
 template <int KIND, int CGB, int W>
 __global__ __launch_bounds__(BNB_T) __attribute__((amdgpu_waves_per_eu(W))) void bnb_apply_kernel_w(TailArgs a) {
-  bnb_apply_impl<KIND, CGB>(a);
+  bnb_apply_impl<KIND, CGB>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Several BN-tail backward passes of one kind in one launch (engine/inception.py: the branch-output tails of
+// an Inception block, whose gradient sources all complete at the block's backward fork): block -> job by
+// binary search; a job's blocks are its (chunk, channel block) grid, chunk fastest.  REDUCE: the reduce
+// pass, else the apply pass.
+template <int KIND, int CGB, int W, bool REDUCE>
+__global__ __launch_bounds__(BNB_T) __attribute__((amdgpu_waves_per_eu(W))) void bnb_batched_kernel(
+    const TailJob* __restrict__ jobs, int nj) {
+  int lo = 0, hi = nj - 1;
+  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= (int)blockIdx.x) lo = mid; else hi = mid - 1; }
+  const TailJob& J = jobs[lo];
+  const int local = (int)blockIdx.x - J.block0;
+  const int nchunk = J.blocks / (J.a.C / (8 * CGB));
+  const int cy = local / nchunk, chunk = local - cy * nchunk;
+  if (REDUCE) bnb_reduce_impl<KIND, CGB>(J.a, chunk, cy, 0);
+  else bnb_apply_impl<KIND, CGB>(J.a, chunk, cy, 0);
 }
 // waves per SIMD each kind's passes fit without spilling (hipcc -Rpass-analysis=kernel-resource-usage, gfx950);
 // 0 = the compiler's default allocation
@@ -590,6 +611,30 @@ int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t 
 #undef K
     default: return -1;
   }
+  return (int)hipGetLastError();
+}
+
+// Batched BN-tail backward of ACT_RELU tails (kind 1, no residual / side outputs): the reduce pass of the jobs
+// that need one (``reduce``), then the apply pass of all.  cgb: channel groups per block, dividing every job's
+// C / 8; each job's ``blocks`` = nchunk * C / (8 * cgb).
+int launch_tail_bwd_batched(int kind, int cgb, int reduce, const TailJob* d_jobs, int nj, int nblocks, hipStream_t st) {
+  if (nblocks <= 0) return 0;
+  if (kind != ACT_RELU) return -1;
+#define KB(CG)                                                                                                    \
+  if (reduce)                                                                                                     \
+    hipLaunchKernelGGL((bnb_batched_kernel<ACT_RELU, CG, bnb_waves<ACT_RELU>(), true>), dim3(nblocks), dim3(BNB_T), \
+                       0, st, d_jobs, nj);                                                                        \
+  else                                                                                                            \
+    hipLaunchKernelGGL((bnb_batched_kernel<ACT_RELU, CG, bnb_waves<ACT_RELU>(), false>), dim3(nblocks),            \
+                       dim3(BNB_T), 0, st, d_jobs, nj);
+  switch (cgb) {
+    case 1: KB(1) break;
+    case 2: KB(2) break;
+    case 4: KB(4) break;
+    case 8: KB(8) break;
+    default: return -1;
+  }
+#undef KB
   return (int)hipGetLastError();
 }
 

@@ -275,6 +275,7 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);
 int launch_tail_fwd_batched(int kind, const TailJob* d_jobs, int nj, int nblocks, int maxC, hipStream_t st);
+int launch_tail_bwd_batched(int kind, int cgb, int reduce, const TailJob* d_jobs, int nj, int nblocks, hipStream_t st);
 int launch_tail_bwd(int kind, const TailArgs& a, int G, int blocks, int fused, hipStream_t st);
 int launch_mtl_head(const HeadArgs& a, hipStream_t st);
 int launch_cls_head(const ClsArgs& a, int64_t* seed_mut, hipStream_t st);

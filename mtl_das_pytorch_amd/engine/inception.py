@@ -28,6 +28,7 @@ from ..models.multi_classifier import (BasicConv2d, InceptionA, InceptionB, Ince
 from . import guard
 from .core import GRAD_DT, NREP, Act, Arena, BNLayer, ConvLayer, FlatState, P, grads_of, new_act, src_dict, stem_pack_geom
 from .lowering import ACT_RELU, LoweredProgram
+from ..ops.hip import lib
 from .program import Phase, k_cls_head, k_pool, k_wgfin
 
 
@@ -99,6 +100,8 @@ class CBR:
 
     def backward(self, prog, ph: Phase):
         prog._tail_bwd(ph, ACT_RELU, 1, self.y, self.bn, grads_of(self.out.grad_sources()), self.dy)
+        if self.defer_tail:  # a block-output tail: InceptionProgram.batch_tails may batch its backward too
+            ph.launches[-1].owner = self
         if self.conv is None:  # a fused member: its HConv's data / weight gradient run over the group's dy
             return
         src, nol = self._src()
@@ -417,6 +420,67 @@ class InceptionProgram(LoweredProgram):
                     and self.op_meta[i] is not None):
                 op.defer_tail = True
                 self.n_tail_batched += 1
+
+    def batch_tails(self) -> int:
+        """The backward of the branch-output BN+ReLU tails of each Inception block as ONE reduce and ONE apply
+        launch on stream 0 right after the block's backward fork (their gradient sources -- the next block's
+        data gradients -- are complete there), instead of a reduce + apply (or the single-launch kernel) at
+        the head of every branch stream (csrc/bn.hip bnb_batched_kernel).  Each branch's first remaining
+        launch waits for the batch.  Runs after the autotuner (which picks the per-tail variants the batch
+        replaces); not with SyncBN (its collectives sit between the passes).  Returns the tails batched."""
+        from .program import Launch, k_tail_bwd_batched
+        if not self.tail_batch_enabled() or getattr(self, "sync_bn_world", None) is not None:
+            return 0
+        ls = self.bwd.launches
+        fork_at = {}
+        blk = None
+        groups = {}
+        for i, l in enumerate(ls):
+            if l.name.startswith("fork:backward_f"):
+                blk = l.name
+                fork_at[blk] = i
+            elif (l.name.startswith("tailbwd") and isinstance(l.owner, CBR) and l.owner.defer_tail and blk is not None
+                  and l.args[3].get("fused", 0) in (0, 1) and l.args[0] == ACT_RELU and l.args[1] == 1
+                  and not l.args[3].get("side")):
+                groups.setdefault(blk, []).append(l)
+        n = 0
+        removed = set()
+        inserts = []
+        for blk, tails in groups.items():
+            cgb = 8
+            while any((t.args[3]["C"] // 8) % cgb for t in tails):
+                cgb //= 2
+            jobs = [dict(t.args[3], fused=0) for t in tails]
+            blocks = [t.args[2] * (t.args[3]["C"] // (8 * cgb)) for t in tails]
+            raw, nblocks, _ = lib().tail_table(jobs, blocks, True)
+            table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+            self._tail_tables = getattr(self, "_tail_tables", [])
+            self._tail_tables.append(table)
+            tag = f"tailbatch_{blk[len('fork:'):]}"
+            red = Launch("tailbatchbwd_reduce", k_tail_bwd_batched, ACT_RELU, cgb, 1, table, len(jobs), nblocks,
+                         owner=tails, stream=0)
+            app = Launch("tailbatchbwd_apply", k_tail_bwd_batched, ACT_RELU, cgb, 0, table, len(jobs), nblocks,
+                         owner=tails, stream=0, record=tag)
+            inserts.append((fork_at[blk] + 1, [red, app]))
+            for t in tails:
+                if t.record is not None:
+                    raise RuntimeError(f"batched tail backward records event {t.record}")
+                removed.add(id(t))
+                # the branch's next launch inherits the tail's waits, now on the batch
+                nxt = next((k for k in ls[ls.index(t) + 1:] if k.stream == t.stream), None)
+                if nxt is not None and t.stream != 0:
+                    nxt.waits = tuple(w for w in nxt.waits if w not in t.waits) + (tag,)
+            n += len(tails)
+        out = []
+        ins = dict(inserts)
+        for i, l in enumerate(ls):
+            if id(l) not in removed:
+                out.append(l)
+            if i + 1 in ins:
+                out += ins[i + 1]
+        self.bwd.launches = out
+        self.n_tail_bwd_batched = n
+        return n
 
     def _patch_forward(self, conv: ConvLayer) -> bool:
         """The conv's training forward runs a 3x3 patch config in the shipped table: its input strip is staged

@@ -540,6 +540,11 @@ class LoweredProgram:
         self.n_wgrad_merged = moved
         return moved
 
+    def batch_tails(self) -> int:
+        """Batch independent BN-tail backward passes into shared launches after tuning (models whose lowering
+        knows such groups override this; engine/inception.py)."""
+        return 0
+
     def spill_wgrads(self, frac: float) -> int:
         """Move the weight gradients of stream 0's EARLIEST convs (in backward order; about ``frac`` of stream
         0's weight-gradient work) to their own batches on the spill stream, which start as soon as the last

@@ -176,6 +176,10 @@ def k_tail_fwd_batched(kind, table, nj, nblocks, max_c, st):
     lib().tail_fwd_batched(kind, table.data_ptr(), nj, nblocks, max_c, st)
 
 
+def k_tail_bwd_batched(kind, cgb, reduce, table, nj, nblocks, st):
+    lib().tail_bwd_batched(kind, cgb, reduce, table.data_ptr(), nj, nblocks, st)
+
+
 def k_tail_bwd(kind, G, blocks, d, st):
     lib().tail_bwd(kind, G, blocks, st, d)
 

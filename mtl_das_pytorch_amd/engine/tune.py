@@ -211,6 +211,7 @@ def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False
     n0 = len(cache)
     autotune_phases([prog.fwd_train, prog.fwd_eval, prog.bwd], cache, verbose, measure)
     if batch_wgrads:
+        prog.batch_tails()
         prog.spill_wgrads(wgrad_spill_frac(prog, cache))
         prog.merge_wgrad_cfgs()
     prog.refresh_wgrad_finalize()

@@ -289,3 +289,29 @@ def test_inception_tail_batches_bitwise(monkeypatch):
         out.append((prog.logp.clone(), f.grads.clone(), f.bn_mean.clone(), f.bn_var.clone()))
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+def test_inception_tail_backward_batches(monkeypatch):
+    """The block-output tails' backward as one batched reduce + apply per block (InceptionProgram.batch_tails)
+    against the per-branch launches.  The first block in backward order (Mixed_7c) sees identical inputs, so
+    its branch-output BN gradients agree to the fp32 order of the block partial sums; further down, bf16
+    rounding flips of the stored gradients propagate (a few 1e-3 globally), so the whole gradient is bounded
+    by cosine."""
+    out = []
+    for batched in (False, True):
+        monkeypatch.setenv("MDA_TAIL_BATCH", "1")
+        model, ref, prog, X, labels = _setup(B=8, seed=4)
+        if batched:
+            assert prog.batch_tails() == 44
+            assert sum(l.name.startswith("tailbatchbwd") for l in prog.bwd.launches) == 22
+        _engine_step(prog, X, labels, torch.arange(8, device="cuda"))
+        prog.flat.sync_module_grads()
+        out.append({n: p.grad.clone() for n, p in model.named_parameters()})
+    last = [n for n in out[0] if n.startswith("Mixed_7c.") and ".bn." in n
+            and any(b in n for b in ("branch1x1.", "branch3x3_2a.", "branch3x3_2b.", "branch3x3dbl_3a.",
+                                     "branch3x3dbl_3b.", "branch_pool."))]
+    assert len(last) == 12
+    for n in last:
+        assert rel(out[1][n], out[0][n]) < 1e-4, n
+    flat = [torch.cat([o[n].flatten() for n in o]) for o in out]
+    assert F.cosine_similarity(flat[0], flat[1], dim=0).item() > 0.999

@@ -198,3 +198,12 @@ if [ "$what" = gclear ]; then
   step benchC timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 && \
   step phaseC timeout -k 10 300 python tools/phase_times.py multi_classifier
 fi
+if [ "$what" = tbwd ]; then
+  step tbtests timeout -k 10 400 python -u -m pytest tests/test_inception_gpu.py tests/test_rccl_gpu.py -x -v --timeout 120 --timeout-method thread && \
+  for r in 1 2; do
+    for v in 0 1; do
+      step benchC_tbw${v}_$r env MDA_TAIL_BATCH=$v timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
+    done
+  done
+  step phaseC timeout -k 10 300 python tools/phase_times.py multi_classifier
+fi
