@@ -207,3 +207,19 @@ if [ "$what" = tbwd ]; then
   done
   step phaseC timeout -k 10 300 python tools/phase_times.py multi_classifier
 fi
+if [ "$what" = final ]; then
+  step gputests timeout -k 10 600 python -u -m pytest tests -m gpu --maxfail=5 -q --timeout 120 --timeout-method thread && \
+  step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" && \
+  step benchA1 timeout -k 10 200 python bench.py --steps 300 --warmup 30 && \
+  step benchA2 timeout -k 10 200 python bench.py && \
+  step benchBe timeout -k 10 200 python bench.py --model single_event --steps 300 --warmup 30 --heldout 0 && \
+  step benchBd timeout -k 10 200 python bench.py --model single_distance --steps 300 --warmup 30 --heldout 0 && \
+  step benchC1 timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 && \
+  step benchC2 timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 && \
+  step phaseA timeout -k 10 200 python tools/phase_times.py MTL && \
+  step phaseC timeout -k 10 300 python tools/phase_times.py multi_classifier && \
+  export MDA_CLEAN_EXIT=1 && \
+  step prof_C timeout -s KILL 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_C \
+      -- python bench.py --model multi_classifier --steps 12 --warmup 2 --no-tune --heldout 0 && \
+  step kernels_C python tools/prof_summary.py gpurun_out/prof_C 6
+fi
