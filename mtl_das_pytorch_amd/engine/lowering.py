@@ -3,6 +3,7 @@ fused BN tails and their backward, wgrad finalize, fused Adam + weight packing, 
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch

@@ -223,3 +223,12 @@ if [ "$what" = final ]; then
       -- python bench.py --model multi_classifier --steps 12 --warmup 2 --no-tune --heldout 0 && \
   step kernels_C python tools/prof_summary.py gpurun_out/prof_C 6
 fi
+if [ "$what" = final2 ]; then
+  step benchA1 timeout -k 10 200 python bench.py --steps 300 --warmup 30 && \
+  step benchA2 timeout -k 10 200 python bench.py && \
+  step benchBe timeout -k 10 200 python bench.py --model single_event --steps 300 --warmup 30 --heldout 0 && \
+  step benchBd timeout -k 10 200 python bench.py --model single_distance --steps 300 --warmup 30 --heldout 0 && \
+  step benchC1 timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 && \
+  step phaseA timeout -k 10 200 python tools/phase_times.py MTL && \
+  step engtests timeout -k 10 400 python -u -m pytest tests/test_engine_gpu.py tests/test_mtl_layer_local_gpu.py tests/test_rccl_gpu.py -q -x --timeout 120 --timeout-method thread
+fi
