@@ -17,7 +17,8 @@ import torch
 
 from ..ops.functional import (CONV_DEEP_CFG0, CONV_DEEP_NCFG, CONV_GLDS_CFG0, CONV_GLDS_NCFG, CONV_LDS_CFG0,
                               CONV_LDS_NCFG, CONV_PATCH_CFG0, CONV_PATCH_NCFG, CONV_PATCHP_CFG0, CONV_PATCHP_NCFG,
-                              CONV_XCD, GDEEP_TILES, WGRAD_PATCH, WGRAD_TILES, conv_workspace, glds_cfg)
+                              CONV_XCD, GDEEP_TILES, WGRAD_BIG0, WGRAD_PATCH, WGRAD_TILES, conv_workspace,
+                              glds_cfg)
 from ..ops.hip import lib
 
 # conv.hip register-pipelined tiles 0-13 (pipeline depth 2, and 4 at CONV_DEEP_CFG0 + tile), then
@@ -222,7 +223,8 @@ def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False
     return cache
 
 
-def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passes: int = 1) -> Dict[str, int]:
+def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passes: int = 1,
+                       init_big: bool = False) -> Dict[str, int]:
     """Choose the weight-gradient configs by the time of the BATCHED launches they end up in.
 
     A conv's weight gradient never runs alone: it is a job of one batched launch per (stream, config)
@@ -230,10 +232,12 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
     staged through LDS, blocks in flight, the finalize's split-slab reads -- not one job's latency, which
     is what the isolated timing of autotune_phases ranks (it favours small tiles with many blocks; in the
     batch the large 32x32x16 tiles, 2-4x fewer staged bytes per output, win on the big layers).  Greedy
-    coordinate descent over the wgrad signatures (costliest first): each valid config is applied, the per-stream config cap (merge_wgrad_cfgs) and the finalize
-    refresh run as the bench runs them, and the sum of the batched launches' and the finalize's isolated
-    graph-replay times decides.  Must run before batch_wgrads (on the per-conv launches).  Updates and
-    returns ``cache``."""
+    coordinate descent over the wgrad signatures (costliest first): each valid config is applied, the
+    per-stream config cap (merge_wgrad_cfgs) and the finalize refresh run as the bench runs them, and the
+    sum of the batched launches' and the finalize's isolated graph-replay times decides.  ``init_big``:
+    start from every im2col conv on the large tile its shape suits (patch configs kept) -- one batch per
+    stream -- instead of the table's choices.  Must run before batch_wgrads (on the per-conv launches).
+    Updates and returns ``cache``."""
     L = lib()
     wg = [l for l in prog.bwd.launches if l.name == "conv_wgrad" and l.owner is not None]
     if not wg:
@@ -267,8 +271,14 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
         d = groups[sig][0].args[2]
         return len(groups[sig]) * d["B"] * d["Ho"] * d["Wo"] * d["Npad"] * d["Kpad"]
 
+    t0 = cost()
+    if init_big:
+        for sig, ls in groups.items():
+            conv = ls[0].owner
+            c = WGRAD_BIG0 + 2 * (conv.Npad > 64) + (conv.Kpad_w > 64)
+            if assign[sig] not in WGRAD_PATCH and all(l.owner.wgrad_valid(c) for l in ls):
+                assign[sig] = c
     best = cost()
-    t0 = best
     for _ in range(passes):
         changed = False
         for sig in sorted(groups, key=weight, reverse=True):

@@ -232,3 +232,14 @@ if [ "$what" = final2 ]; then
   step phaseA timeout -k 10 200 python tools/phase_times.py MTL && \
   step engtests timeout -k 10 400 python -u -m pytest tests/test_engine_gpu.py tests/test_mtl_layer_local_gpu.py tests/test_rccl_gpu.py -q -x --timeout 120 --timeout-method thread
 fi
+if [ "$what" = wgbig2 ]; then
+  step wgb3 timeout -k 10 600 python -u tools/retune.py --keep --wgrad-batches --wgrad-big-init --models multi_classifier \
+      --out gpurun_out/tuned_wgb3.json && \
+  cp gpurun_out/tuned_wgb3.json mtl_das_pytorch_amd/engine/tuned_wgb3.json && \
+  for r in 1 2 3; do
+    step benchC_ship$r timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 && \
+    step benchC_wgb3_$r env MDA_TUNED_CFGS=mtl_das_pytorch_amd/engine/tuned_wgb3.json timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
+  done
+  step wgassign_ship timeout -k 10 300 python tools/wgrad_assign.py multi_classifier table && \
+  step wgassign_wgb3 env MDA_TUNED_CFGS=mtl_das_pytorch_amd/engine/tuned_wgb3.json timeout -k 10 300 python tools/wgrad_assign.py multi_classifier table
+fi

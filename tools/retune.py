@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--margin", type=float, default=0.002, help="in-context: relative step-time gain to keep a config")
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--drop", default="", help="with --keep: comma-separated key prefixes to re-measure (e.g. wgrad)")
+    ap.add_argument("--wgrad-big-init", action="store_true",
+                    help="--wgrad-batches starts from every im2col conv on its large tile")
     ap.add_argument("--wgrad-batches", action="store_true",
                     help="re-choose the weight-gradient configs by their batched launches' time (tune_wgrad_batches)")
     ap.add_argument("--spill", action="store_true",
@@ -83,7 +85,7 @@ def main():
         print(f"{name}: {len(cache) - n0} new entries in {time.time() - t0:.1f} s", flush=True)
         if args.wgrad_batches and name in ("MTL", "multi_classifier"):
             _warm_step(prog, name, args.batch)
-            tune_wgrad_batches(prog, cache, verbose=True)
+            tune_wgrad_batches(prog, cache, verbose=True, passes=2, init_big=args.wgrad_big_init)
             print(f"{name}: weight-gradient batches tuned at {time.time() - t0:.1f} s", flush=True)
         if args.spill and name in ("MTL", "multi_classifier"):
             X, d, e = generate(4 * args.batch, seed=3, device="cuda")
