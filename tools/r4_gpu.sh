@@ -243,3 +243,9 @@ if [ "$what" = wgbig2 ]; then
   step wgassign_ship timeout -k 10 300 python tools/wgrad_assign.py multi_classifier table && \
   step wgassign_wgb3 env MDA_TUNED_CFGS=mtl_das_pytorch_amd/engine/tuned_wgb3.json timeout -k 10 300 python tools/wgrad_assign.py multi_classifier table
 fi
+if [ "$what" = final3 ]; then
+  step gputests timeout -k 10 600 python -u -m pytest tests -m gpu --maxfail=5 -q --timeout 120 --timeout-method thread && \
+  step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" && \
+  step benchA timeout -k 10 200 python bench.py && \
+  step benchC timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20
+fi
