@@ -483,24 +483,25 @@ class LoweredProgram:
         buckets = getattr(self, "buckets", None) or [(0, f.numel)]
         ph = Phase("backward_dp")
         ph.alias = dict(self.bwd.alias)
-        n = 0
+        fins = [l for l in self.bwd.launches if l.name == "wgrad_finalize"]
+        last = {l.bucket: l for l in fins}  # a bucket may be finalized by several streams (SIDE_FINALIZE)
+        done = {}
         for l in self.bwd.launches:
             if l.name == "cut":
                 continue
             if l.name != "wgrad_finalize":
                 ph.launches.append(l)
                 continue
-            if l.record is not None:
-                raise ValueError("a gradient bucket's finalize already records an event")
-            tag = f"bucket{l.bucket}_grads"
+            tag = l.record or f"bucket{l.bucket}_grads_{len(done.get(l.bucket, []))}"
             ph.launches.append(Launch(l.name, l.fn, *l.args, owner=l.owner, stream=l.stream, waits=l.waits,
                                       record=tag, bucket=l.bucket))
-            lo, hi = buckets[l.bucket]
-            ph.launches.append(Launch("allreduce_grads", k_allreduce, allreduce, f.grads[lo:hi], stream=COMM_STREAM,
-                                      waits=(tag,), bucket=l.bucket))
-            n += 1
-        if n != len(buckets):
-            raise ValueError(f"{n} finalize launches for {len(buckets)} gradient buckets")
+            done.setdefault(l.bucket, []).append(tag)
+            if l is last[l.bucket]:
+                lo, hi = buckets[l.bucket]
+                ph.launches.append(Launch("allreduce_grads", k_allreduce, allreduce, f.grads[lo:hi],
+                                          stream=COMM_STREAM, waits=tuple(done[l.bucket]), bucket=l.bucket))
+        if sorted(done) != list(range(len(buckets))):
+            raise ValueError(f"finalize launches for buckets {sorted(done)}, expected {len(buckets)} buckets")
         return ph
 
     WGRAD_MAX_BATCHES = 3
@@ -581,6 +582,9 @@ class LoweredProgram:
         self.n_wgrad_spilled = n
         return n
 
+    # MDA_SIDE_FINALIZE=1: side streams finalize their own weight gradients (batch_wgrads)
+    SIDE_FINALIZE = os.environ.get("MDA_SIDE_FINALIZE", "1") == "1"
+
     def batch_wgrads(self):
         """Replace the per-conv weight-gradient launches by batched launches, one per (stream, tile
         config) (csrc/conv.hip conv_wgrad_batched_kernel).  Each stream's batch goes after that stream's
@@ -625,6 +629,26 @@ class LoweredProgram:
             batched[-1].record = f"wgrads_s{st}"
             tags.append(batched[-1].record)
             inserts.append((pos, batched))
+        if self.SIDE_FINALIZE:
+            # every side stream reduces its own convs' split slabs right after its batches (overlapping
+            # stream 0's remaining chain); the tail finalize keeps stream 0's convs
+            side = {}
+            for l in wg:
+                if l.stream != 0 and l.owner is not None:
+                    side.setdefault(l.stream, []).append(l.owner)
+            for pos_batched in inserts:
+                batched = pos_batched[1]
+                st = batched[-1].stream
+                if st in side:
+                    convs = list(dict.fromkeys(side[st]))
+                    tag = f"wgfin_s{st}"
+                    batched.append(Launch("wgrad_finalize", k_wgfin, *self._wgfin_args(convs), owner=convs, stream=st,
+                                          record=tag))
+                    tags = [t for t in tags if t != batched[-2].record] + [tag]
+            rest = [c for c in self.convs if not any(c in v for v in side.values())]
+            if side and rest:
+                ls[fin].owner = rest
+                ls[fin].args = self._wgfin_args(rest)
         for pos, batched in sorted(inserts, key=lambda x: -x[0]):
             keep[pos:pos] = batched
         for l in keep:  # the per-conv "wgrads" event is gone

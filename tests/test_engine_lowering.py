@@ -109,7 +109,7 @@ def test_inception_program_structure():
 
 def test_wgrad_batching_structure():
     """All per-conv weight-gradient launches collapse into one launch per (stream, tile config); every conv
-    appears in exactly one job table and one finalize waits for every stream's last batch."""
+    appears in exactly one job table and exactly one finalize."""
     p = MTLProgram(MTL_Net(), 32, "cpu")
     n_wg = sum(1 for l in p.bwd.launches if l.name == "conv_wgrad")
     p.batch_wgrads()
@@ -118,7 +118,13 @@ def test_wgrad_batching_structure():
     fin = p.bwd.launches[-1]
     assert fin.name == "wgrad_finalize" and fin.stream == 0
     fins = [l for l in p.bwd.launches if l.name == "wgrad_finalize"]
-    assert len(fins) == 1 and set(fin.waits) == {f"wgrads_s{s}" for s in {l.stream for l in b}}
+    # side streams finalize their own convs right after their batches; the tail finalize keeps stream 0's
+    # and waits for stream 0's batches and every side finalize; every conv is finalized exactly once
+    side = [l for l in fins if l.stream != 0]
+    assert {l.stream for l in side} == {l.stream for l in b} - {0}
+    assert set(fin.waits) == {"wgrads_s0"} | {l.record for l in side}
+    owners = [c for l in fins for c in l.owner]
+    assert len(owners) == len(set(map(id, owners))) == len(p.convs)
     _check_event_order(p.bwd)
 
 
@@ -290,9 +296,10 @@ def test_spill_wgrads(model):
     fork = next(i for i, l in enumerate(ls) if l.record == "wgspill")
     sp = [i for i, l in enumerate(ls) if l.stream == SPILL_STREAM]
     assert sp and sp[0] == fork + 1 and ls[sp[0]].waits == ("wgspill",)
-    assert all(l.name == "wgrad_batched" for l in (ls[i] for i in sp))
-    fin = next(l for l in ls if l.name == "wgrad_finalize")
-    assert f"wgrads_s{SPILL_STREAM}" in fin.waits
+    assert all(l.name == "wgrad_batched" for l in (ls[i] for i in sp[:-1]))
+    # the spill stream finalizes its own convs after its batches; the tail finalize waits for that
+    assert ls[sp[-1]].name == "wgrad_finalize" and ls[sp[-1]].record == f"wgfin_s{SPILL_STREAM}"
+    assert f"wgfin_s{SPILL_STREAM}" in ls[-1].waits
 
 
 def test_inception_tail_batches_structure():

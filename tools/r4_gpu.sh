@@ -249,3 +249,21 @@ if [ "$what" = final3 ]; then
   step benchA timeout -k 10 200 python bench.py && \
   step benchC timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20
 fi
+if [ "$what" = sidefin ]; then
+  for r in 1 2; do
+    for v in 0 1; do
+      step benchA_sf${v}_$r env MDA_SIDE_FINALIZE=$v timeout -k 10 200 python bench.py --steps 300 --warmup 30 --heldout 0 && \
+      step benchC_sf${v}_$r env MDA_SIDE_FINALIZE=$v timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --heldout 0 || exit $?
+    done
+  done
+fi
+if [ "$what" = sidefin2 ]; then
+  for r in 1 2 3; do
+    for v in 1 0; do
+      step benchC_sfb${v}_$r env MDA_SIDE_FINALIZE=$v timeout -k 10 300 python bench.py --model multi_classifier --steps 200 --warmup 20 --heldout 0 || exit $?
+    done
+  done
+  for v in 1 0; do
+    step benchA_sfb${v} env MDA_SIDE_FINALIZE=$v timeout -k 10 200 python bench.py --steps 500 --warmup 30 --heldout 0 || exit $?
+  done
+fi
