@@ -380,6 +380,7 @@ void adam_pack(int64_t stream, py::dict d) {
   a.b1 = (float)F(d, "b1", 0.9); a.b2 = (float)F(d, "b2", 0.999); a.eps = (float)F(d, "eps", 1e-8);
   a.wd = (float)F(d, "wd", 0.0); a.grad_scale = (float)F(d, "grad_scale", 1.0);
   a.update = (int)I(d, "update", 1);
+  a.inc_step = (int)I(d, "inc_step", 1);
   check(launch_adam_pack(a, P<const OptSeg>(d, "segs"), (int)I(d, "nsegs"), I(d, "nblocks"), S(stream)), "adam_pack");
 }
 

@@ -244,6 +244,7 @@ struct AdamArgs {
   const float* lr; const float* step;  // device scalars (step = number of completed steps)
   float b1, b2, eps, wd, grad_scale;
   int update;  // 0: pack only
+  int inc_step;  // advance the step counter after the update (0: a partial update -- another launch of the step does)
 };
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);

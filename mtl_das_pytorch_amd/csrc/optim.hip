@@ -153,7 +153,7 @@ int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nb
   if (nblocks <= 0 || nblocks >= (1ll << 31)) return -2;
   hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, a, d_segs, ns);
   int rc = (int)hipGetLastError();
-  if (rc || !a.update) return rc;
+  if (rc || !a.update || !a.inc_step) return rc;
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, const_cast<float*>(a.step));
   return (int)hipGetLastError();
 }

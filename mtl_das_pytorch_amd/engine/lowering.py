@@ -582,8 +582,10 @@ class LoweredProgram:
         self.n_wgrad_spilled = n
         return n
 
-    # MDA_SIDE_FINALIZE=1: side streams finalize their own weight gradients (batch_wgrads)
+    # MDA_SIDE_FINALIZE=1: side streams finalize their own weight gradients (batch_wgrads); MDA_EARLY_ADAM=1: and
+    # update them (single process)
     SIDE_FINALIZE = os.environ.get("MDA_SIDE_FINALIZE", "1") == "1"
+    EARLY_ADAM = os.environ.get("MDA_EARLY_ADAM", "1") == "1"
 
     def batch_wgrads(self):
         """Replace the per-conv weight-gradient launches by batched launches, one per (stream, tile
@@ -649,6 +651,32 @@ class LoweredProgram:
             if side and rest:
                 ls[fin].owner = rest
                 ls[fin].args = self._wgfin_args(rest)
+            if side and self.EARLY_ADAM and self._opt_hparams.get("grad_scale", 1.0) == 1.0:
+                # single process: the side convs' Adam + re-pack right after their finalize, on their stream
+                # (the optimizer phase then covers the rest); with gradient averaging (DP) the update must wait
+                # for the all-reduce, so it stays in the optimizer phase
+                early = set()
+                for pos_batched in inserts:
+                    batched = pos_batched[1]
+                    st = batched[-1].stream
+                    if st not in side:
+                        continue
+                    offs = {self.flat.off(m.weight) for c in side[st] for m in c.mods}
+                    segs = [g for g in self.opt_segs if g["kind"] == 3 and g["off"] in offs]
+                    early |= offs
+                    table, ns, nb = build_optseg_table(segs, self.device)
+                    self._opt_tables = getattr(self, "_opt_tables", []) + [table]
+                    d = dict(self._opt_base, segs=P(table), nsegs=ns, nblocks=nb, update=1, inc_step=0,
+                             **self._opt_hparams)
+                    tag = f"adam_s{st}"
+                    batched.append(Launch("adam_pack_early", k_adam, d, stream=st, record=tag))
+                    tags = [t for t in tags if t != f"wgfin_s{st}"] + [tag]
+                    self._early_adam = getattr(self, "_early_adam", []) + [d]
+                segs = [g for g in self.opt_segs if not (g["kind"] == 3 and g["off"] in early)]
+                table, ns, nb = build_optseg_table(segs, self.device)
+                self._opt_tables = getattr(self, "_opt_tables", []) + [table]
+                self._opt_base = dict(self._opt_base, segs=P(table), nsegs=ns, nblocks=nb)
+                self.set_optimizer(**self._opt_kwargs)
         for pos, batched in sorted(inserts, key=lambda x: -x[0]):
             keep[pos:pos] = batched
         for l in keep:  # the per-conv "wgrads" event is gone
@@ -732,6 +760,7 @@ class LoweredProgram:
                 "lr": P(f.lr), "step": P(f.step), "segs": P(self.optseg_table), "nsegs": ns, "nblocks": nblocks}
         self._opt_base = base
         self._opt_hparams = dict(b1=0.9, b2=0.999, eps=1e-8, wd=0.0, grad_scale=grad_scale)
+        self._opt_kwargs = dict(betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, grad_scale=grad_scale)
         upd = Phase("adam")
         upd.add("adam_pack", k_adam, dict(base, update=1, **self._opt_hparams))
         pack = Phase("pack")
@@ -739,7 +768,12 @@ class LoweredProgram:
         return {"adam": upd, "pack": pack}
 
     def set_optimizer(self, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, grad_scale: float = 1.0):
+        self._opt_kwargs = dict(betas=betas, eps=eps, weight_decay=weight_decay, grad_scale=grad_scale)
         self._opt_hparams = dict(b1=betas[0], b2=betas[1], eps=eps, wd=weight_decay, grad_scale=grad_scale)
+        if getattr(self, "_early_adam", None) and grad_scale != 1.0:
+            raise RuntimeError("the weight updates already run inside the backward: gradient averaging would miss them")
+        for d in getattr(self, "_early_adam", []):  # the side streams' partial updates (batch_wgrads)
+            d.update(self._opt_hparams)
         upd = Phase("adam")
         upd.add("adam_pack", k_adam, dict(self._opt_base, update=1, **self._opt_hparams))
         self.opt["adam"] = upd

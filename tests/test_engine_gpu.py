@@ -320,3 +320,43 @@ def test_training_trajectory_matches_fp32_oracle():
     e, bound = rel(upd_e, upd_r), 1.5 * rel(upd_n, upd_r) + 0.05
     print(f"3-step update: engine vs oracle {e:.3f}, noisy oracle vs oracle {rel(upd_n, upd_r):.3f}")
     assert e <= bound, (e, bound)
+
+
+@pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
+def test_early_adam_matches_optimizer_phase(model_name, monkeypatch):
+    """Side streams finalize AND update their convs right after their weight-gradient batches
+    (LoweredProgram.SIDE_FINALIZE / EARLY_ADAM); two training steps give bitwise the parameters, moments and
+    bf16 weight images of the program whose optimizer phase updates everything."""
+    from mtl_das_pytorch_amd.data.synthetic import generate
+    from mtl_das_pytorch_amd.engine.lowering import LoweredProgram
+    from mtl_das_pytorch_amd.engine.tune import autotune_program
+    from mtl_das_pytorch_amd.models import build_model, encode_joint
+    res = []
+    for early in (False, True):
+        monkeypatch.setattr(LoweredProgram, "EARLY_ADAM", early)
+        torch.manual_seed(0)
+        m = build_model(model_name)
+        if model_name == "multi_classifier":
+            from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+            prog = InceptionProgram(m, 8, "cuda", p_drop=0.0)
+        else:
+            from mtl_das_pytorch_amd.engine.mtl import MTLProgram
+            prog = MTLProgram(m, 8, "cuda")
+        prog.set_optimizer(weight_decay=1e-5)
+        autotune_program(prog, measure=False)
+        assert any(l.name == "adam_pack_early" for l in prog.bwd.launches) == early
+        prog.flat.lr.fill_(1e-3)
+        X, d, e = generate(16, seed=1, device="cuda")
+        lab = encode_joint(d, e) if model_name == "multi_classifier" else torch.stack([d, e], 1)
+        prog.opt["pack"].run()
+        for s in range(2):
+            prog.gather_phase(X, lab, torch.arange(8, device="cuda") + 8 * s, clear=True).run()
+            prog.fwd_train.run()
+            prog.bwd.run()
+            prog.opt["adam"].run()
+        torch.cuda.synchronize()
+        f = prog.flat
+        res.append([f.params.clone(), f.exp_avg.clone(), f.exp_avg_sq.clone(), f.step.clone()]
+                   + [c.wf.clone() for c in prog.convs] + [c.wd.clone() for c in prog.convs])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

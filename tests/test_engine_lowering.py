@@ -122,7 +122,10 @@ def test_wgrad_batching_structure():
     # and waits for stream 0's batches and every side finalize; every conv is finalized exactly once
     side = [l for l in fins if l.stream != 0]
     assert {l.stream for l in side} == {l.stream for l in b} - {0}
-    assert set(fin.waits) == {"wgrads_s0"} | {l.record for l in side}
+    # (with EARLY_ADAM each side stream's last launch is its partial Adam update, which the tail waits for)
+    last = {st: [l for l in p.bwd.launches if l.stream == st][-1] for st in {l.stream for l in side}}
+    assert set(fin.waits) == {"wgrads_s0"} | {l.record for l in last.values()}
+    assert all(l.name == ("adam_pack_early" if p.EARLY_ADAM else "wgrad_finalize") for l in last.values())
     owners = [c for l in fins for c in l.owner]
     assert len(owners) == len(set(map(id, owners))) == len(p.convs)
     _check_event_order(p.bwd)
@@ -296,10 +299,12 @@ def test_spill_wgrads(model):
     fork = next(i for i, l in enumerate(ls) if l.record == "wgspill")
     sp = [i for i, l in enumerate(ls) if l.stream == SPILL_STREAM]
     assert sp and sp[0] == fork + 1 and ls[sp[0]].waits == ("wgspill",)
-    assert all(l.name == "wgrad_batched" for l in (ls[i] for i in sp[:-1]))
-    # the spill stream finalizes its own convs after its batches; the tail finalize waits for that
-    assert ls[sp[-1]].name == "wgrad_finalize" and ls[sp[-1]].record == f"wgfin_s{SPILL_STREAM}"
-    assert f"wgfin_s{SPILL_STREAM}" in ls[-1].waits
+    tail = 2 if p.EARLY_ADAM else 1  # the stream's finalize (and partial Adam) follow its batches
+    assert all(l.name == "wgrad_batched" for l in (ls[i] for i in sp[:-tail]))
+    # the spill stream finalizes (and with EARLY_ADAM updates) its own convs after its batches; the tail
+    # finalize waits for that
+    assert ls[sp[-1]].name == ("adam_pack_early" if p.EARLY_ADAM else "wgrad_finalize")
+    assert ls[sp[-1]].record in ls[-1].waits
 
 
 def test_inception_tail_batches_structure():

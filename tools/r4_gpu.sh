@@ -267,3 +267,22 @@ if [ "$what" = sidefin2 ]; then
     step benchA_sfb${v} env MDA_SIDE_FINALIZE=$v timeout -k 10 200 python bench.py --steps 500 --warmup 30 --heldout 0 || exit $?
   done
 fi
+if [ "$what" = early ]; then
+  step eatests timeout -k 10 500 python -u -m pytest tests/test_engine_gpu.py tests/test_rccl_gpu.py tests/test_inception_gpu.py \
+      tests/test_mtl_layer_local_gpu.py -x -v --timeout 120 --timeout-method thread && \
+  for r in 1 2 3; do
+    for v in 1 0; do
+      step benchC_ea${v}_$r env MDA_EARLY_ADAM=$v timeout -k 10 300 python bench.py --model multi_classifier --steps 200 --warmup 20 --heldout 0 || exit $?
+    done
+  done
+  for v in 1 0; do
+    step benchA_ea${v} env MDA_EARLY_ADAM=$v timeout -k 10 200 python bench.py --steps 500 --warmup 30 --heldout 0 || exit $?
+  done
+fi
+if [ "$what" = earlyA ]; then
+  for r in 1 2 3; do
+    for v in 1 0; do
+      step benchA_eb${v}_$r env MDA_EARLY_ADAM=$v timeout -k 10 200 python bench.py --steps 500 --warmup 30 --heldout 0 || exit $?
+    done
+  done
+fi
