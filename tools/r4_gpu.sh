@@ -286,3 +286,8 @@ if [ "$what" = earlyA ]; then
     done
   done
 fi
+if [ "$what" = accfinal ]; then
+  for sd in 0 1 2; do
+    step accf$sd timeout -k 10 400 python -X faulthandler -u tools/accuracy_table.py --seeds $sd --out gpurun_out/accf$sd || exit $?
+  done
+fi
