@@ -582,10 +582,10 @@ class LoweredProgram:
         self.n_wgrad_spilled = n
         return n
 
-    # MDA_SIDE_FINALIZE=1: side streams finalize their own weight gradients (batch_wgrads); MDA_EARLY_ADAM=1: and
-    # update them (single process)
-    SIDE_FINALIZE = os.environ.get("MDA_SIDE_FINALIZE", "1") == "1"
-    EARLY_ADAM = os.environ.get("MDA_EARLY_ADAM", "1") == "1"
+    # side streams finalize their own weight gradients (batch_wgrads) and, in a single process, update them:
+    # C +0.6-7.5 % / A neutral, and A +0.3-0.6 % / C neutral (docs/PERF.md round 4); class switches for A/B runs
+    SIDE_FINALIZE = True
+    EARLY_ADAM = True
 
     def batch_wgrads(self):
         """Replace the per-conv weight-gradient launches by batched launches, one per (stream, tile
