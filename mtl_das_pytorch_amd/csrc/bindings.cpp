@@ -7,8 +7,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "kernels.h"
@@ -437,5 +439,125 @@ PYBIND11_MODULE(_mda_hip, m) {
   });
   m.def("adam_pack", &adam_pack);
   m.def("hip_device_sync", []() { return (int)hipDeviceSynchronize(); });
+  // engine-owned streams (engine/program.py EngineStreams): created once per device, never drawn from
+  // torch's round-robin stream pool, so they cannot alias a capture stream or each other
+  m.def("stream_create", [](int priority) {
+    hipStream_t s = nullptr;
+    check((int)hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority), "hipStreamCreateWithPriority");
+    return static_cast<int64_t>(reinterpret_cast<intptr_t>(s));
+  });
+  m.def("stream_destroy", [](int64_t s) { check((int)hipStreamDestroy(S(s)), "hipStreamDestroy"); });
+  m.def("stream_priority_range", []() {
+    int least = 0, greatest = 0;
+    check((int)hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+    return py::make_tuple(least, greatest);
+  });
+  // ---- captured-graph surgery (engine/graphsched.py): read a capture's DAG, rewrite its edge order ----
+  // the graph a stream is capturing into, and the node count so far (0, 0 when not capturing)
+  m.def("capture_graph_count", [](int64_t stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    hipGraph_t g = nullptr;
+    check((int)hipStreamGetCaptureInfo_v2(S(stream), &st, nullptr, &g, nullptr, nullptr), "hipStreamGetCaptureInfo_v2");
+    if (st != hipStreamCaptureStatusActive || g == nullptr) return py::make_tuple((int64_t)0, (int64_t)0);
+    size_t n = 0;
+    check((int)hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
+    return py::make_tuple(static_cast<int64_t>(reinterpret_cast<intptr_t>(g)), (int64_t)n);
+  });
+  // the last node(s) a capturing stream's next node will depend on
+  m.def("capture_tail", [](int64_t stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    check((int)hipStreamGetCaptureInfo_v2(S(stream), &st, nullptr, nullptr, &deps, &nd), "hipStreamGetCaptureInfo_v2");
+    py::list out;
+    for (size_t i = 0; i < nd; ++i) out.append(static_cast<int64_t>(reinterpret_cast<intptr_t>(deps[i])));
+    return out;
+  });
+  // which logical (engine) stream created each node of a capture: note() after every launch tags the
+  // nodes that appeared since the previous note with that launch's target stream
+  struct CaptureTracker {
+    std::unordered_map<hipGraphNode_t, int> tag;
+    void note(int64_t stream, int target) {
+      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+      hipGraph_t g = nullptr;
+      check((int)hipStreamGetCaptureInfo_v2(S(stream), &st, nullptr, &g, nullptr, nullptr), "hipStreamGetCaptureInfo_v2");
+      if (st != hipStreamCaptureStatusActive || g == nullptr) return;
+      size_t n = 0;
+      check((int)hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
+      if (n == tag.size()) return;
+      std::vector<hipGraphNode_t> nodes(n);
+      check((int)hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
+      for (auto x : nodes) tag.emplace(x, target);  // only inserts the new ones
+    }
+    py::list targets(int64_t graph) const {
+      hipGraph_t g = reinterpret_cast<hipGraph_t>(static_cast<intptr_t>(graph));
+      size_t n = 0;
+      check((int)hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
+      std::vector<hipGraphNode_t> nodes(n);
+      check((int)hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
+      py::list out;
+      for (auto x : nodes) {
+        auto it = tag.find(x);
+        if (it == tag.end()) out.append(py::none()); else out.append(it->second);
+      }
+      return out;
+    }
+  };
+  py::class_<CaptureTracker>(m, "CaptureTracker")
+      .def(py::init<>())
+      .def("note", &CaptureTracker::note)
+      .def("targets", &CaptureTracker::targets)
+      .def("size", [](const CaptureTracker& t) { return t.tag.size(); });
+  // nodes (runtime order) and, per node, its children in edge-insertion order as node indices
+  m.def("graph_structure", [](int64_t graph) {
+    hipGraph_t g = reinterpret_cast<hipGraph_t>(static_cast<intptr_t>(graph));
+    size_t n = 0;
+    check((int)hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
+    std::vector<hipGraphNode_t> nodes(n);
+    check((int)hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
+    py::list handles, children;
+    std::vector<std::pair<hipGraphNode_t, int64_t>> idx;
+    idx.reserve(n);
+    for (size_t i = 0; i < n; ++i) idx.emplace_back(nodes[i], (int64_t)i);
+    std::sort(idx.begin(), idx.end());
+    auto find = [&](hipGraphNode_t x) {
+      auto it = std::lower_bound(idx.begin(), idx.end(), std::make_pair(x, (int64_t)-1));
+      if (it == idx.end() || it->first != x) throw std::runtime_error("graph_structure: unknown node");
+      return it->second;
+    };
+    for (size_t i = 0; i < n; ++i) {
+      handles.append(static_cast<int64_t>(reinterpret_cast<intptr_t>(nodes[i])));
+      size_t nc = 0;
+      check((int)hipGraphNodeGetDependentNodes(nodes[i], nullptr, &nc), "hipGraphNodeGetDependentNodes");
+      std::vector<hipGraphNode_t> ch(nc);
+      if (nc) check((int)hipGraphNodeGetDependentNodes(nodes[i], ch.data(), &nc), "hipGraphNodeGetDependentNodes");
+      py::list row;
+      for (size_t j = 0; j < nc; ++j) row.append(find(ch[j]));
+      children.append(row);
+    }
+    return py::make_tuple(handles, children);
+  });
+  // replace every edge of the graph by ``children`` (per node index, in the wanted insertion order)
+  m.def("graph_set_children", [](int64_t graph, py::list children) {
+    hipGraph_t g = reinterpret_cast<hipGraph_t>(static_cast<intptr_t>(graph));
+    size_t n = 0;
+    check((int)hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
+    std::vector<hipGraphNode_t> nodes(n);
+    check((int)hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
+    if ((size_t)children.size() != n) throw std::runtime_error("graph_set_children: node count mismatch");
+    size_t ne = 0;
+    check((int)hipGraphGetEdges(g, nullptr, nullptr, &ne), "hipGraphGetEdges");
+    std::vector<hipGraphNode_t> from(ne), to(ne);
+    if (ne) {
+      check((int)hipGraphGetEdges(g, from.data(), to.data(), &ne), "hipGraphGetEdges");
+      check((int)hipGraphRemoveDependencies(g, from.data(), to.data(), ne), "hipGraphRemoveDependencies");
+    }
+    for (size_t i = 0; i < n; ++i) {
+      for (auto c : py::list(children[i])) {
+        hipGraphNode_t a = nodes[i], b = nodes[c.cast<size_t>()];
+        check((int)hipGraphAddDependencies(g, &a, &b, 1), "hipGraphAddDependencies");
+      }
+    }
+  });
   register_matio(m);
 }

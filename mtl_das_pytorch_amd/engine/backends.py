@@ -61,6 +61,7 @@ class Backend:
     def sync_bn_stats(self): ...
     def optimizer_state(self) -> dict: ...
     def load_optimizer_state(self, st: dict): ...
+    def close(self): ...
 
 
 def _report_tasks(model_type: str):
@@ -297,6 +298,10 @@ class EngineBackend(Backend):
     def after_load(self):
         """Re-pack bf16 weight images after the fp32 masters were overwritten (checkpoint load)."""
         self.runner.pack_weights()
+
+    def close(self):
+        """Release the step runner's graphs, captured events and replay stream (Trainer.run's exit)."""
+        self.runner.close()
 
 
 def portable_adam_state(st: dict, model: nn.Module):

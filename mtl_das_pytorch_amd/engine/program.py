@@ -24,10 +24,13 @@ from ..ops.hip import lib, stream
 # (join-then-fork points, wgrads on their producer's stream): denser event patterns crashed
 # hipStreamEndCapture on ROCm 7.
 MULTI_STREAM = os.environ.get("MDA_STREAMS", "1") == "1"
-# streams used at most (ids above are folded onto the last one -- still a valid schedule); never more than
-# the process's hardware queues: with GPU_MAX_HW_QUEUES=2 a 4-stream graph segfaults inside the HIP runtime
-# at replay, engine-free repro in tools/hwq_repro.py (profiles/r4_runtime_faults.txt)
-MAX_STREAMS = max(1, min(4, int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))))
+# hardware queues of this process (HIP's default 4): the budget for ALL streams a phase touches -- caller,
+# compute side streams, communication and spill streams.  With more streams than queues a multi-stream
+# graph segfaults inside the HIP runtime at replay (engine-free repro: tools/hwq_repro.py,
+# profiles/r4_runtime_faults.txt).
+HW_QUEUES = max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
+# compute streams used at most (logical ids above are folded onto the last one -- still a valid schedule)
+MAX_STREAMS = max(1, min(4, HW_QUEUES))
 # logical id of the communication stream: data-parallel gradient all-reduces embedded in the backward
 # (LoweredProgram.backward_with_allreduce) run there, beside the compute streams, never folded onto them
 COMM_STREAM = 7
@@ -64,11 +67,110 @@ class Launch:
         self.fn(*self.args, st)
 
 
+def stream_slots(launches, hw_queues: int = None) -> dict:
+    """Logical stream id -> physical slot for one phase, within the hardware-queue budget: slot 0 is the
+    caller's stream, 1..MAX_STREAMS-1 the compute side streams, MAX_STREAMS the communication stream and
+    MAX_STREAMS+1 the spill stream (EngineStreams order).  The communication and spill streams count
+    against the budget: the compute streams shrink first (never below 1), then the spill and finally the
+    communication stream fold onto the last compute stream (a valid schedule, less overlap)."""
+    hwq = HW_QUEUES if hw_queues is None else hw_queues
+    ids = {l.stream for l in launches}
+    comm, spill = COMM_STREAM in ids, SPILL_STREAM in ids
+    ncomp = max(1, min(MAX_STREAMS, hwq - comm - spill))
+    room = hwq - ncomp
+    own_comm = comm and room >= 1
+    own_spill = spill and room >= 1 + own_comm
+    out = {}
+    for s in ids:
+        if s == COMM_STREAM:
+            out[s] = MAX_STREAMS if own_comm else ncomp - 1
+        elif s == SPILL_STREAM:
+            out[s] = MAX_STREAMS + 1 if own_spill else ncomp - 1
+        else:
+            out[s] = min(s, ncomp - 1)
+    return out
+
+
+class EngineStreams:
+    """The HIP streams the engine runs its side branches on: one fixed set per device for the whole process,
+    created with ``hipStreamCreateWithPriority`` by the extension (not drawn from torch's 32-entry
+    round-robin pool, whose streams a phase could share with the graph-capture stream or another phase's
+    streams), and released by :func:`release_streams` (atexit).  Index 0..MAX_STREAMS-2 are the compute
+    side streams, then the communication and the spill stream."""
+
+    _by_device = {}
+
+    def __init__(self, device):
+        import torch
+        self.device = device
+        n = MAX_STREAMS - 1 + 2
+        self.handles = [lib().stream_create(0) for _ in range(n)]
+        self.streams = [torch.cuda.ExternalStream(h, device=device) for h in self.handles]
+
+    @classmethod
+    def get(cls, device):
+        s = cls._by_device.get(device)
+        if s is None:
+            s = cls._by_device[device] = cls(device)
+        return s
+
+    def destroy(self):
+        for h in self.handles:
+            lib().stream_destroy(h)
+        self.handles, self.streams = [], []
+
+
+def release_streams():
+    """Synchronize and destroy the engine's streams (safe to call more than once; they are re-created on
+    demand)."""
+    import torch
+    if not EngineStreams._by_device:
+        return
+    torch.cuda.synchronize()
+    for s in EngineStreams._by_device.values():
+        s.destroy()
+    EngineStreams._by_device.clear()
+
+
+import atexit  # noqa: E402
+
+atexit.register(release_streams)
+
+
+class EventKeeper:
+    """Owner of the events a phase records while a HIP graph is captured: their lifetime is tied to the
+    graph (StepRunner keeps the keeper next to the graph executable and drops both together), so no phase
+    re-run -- eager or another capture -- can destroy an event a live graph was built from."""
+
+    active = None  # the keeper of the capture in progress, if any
+
+    def __init__(self, track: bool = False):
+        self.events = []
+        # tags every captured node with the executor stream its launch should run on (graphsched.restream)
+        self.tracker = lib().CaptureTracker() if track else None
+
+    def __enter__(self):
+        if EventKeeper.active is not None:
+            raise RuntimeError("nested EventKeeper")
+        EventKeeper.active = self
+        return self
+
+    def __exit__(self, *exc):
+        EventKeeper.active = None
+        return False
+
+
 class Phase:
+    # issue order of the launches on the host (the order the capture sees them in): "program" as emitted,
+    # or "main_first": a stream-0 launch whose waits are satisfied is always issued before any side-stream
+    # launch, so that in the captured graph a stream-0 node's first successor edge is the next stream-0 node
+    # (the HIP graph executor walks first edges to build the chain it runs on the launch stream)
+    ISSUE_ORDER = "program"
+
     def __init__(self, name: str):
         self.name = name
         self.launches: List[Launch] = []
-        self._streams = None
+        self._live_events = None
         self.cur_stream = 0      # default stream id for add()
         self.pending_waits = []  # waits attached to the next add() on any stream
         self.alias = {}          # event tag -> tag it is recorded under (after launches were removed)
@@ -96,38 +198,81 @@ class Phase:
 
     def run(self, st=None):
         import torch
+        keeper = EventKeeper.active
+        tracker = keeper.tracker if keeper is not None else None
         if not MULTI_STREAM or all(l.stream == 0 and not l.waits for l in self.launches):
             st = stream() if st is None else st
             for l in self.launches:
                 if l.fn is not None:
                     l(st)
+                    if tracker is not None:
+                        tracker.note(st, 0)
             return
         main = torch.cuda.current_stream()
-        if self._streams is None or self._streams[0].device != main.device:
-            self._streams = [torch.cuda.Stream(device=main.device) for _ in range(MAX_STREAMS + 1)]
-        streams = [main] + self._streams  # [MAX_STREAMS] communication, [MAX_STREAMS + 1] spill stream
-        sid_of = lambda l: (MAX_STREAMS if l.stream == COMM_STREAM else MAX_STREAMS + 1 if l.stream == SPILL_STREAM  # noqa: E731
-                            else min(l.stream, MAX_STREAMS - 1))
-        used = {sid_of(l) for l in self.launches}
+        es = EngineStreams.get(main.device)
+        slot = stream_slots(self.launches)
+        phys = {0: main}
+        for sid in set(slot.values()) - {0}:
+            phys[sid] = es.streams[sid - 1]
         start = main.record_event()
-        for sid in used - {0}:
-            streams[sid].wait_event(start)
+        for sid in phys:
+            if sid:
+                phys[sid].wait_event(start)
         events = {}
-        for l in self.launches:
-            s = streams[sid_of(l)]
+        rank = {sid: i for i, sid in enumerate(sorted(phys))}  # executor stream of each slot (graphsched)
+        for l in self.issue_order():
+            s = phys[slot[l.stream]]
             for tag in l.waits:
                 s.wait_event(events[self.alias.get(tag, tag)])
             l(s.cuda_stream, s)
+            if tracker is not None and l.fn is not None:
+                tracker.note(s.cuda_stream, rank[slot[l.stream]])
             if l.record is not None:
                 events[l.record] = s.record_event()
-        for sid in used - {0}:
-            main.wait_stream(streams[sid])
-        # keep the events alive past this call: under HIP-graph capture they must outlive the capture
-        # (destroying a recorded event while the capture is open crashed hipStreamEndCapture)
-        self._live_events = (start, events)
+        for sid in phys:
+            if sid:
+                main.wait_stream(phys[sid])
+        # keep the events alive past this call: under HIP-graph capture they must live as long as the graph
+        # (destroying a recorded event while the capture is open crashed hipStreamEndCapture), so a capture's
+        # events go to its EventKeeper; an eager run's are held until the phase runs again
+        if keeper is not None:
+            keeper.events.append((start, events))
+        else:
+            self._live_events = (start, events)
+
+    def issue_order(self) -> List[Launch]:
+        """The launches in host issue order (see ISSUE_ORDER); every order returned keeps each stream's own
+        order and issues a wait only after the launch recording its event."""
+        if self.ISSUE_ORDER != "main_first":
+            return self.launches
+        recs = [l.record for l in self.launches if l.record is not None]
+        if len(recs) != len(set(recs)):  # a re-recorded tag: only the program order defines which record a wait sees
+            return self.launches
+        queues: dict = {}
+        for i, l in enumerate(self.launches):
+            queues.setdefault(l.stream, []).append(i)
+        heads = {s: 0 for s in queues}
+        recorded, out = set(), []
+        ready = lambda l: all(self.alias.get(t, t) in recorded for t in l.waits)  # noqa: E731
+        while len(out) < len(self.launches):
+            q0 = queues.get(0)
+            if q0 is not None and heads[0] < len(q0) and ready(self.launches[q0[heads[0]]]):
+                pick = 0
+            else:  # the earliest pending head in program order is always ready (all launches before it issued)
+                pick = min((queues[s][heads[s]], s) for s in queues if heads[s] < len(queues[s]))[1]
+            l = self.launches[queues[pick][heads[pick]]]
+            heads[pick] += 1
+            out.append(l)
+            if l.record is not None:
+                recorded.add(l.record)
+        return out
 
     def __len__(self):
         return len(self.launches)
+
+    def release(self):
+        """Drop the events of the last eager run (the caller has synchronized)."""
+        self._live_events = None
 
     def split(self) -> List["Phase"]:
         """Cut the phase at its pseudo-launches named ``cut`` into consecutive phases.

@@ -25,7 +25,8 @@ from typing import Callable, Dict, List, Optional
 
 import torch
 
-from .program import Phase
+from .program import EventKeeper, Phase
+from ..ops.hip import lib
 
 
 class StateSnapshot:
@@ -40,7 +41,35 @@ class StateSnapshot:
             t.copy_(s)
 
 
+def capture_graph(fns, restream: Optional[bool] = None, error_mode: str = "global"):
+    """Capture ``fns`` (phase runs) into one HIP graph.  Returns (graph, EventKeeper, restream info): the
+    keeper holds the events the capture recorded and must live as long as the graph; with ``restream``
+    (default StepRunner.RESTREAM) the graph's edge order is rewritten before instantiation so that the
+    executor keeps every engine stream on one stream of its own (engine/graphsched.py)."""
+    restream = StepRunner.RESTREAM if restream is None else restream
+    keeper = EventKeeper(track=restream)
+    g = torch.cuda.CUDAGraph(keep_graph=True) if restream else torch.cuda.CUDAGraph()
+    with keeper, torch.cuda.graph(g, capture_error_mode=error_mode):
+        for f in fns:
+            f()
+    info = None
+    if restream:
+        from .graphsched import restream as _restream
+        info = _restream(g.raw_cuda_graph(), keeper.tracker)
+        g.instantiate()
+    return g, keeper, info
+
+
 class StepRunner:
+    # stream the captured graphs are replayed on: None = the caller's current stream; an int = a dedicated
+    # stream of that HIP priority (-1 = high): the graph's first chain runs on the launch stream, its other
+    # branches on streams the HIP graph executor creates at normal priority
+    REPLAY_PRIORITY = None
+    # rewrite each captured graph's edge order so that the HIP graph executor runs every engine stream on a
+    # stream of its own (engine/graphsched.py: the executor otherwise re-derives streams from the DAG and
+    # mixes the critical chain with side work)
+    RESTREAM = True
+
     def __init__(self, program, X: torch.Tensor, labels: torch.Tensor, use_graph: bool = True,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None, X_eval: torch.Tensor = None,
                  labels_eval: torch.Tensor = None):
@@ -53,6 +82,9 @@ class StepRunner:
         if X_eval is not None:
             self.sources["eval"] = (X_eval, labels_eval)
         self.graphs: Dict[str, torch.cuda.CUDAGraph] = {}
+        self.keepers: Dict[str, EventKeeper] = {}  # events each graph was captured with (same lifetime)
+        self._replay = None  # (handle, ExternalStream) of the dedicated replay stream
+        self.restream_info: Dict[str, dict] = {}
         self._packed = False
         self._bwd_pieces = None
         self._bwd_dp = None
@@ -106,7 +138,27 @@ class StepRunner:
                 f()
             return
         self._ensure_graph(kind)
-        self.graphs[kind].replay()
+        if self.REPLAY_PRIORITY is None:
+            self.graphs[kind].replay()
+            return
+        if self._replay is None:
+            h = lib().stream_create(int(self.REPLAY_PRIORITY))
+            self._replay = (h, torch.cuda.ExternalStream(h, device=self.p.device))
+        rs, cur = self._replay[1], torch.cuda.current_stream()
+        rs.wait_stream(cur)
+        with torch.cuda.stream(rs):
+            self.graphs[kind].replay()
+        cur.wait_stream(rs)
+
+    def _drop_graph(self, kind: str):
+        """Release one captured graph and the events it was captured with, after the device has finished
+        every replay of it (destroying an executable that may still run is undefined)."""
+        g = self.graphs.pop(kind, None)
+        if g is None:
+            return
+        torch.cuda.synchronize()
+        g.reset()
+        self.keepers.pop(kind, None)
 
     def _ensure_graph(self, kind: str):
         """Warm up (side effects rolled back) and capture the graph of ``kind`` once."""
@@ -123,15 +175,15 @@ class StepRunner:
             torch.cuda.synchronize()
             snap.restore()
             self.p.opt["pack"].run()  # the bf16 weight images are derived state: rebuild from restored masters
-            g = torch.cuda.CUDAGraph()
             # Collectives captured here run on the capture-only RCCL communicator (DistContext.capture_group),
             # which never has eager work for the process-group watchdog to poll; the capture is thread-local
             # so that the watchdog's polls of the default communicator's eager work stay legal meanwhile.
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                for f in fns:
-                    f()
+            g, keeper, info = capture_graph(fns, self.RESTREAM, "thread_local")
+            if info is not None:
+                self.restream_info[kind] = info
             torch.cuda.synchronize()
             self.graphs[kind] = g
+            self.keepers[kind] = keeper
 
     # -------------------------------------------------------------------------------------------
     def set_lr(self, lr: float):
@@ -170,7 +222,7 @@ class StepRunner:
         if cur is not None and cur[0] is X and cur[1] is labels:
             return
         self.sources["eval"] = (X, labels)
-        self.graphs.pop("eval", None)
+        self._drop_graph("eval")
 
     def eval_step(self, idx: torch.Tensor):
         if not self._packed:
@@ -183,20 +235,21 @@ class StepRunner:
         self.p.confusion.zero_()
 
     def close(self):
-        """Release every HIP object the runner and its program's phases hold -- graph executables, the phases'
-        side streams and recorded events -- while the HIP runtime is certainly alive (at interpreter exit the
+        """Release every HIP object the runner and its program's phases hold -- graph executables with the
+        events they were captured with, the phases' last eager events, the replay stream -- while the HIP runtime is certainly alive (at interpreter exit the
         order in which module globals, the runtime and these objects are finalised is not defined).  The
         runner can be used again afterwards (graphs are re-captured on demand)."""
         torch.cuda.synchronize()
-        for g in self.graphs.values():
-            g.reset()
-        self.graphs.clear()
+        for k in list(self.graphs):
+            self._drop_graph(k)
         p = self.p
         phases = [p.fwd_train, p.fwd_eval, p.bwd] + list(p.opt.values()) + list(self._bwd_pieces or [])
         if self._bwd_dp is not None:
             phases.append(self._bwd_dp)
         for ph in phases:
-            ph._live_events = None
-            ph._streams = None
+            ph.release()
         self._bwd_pieces = self._bwd_dp = None
+        if self._replay is not None:
+            lib().stream_destroy(self._replay[0])
+            self._replay = None
         torch.cuda.synchronize()

@@ -220,11 +220,22 @@ class Trainer:
                         np.save(p, self._train_line(name))
                 plot_curves(self.save_dir, cfg.model)
         self.ctx.barrier()
+        self.close()
+        return self.save_dir
+
+    def close(self):
+        """Release the backend's device objects (graphs, events, streams), the data sources and the log.
+        ``run`` calls it at its end; ``evaluate`` still works afterwards (it re-captures its graph; call ``close``
+        again when done)."""
+        if getattr(self, "backend", None) is not None:
+            self.backend.close()  # idempotent; graphs captured by a later ``evaluate`` are released again
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
         for src in {id(self.train_src): self.train_src, id(self.val_src): self.val_src}.values():
             src.close()
         self.logger.save()
         self.logger.close()
-        return self.save_dir
 
     # --------------------------------------------------------------------------------------------
     def _train_line(self, name):

@@ -20,6 +20,7 @@ from ..ops.functional import (CONV_DEEP_CFG0, CONV_DEEP_NCFG, CONV_GLDS_CFG0, CO
                               CONV_XCD, GDEEP_TILES, WGRAD_BIG0, WGRAD_PATCH, WGRAD_TILES, conv_workspace,
                               glds_cfg)
 from ..ops.hip import lib
+from .program import EventKeeper
 
 # conv.hip register-pipelined tiles 0-13 (pipeline depth 2, and 4 at CONV_DEEP_CFG0 + tile), then
 # conv_lds.hip LDS-staged tiles x K chunk x K split, its LDS-DMA tiles x K split, the 3x3 / stride-1
@@ -71,7 +72,7 @@ def _time(fn, inner: int = 10, reps: int = 5) -> float:
     fn()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with EventKeeper() as keep, torch.cuda.graph(g):
         for _ in range(inner):
             fn()
     g.replay()
@@ -82,6 +83,8 @@ def _time(fn, inner: int = 10, reps: int = 5) -> float:
         g.replay()
     e.record()
     torch.cuda.synchronize()
+    g.reset()
+    del g, keep
     return s.elapsed_time(e) / (inner * reps)
 
 
@@ -309,7 +312,7 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
 def step_time_us(prog, X: torch.Tensor, labels: torch.Tensor, reps: int = 100, rounds: int = 3) -> float:
     """Best-of-``rounds`` mean time of the training step (gather, forward, backward, Adam + re-pack at
     learning rate 0) captured as one HIP graph; the program's mutable state is restored afterwards."""
-    from .step import StateSnapshot
+    from .step import StateSnapshot, capture_graph
     f = prog.flat
     snap = StateSnapshot([f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step,
                           f.lr, prog.metrics, prog.confusion, prog.logp] + list(getattr(prog, "extra_state", [])))
@@ -321,10 +324,7 @@ def step_time_us(prog, X: torch.Tensor, labels: torch.Tensor, reps: int = 100, r
     for fn_ in fns:
         fn_()
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        for fn_ in fns:
-            fn_()
+    g, keep, _ = capture_graph(fns)
     for _ in range(10):
         g.replay()
     torch.cuda.synchronize()
@@ -338,7 +338,7 @@ def step_time_us(prog, X: torch.Tensor, labels: torch.Tensor, reps: int = 100, r
         torch.cuda.synchronize()
         best = min(best, 1e3 * s.elapsed_time(e) / reps)
     g.reset()
-    del g
+    del g, keep
     snap.restore()
     prog.opt["pack"].run()
     torch.cuda.synchronize()
@@ -402,7 +402,7 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
     largest isolated time first, each of its ``topk`` best isolated configs is tried and kept when the
     replayed step gets faster by more than ``margin``.  The program's mutable state is restored afterwards.
     Updates and returns ``cache``."""
-    from .step import StateSnapshot
+    from .step import StateSnapshot, capture_graph
     f = prog.flat
     snap = StateSnapshot([f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step,
                           f.lr, prog.metrics, prog.confusion, prog.logp] + list(getattr(prog, "extra_state", [])))
@@ -418,10 +418,7 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
         for fn_ in fns:  # eager pass: code objects of a new config loaded before capture
             fn_()
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for fn_ in fns:
-                fn_()
+        g, keep, _ = capture_graph(fns)
         g.replay()
         torch.cuda.synchronize()
         best = float("inf")
@@ -434,7 +431,7 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
             torch.cuda.synchronize()
             best = min(best, s.elapsed_time(e) / reps)
         g.reset()  # release the graph and its executable now (hundreds of captures per tuning run)
-        del g
+        del g, keep
         return best
 
     groups: Dict[str, list] = {}

@@ -338,3 +338,114 @@ def test_optimizer_segments_cover_flat(model):
     assert all(a["off"] + a["n"] == b["off"] for a, b in zip(segs, segs[1:]))
     convw = {p.flat.off(mod.weight) for c in p.convs for mod in c.mods}
     assert {s["off"] for s in segs if s["kind"] == 3} == convw
+
+
+def test_stream_slots_count_comm_and_spill_in_the_queue_budget():
+    """the communication and spill streams share the hardware-queue budget with the compute
+    streams (more streams than queues crashes graph replay, tools/hwq_repro.py)."""
+    from mtl_das_pytorch_amd.engine.program import COMM_STREAM, MAX_STREAMS, SPILL_STREAM, Launch, stream_slots
+
+    def ls(*ids):
+        return [Launch("x", None, stream=s) for s in ids]
+
+    for hwq in (1, 2, 3, 4, 8):
+        for ids in ((0, 1, 2, 3), (0, 1, 2, 3, COMM_STREAM), (0, 1, 2, 3, COMM_STREAM, SPILL_STREAM),
+                    (0, 1, SPILL_STREAM), (0, COMM_STREAM)):
+            m = stream_slots(ls(*ids), hw_queues=hwq)
+            assert len(set(m.values())) <= max(1, hwq), (hwq, ids, m)
+            assert m[0] == 0 and all(0 <= v <= MAX_STREAMS + 1 for v in m.values())
+            if COMM_STREAM in ids and hwq >= 2:
+                assert m[COMM_STREAM] == MAX_STREAMS  # the collective keeps a stream of its own when it can
+    # the round-4 Model C DP case: 4 compute branches + the comm stream on 4 queues -> 3 compute streams
+    m = stream_slots(ls(0, 1, 2, 3, COMM_STREAM), hw_queues=4)
+    assert sorted(set(m.values())) == [0, 1, 2, MAX_STREAMS]
+
+
+def _issue_check(ph, order):
+    pos = {id(l): i for i, l in enumerate(order)}
+    assert sorted(pos.values()) == list(range(len(ph.launches)))
+    for s in {l.stream for l in ph.launches}:  # every stream keeps its own order
+        mine = [pos[id(l)] for l in ph.launches if l.stream == s]
+        assert mine == sorted(mine)
+    rec = {l.record: pos[id(l)] for l in ph.launches if l.record is not None}
+    for l in ph.launches:  # every wait is issued after its record
+        for t in l.waits:
+            assert rec[ph.alias.get(t, t)] < pos[id(l)]
+
+
+@pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
+def test_main_first_issue_order_is_a_valid_schedule(model):
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.engine.program import Phase
+    from mtl_das_pytorch_amd.models import build_model
+    m = build_model(model)
+    p = InceptionProgram(m, 4, "cpu") if model == "multi_classifier" else MTLProgram(m, 4, "cpu")
+    try:
+        Phase.ISSUE_ORDER = "main_first"
+        for ph in (p.fwd_train, p.bwd, p.fwd_eval):
+            order = ph.issue_order()
+            _issue_check(ph, order)
+            # stream 0 is never behind: a side launch is issued only while stream 0's next launch waits
+            recorded = set()
+            q0 = [l for l in ph.launches if l.stream == 0]
+            k = 0
+            for l in order:
+                if l.stream == 0:
+                    k += 1
+                elif k < len(q0):
+                    assert not all(ph.alias.get(t, t) in recorded for t in q0[k].waits)
+                if l.record is not None:
+                    recorded.add(l.record)
+    finally:
+        Phase.ISSUE_ORDER = "program"
+
+
+def test_executor_schedule_rule_on_a_recorded_dot():
+    """graphsched.schedule reproduces the HIP graph executor's StreamId of every node of a recorded
+    DEBUG_HIP_GRAPH_DOT_PRINT dump (tools/hwq_repro.py --streams 3 --layers 2 on MI355X: 16 nodes; the
+    Model A / C step dumps of round 5 match as well, profiles/r5_graph_streams.md)."""
+    from mtl_das_pytorch_amd.engine import graphsched as gs
+    edges = [(0, 1), (1, 8), (1, 10), (1, 12), (2, 3), (3, 6), (4, 5), (5, 6), (5, 8), (5, 10), (5, 12), (6, 7),
+             (7, 8), (7, 10), (7, 12), (8, 9), (10, 11), (11, 14), (12, 13), (13, 14), (14, 15)]
+    truth = [0, 0, 1, 1, 2, 2, 1, 1, 0, 0, 1, 1, 2, 2, 1, 1]
+    ch = [[] for _ in range(16)]
+    for a, b in edges:
+        ch[a].append(b)
+    assert gs.schedule(ch) == truth
+
+
+@pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
+def test_restream_plan_puts_every_engine_stream_on_its_own_executor_stream(model):
+    """The child-order plan (graphsched.plan_children) makes the emulated executor assignment equal the
+    engine's streams on the captured step's DAG, only by reordering / adding redundant edges."""
+    from mtl_das_pytorch_amd.engine import graphsched as gs
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.models import build_model
+    m = build_model(model)
+    p = InceptionProgram(m, 4, "cpu") if model == "multi_classifier" else MTLProgram(m, 4, "cpu")
+    recs = gs.launch_records([p.fwd_train, p.bwd, p.opt["adam"]])
+    nodes, ch = gs.capture_dag(recs)
+    ranks = {}
+    for r in recs:
+        ranks.setdefault(r["phase"], set()).add(r["stream"])
+    tgt = [sorted(ranks[r["phase"]]).index(r["stream"]) for r in nodes]
+    n, bad = gs.restream_check(ch, tgt)
+    assert bad > 0  # the capture order alone leaves streams mixed (what the timelines showed)
+    new, _ = gs.plan_children(ch, tgt)
+    assert gs.restream_check(new, tgt) == (n, 0)
+    assert all(set(a) <= set(b) for a, b in zip(ch, new))  # every dependency kept
+    # the added edges are redundant: each new child was already a descendant
+    desc = [None] * len(ch)
+
+    def reach(v):
+        if desc[v] is None:
+            s = set()
+            for c in ch[v]:
+                s.add(c)
+                s |= reach(c)
+            desc[v] = s
+        return desc[v]
+    import sys
+    sys.setrecursionlimit(10000)
+    for v, (a, b) in enumerate(zip(ch, new)):
+        assert set(b) - set(a) <= reach(v)

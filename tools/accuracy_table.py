@@ -81,6 +81,7 @@ def run_one(name, model, backend, args, seed, test_sets, lab2, joint, ev, out_di
                            "top_pred_class": int(cm.sum(0).argmax()),
                            "top_pred_share": round(float(cm.sum(0).max() / cm.sum()), 3)})
             row["test"][k]["distance_by_event"] = by
+    tr.close()  # graphs, captured events and streams of this program released before the next one is built
     print(json.dumps(row), flush=True)
     return row
 

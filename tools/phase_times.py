@@ -11,7 +11,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mtl_das_pytorch_amd.data.synthetic import generate  # noqa: E402
-from mtl_das_pytorch_amd.engine.step import StateSnapshot  # noqa: E402
+from mtl_das_pytorch_amd.engine.step import StateSnapshot, capture_graph  # noqa: E402
 from mtl_das_pytorch_amd.engine.tune import autotune_program  # noqa: E402
 from mtl_das_pytorch_amd.models import build_model, encode_joint  # noqa: E402
 
@@ -57,10 +57,7 @@ def main():
                 fn()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for fn in fns:
-                fn()
+        g, keep, _ = capture_graph(fns)
         for _ in range(20):
             g.replay()
         torch.cuda.synchronize()
@@ -76,7 +73,8 @@ def main():
         if name != "eval fwd":
             prev = us
         snap.restore()
-        del g
+        g.reset()
+        del g, keep
     p.opt["pack"].run()
 
 

@@ -20,7 +20,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mtl_das_pytorch_amd.data.synthetic import generate  # noqa: E402
 from mtl_das_pytorch_amd.engine.program import Launch  # noqa: E402
-from mtl_das_pytorch_amd.engine.step import StateSnapshot  # noqa: E402
+from mtl_das_pytorch_amd.engine.step import StateSnapshot, StepRunner, capture_graph  # noqa: E402
 from mtl_das_pytorch_amd.engine.tune import autotune_program  # noqa: E402
 from mtl_das_pytorch_amd.models import build_model, encode_joint  # noqa: E402
 from mtl_das_pytorch_amd.ops.hip import lib  # noqa: E402
@@ -83,12 +83,16 @@ def main():
     for fn in fns:
         fn()
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        for fn in fns:
-            fn()
-    for _ in range(10):
-        g.replay()
+    g, keep, info = capture_graph(fns)  # noqa: F841 (the events live as long as the graph)
+    if info:
+        print("restream:", info)
+    rs = torch.cuda.current_stream()
+    if StepRunner.REPLAY_PRIORITY is not None:  # replay as StepRunner does (tools/variant.py)
+        rs = torch.cuda.ExternalStream(lib().stream_create(int(StepRunner.REPLAY_PRIORITY)))
+        rs.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(rs):
+        for _ in range(10):
+            g.replay()
     torch.cuda.synchronize()
     snap.restore()
     # clock calibration
@@ -106,6 +110,16 @@ def main():
     base = min(t[:n])
     us = [(t[i] - base) / mhz for i in range(n)]
     print(f"{model_type}: {n} launches, clock {mhz:.1f} MHz, last tick at {max(us):.1f} us")
+    # the HSA queue each tick was dispatched from: how the graph executor mapped the captured (logical)
+    # streams onto its own streams / hardware queues
+    qids = {}
+    q = [qids.setdefault(t[4096 + i], len(qids)) if i < 4096 else -1 for i in range(n)]
+    per = {}
+    for i in range(n):
+        per.setdefault(labels[i][2], {}).setdefault(q[i], 0)
+        per[labels[i][2]][q[i]] += 1
+    print("queues per logical stream (queue: launches): " +
+          "; ".join(f"s{s_}: " + ", ".join(f"q{k}:{v}" for k, v in sorted(d.items())) for s_, d in sorted(per.items())))
     last = {}
     order = sorted(range(n), key=lambda i: us[i])
     for i in order:
@@ -113,7 +127,7 @@ def main():
         key = s
         prev = last.get(key, 0.0)
         last[key] = us[i]
-        print(f"{us[i]:8.1f} s{s} +{us[i] - prev:6.1f}  {tag:5s} {name:16s} {shp}")
+        print(f"{us[i]:8.1f} s{s} q{q[i]} +{us[i] - prev:6.1f}  {tag:5s} {name:16s} {shp}")
 
 
 if __name__ == "__main__":
