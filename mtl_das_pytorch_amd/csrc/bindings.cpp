@@ -174,6 +174,7 @@ ConvArgs parse_conv(int mode, py::dict d) {
   }
   a.ws = P<float>(d, "ws");
   a.cnt = P<unsigned>(d, "cnt");
+  a.ptm = P<uint64_t>(d, "ptm");
   return a;
 }
 
@@ -200,9 +201,9 @@ py::tuple wgrad_table(int cfg, py::list dicts, py::list groups) {
   return py::make_tuple(py::bytes(reinterpret_cast<const char*>(jobs.data()), jobs.size() * sizeof(WgradJob)), b0);
 }
 
-void wgrad_batched(int cfg, int64_t table, int nj, int64_t nblocks, int64_t stream) {
+void wgrad_batched(int cfg, int64_t table, int nj, int64_t nblocks, int64_t stream, int64_t cap) {
   check(launch_wgrad_batched(cfg, reinterpret_cast<const WgradJob*>(static_cast<intptr_t>(table)), nj, nblocks,
-                             S(stream)), "wgrad_batched");
+                             S(stream), cap), "wgrad_batched");
 }
 
 WgradArgs parse_wgrad(const py::dict& d) {
@@ -253,6 +254,7 @@ TailArgs parse_tail(const py::dict& d) {
   a.pgs = I(d, "pgs");
   a.gscale = (float)F(d, "gscale", 1.0);
   a.tsc = P<uint64_t>(d, "tsc");
+  a.ptm = P<uint64_t>(d, "ptm");
   if (a.C % 8 || a.C > 2048) throw std::runtime_error("tail: C must be a multiple of 8 and <= 2048");
   return a;
 }
@@ -427,7 +429,8 @@ PYBIND11_MODULE(_mda_hip, m) {
         py::arg("taps") = 0, py::arg("off") = 0, py::arg("zero") = py::list());
   m.def("pool3", &pool3);
   m.def("wgrad_table", &wgrad_table);
-  m.def("wgrad_batched", &wgrad_batched);
+  m.def("wgrad_batched", &wgrad_batched, py::arg("cfg"), py::arg("table"), py::arg("nj"), py::arg("nblocks"),
+        py::arg("stream"), py::arg("cap") = 0);
   m.def("grad_sum", &grad_sum);
   m.def("synth_das", &synth_das);
   m.def("philox_kat", [](int64_t ctr, uint64_t key, int64_t out, int n, int64_t stream) {

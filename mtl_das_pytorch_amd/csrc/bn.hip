@@ -66,9 +66,11 @@ DEV void tail_fwd_impl(const TailArgs& a, const int bx, const int nbx, const int
   float* s_sc2 = sm + 2 * a.C;
   float* s_sh2 = sm + 3 * a.C;
   const bool upd = bx == 0;
+  ptick(a.ptm, 0);
   bn_prepare(a.bn, z, s_sc, s_sh, nullptr, nullptr, upd);
   if (KIND == ADD_RELU2) bn_prepare(a.bn2, z, s_sc2, s_sh2, nullptr, nullptr, upd);
   __syncthreads();
+  ptick(a.ptm, 1);
   Lanes L(a.C);
   if (!L.active) return;
   const int c = L.cg * 8;
@@ -158,6 +160,7 @@ DEV void tail_fwd_impl(const TailArgs& a, const int bx, const int nbx, const int
       store8(oz + (int64_t)(h ? p2 : p) * a.ldo + c, v);
     }
   }
+  ptick(a.ptm, 3);
 }
 
 // Default register allocation: ~100 VGPRs (4 waves per SIMD) for most kinds, which keeps bn_prepare's fp64
@@ -382,6 +385,7 @@ DEV void bnb_apply_impl(const TailArgs& a, const int chunk, const int cy, const 
   const int cgl = threadIdx.x % CGB, pl = threadIdx.x / CGB;
   const int cblk = cy * CB, c = cblk + cgl * 8;
   constexpr bool two = KIND == ADD_RELU2;
+  ptick(a.ptm, 0);
   BwdCtx X;
   bnb_ctx<KIND, CGB>(a, z, cblk, cgl, X, s_x);
   // the NREP replicas of this block's channels: item = (stat, channel), Q threads per item
@@ -425,6 +429,7 @@ DEV void bnb_apply_impl(const TailArgs& a, const int chunk, const int cy, const 
     }
   }
   __syncthreads();
+  ptick(a.ptm, 1);
   const float *A1 = &s_coef[0][0][cgl * 8], *B1 = &s_coef[0][1][cgl * 8], *C1 = &s_coef[0][2][cgl * 8];
   const float *A2 = &s_coef[1][0][cgl * 8], *B2 = &s_coef[1][1][cgl * 8], *C2 = &s_coef[1][2][cgl * 8];
   const int M = a.B * a.H * a.W;
@@ -453,6 +458,7 @@ DEV void bnb_apply_impl(const TailArgs& a, const int chunk, const int cy, const 
       store8(a.dy2 + a.d2gs * z + (int64_t)p * a.ldd2 + c, o);
     }
   }
+  ptick(a.ptm, 3);
 }
 
 // Kernels: plain, and with the register budget of 5 waves per SIMD (<= 96 VGPRs) for the kinds that fit it

@@ -49,6 +49,17 @@ DEV Blk block_coords(int remap) {
   return k;
 }
 
+// Per-block phase timers (profiling only, tools/kernel_phases.py; the pointer is null in production): thread
+// 0 of hardware block b stores the 100 MHz wall clock of phase i (0 entry, 1 prologue done, 2 main loop done,
+// 3 exit) at t[4 * b + i], for the first PT_MAX_BLOCKS blocks of the grid.
+constexpr unsigned PT_MAX_BLOCKS = 16384;
+DEV void ptick(uint64_t* t, int i) {
+  if (t != nullptr && threadIdx.x == 0) {
+    const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (b < PT_MAX_BLOCKS) t[4 * b + i] = wall_clock64();
+  }
+}
+
 DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 // round-to-nearest-even; NaN-preserving via the hardware conversion
 DEV bf16_t f2bf(float f) {

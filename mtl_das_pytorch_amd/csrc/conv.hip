@@ -140,6 +140,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   float* s_bn = s_red + (RED > ST2 ? RED : ST2);  // [8][BN_T] fused BN-backward: scale, shift, mean, invstd
                                                   // of the tail's BN, then of its residual's BN2
   float* s_nol = s_bn;                             // [2][Cs] normalise-on-load scale, shift (forward only)
+  ptick(a.ptm, 0);
   const Blk blk = block_coords(a.xcd);
   const int z = blk.z;
   const int Ktot = a.KH * a.KW * a.Cs;
@@ -168,6 +169,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
   if (NOL) bn_prepare(a.nbn, z, s_nol, s_nol + a.Cs, nullptr, nullptr, blk.x == 0 && blk.y == 0);
   const bool nol_relu = a.nol_kind == ACT_RELU;
   __syncthreads();
+  ptick(a.ptm, 1);
 
   // wave index through readfirstlane: the compiler then knows every K-loop bound and guard below is
   // wave-uniform and branches on it.  An MFMA ignores EXEC, so a guard lowered to an exec mask would still
@@ -293,6 +295,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     __syncthreads();  // partial tiles consumed: s_red may be reused for the statistics below
   }
 
+  ptick(a.ptm, 2);
   // ---------------------------------------------------------------- epilogue
   // BN partial sums are reduced across the block's pixel-waves in LDS and published with ONE atomic per
   // (channel, statistic) per block into replica blk.x % NREP.
@@ -403,6 +406,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
       }
     }
   }
+  ptick(a.ptm, 3);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -611,15 +615,25 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 // the step ends, so all of them are deferred to the end of the backward pass; the ~40 (Model A) / ~90
 // (Model C) small launches become <= 8 large ones that fill the 256 CUs (the deep, small-M layers run
 // side by side instead of one after another).  Block -> job by binary search over the jobs' first blocks.
+// The batched launches walk nvb virtual blocks with a grid of at most nvb hardware blocks: a side stream's
+// batch may run on a capped, persistent grid (launch_wgrad_batched ``cap``), so that it never fills every CU
+// slot while the critical data-gradient chain needs blocks (tools/kernel_phases.py: chain kernels waited up
+// to 16 us for their blocks to start beside an uncapped batch).
+#define WGRAD_FOR_VBLOCKS(BODY)                                                                            \
+  for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {                                              \
+    int lo = 0, hi = nj - 1;                                                                               \
+    while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= vb) lo = mid; else hi = mid - 1; } \
+    const WgradJob& J = jobs[lo];                                                                          \
+    const int local = (int)(vb - J.block0);                                                                \
+    const int per_z = J.ntiles * J.a.splits;                                                               \
+    const int z = local / per_z, r = local - z * per_z;                                                    \
+    BODY;                                                                                                  \
+    __syncthreads(); /* the next virtual block re-stages the LDS tiles */                                  \
+  }
+
 template <int TN, int TK, int MCH>
-__global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob* __restrict__ jobs, int nj) {
-  int lo = 0, hi = nj - 1;
-  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
-  const WgradJob& J = jobs[lo];
-  const int local = (int)((int64_t)blockIdx.x - J.block0);
-  const int per_z = J.ntiles * J.a.splits;
-  const int z = local / per_z, r = local - z * per_z;
-  wgrad_block<TN, TK, MCH>(J.a, r % J.ntiles, r / J.ntiles, z);
+__global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob* __restrict__ jobs, int nj, int64_t nvb) {
+  WGRAD_FOR_VBLOCKS((wgrad_block<TN, TK, MCH>(J.a, r % J.ntiles, r / J.ntiles, z)))
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -713,14 +727,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_big_kernel(WgradArgs a) {
 }
 
 template <int TN, int TK>
-__global__ __launch_bounds__(256) void conv_wgrad_big_batched_kernel(const WgradJob* __restrict__ jobs, int nj) {
-  int lo = 0, hi = nj - 1;
-  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
-  const WgradJob& J = jobs[lo];
-  const int local = (int)((int64_t)blockIdx.x - J.block0);
-  const int per_z = J.ntiles * J.a.splits;
-  const int z = local / per_z, r = local - z * per_z;
-  wgrad_big_block<TN, TK>(J.a, r % J.ntiles, r / J.ntiles, z);
+__global__ __launch_bounds__(256) void conv_wgrad_big_batched_kernel(const WgradJob* __restrict__ jobs, int nj, int64_t nvb) {
+  WGRAD_FOR_VBLOCKS((wgrad_big_block<TN, TK>(J.a, r % J.ntiles, r / J.ntiles, z)))
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -878,14 +886,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(WgradArgs a) {
 }
 
 template <int TN, int CB, int W8, int R>
-__global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const WgradJob* __restrict__ jobs, int nj) {
-  int lo = 0, hi = nj - 1;
-  while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1; }
-  const WgradJob& J = jobs[lo];
-  const int local = (int)((int64_t)blockIdx.x - J.block0);
-  const int per_z = J.ntiles * J.a.splits;
-  const int z = local / per_z, r = local - z * per_z;
-  wgrad_patch_block<TN, CB, W8, R>(J.a, r % J.ntiles, r / J.ntiles, z);
+__global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const WgradJob* __restrict__ jobs, int nj, int64_t nvb) {
+  WGRAD_FOR_VBLOCKS((wgrad_patch_block<TN, CB, W8, R>(J.a, r % J.ntiles, r / J.ntiles, z)))
 }
 
 // Sums the split-M partial slabs of many convolutions into the flat fp32 gradient buffer (deterministic,
@@ -1149,12 +1151,12 @@ int wgrad_tile_shape(int cfg, int& TN, int& TK) {
   return 0;
 }
 
-int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st) {
+int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st, int64_t cap) {
   if (nblocks <= 0) return 0;
-  dim3 grid((unsigned)nblocks);
+  dim3 grid((unsigned)(cap > 0 && cap < nblocks ? cap : nblocks));
   if (cfg >= WGRAD_BIG_CFG0) {
 #define LAUNCH_WGBIGB(TN, TK)                                                                                 \
-  hipLaunchKernelGGL((conv_wgrad_big_batched_kernel<TN, TK>), grid, dim3(256), 0, st, d_jobs, nj); \
+  hipLaunchKernelGGL((conv_wgrad_big_batched_kernel<TN, TK>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \
   break;
     switch (cfg) {
       WGRAD_BIG_CASES(LAUNCH_WGBIGB)
@@ -1165,7 +1167,7 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
   }
   if (cfg >= WGRAD_PATCH_CFG0) {
 #define LAUNCH_WGPB(TN, CB, W8, R)                                                                              \
-  hipLaunchKernelGGL((conv_wgrad_patch_batched_kernel<TN, CB, W8, R>), grid, dim3(256), 0, st, d_jobs, nj); \
+  hipLaunchKernelGGL((conv_wgrad_patch_batched_kernel<TN, CB, W8, R>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \
   break;
     switch (cfg) {
       WGRAD_PATCH_CASES(LAUNCH_WGPB)
@@ -1175,7 +1177,7 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
     return (int)hipGetLastError();
   }
 #define LAUNCH_WGB(TN, TK, MCH)                                                                              \
-  hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, d_jobs, nj); \
+  hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \
   break;
   switch (cfg) {
     WGRAD_CFG_CASES(LAUNCH_WGB)

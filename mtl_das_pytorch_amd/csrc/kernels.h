@@ -63,6 +63,7 @@ struct ConvArgs {
   float* ws;
   unsigned* cnt;
   int xcd;  // block_coords remap (common.h): XCD-contiguous tile order (set from the CONV_XCD cfg flag)
+  uint64_t* ptm;  // optional per-block phase timers (common.h ptick; profiling only)
 };
 
 // ConvArgs::add: the extra gradient sources of output element (row m, channels n0 .. n0+3), added in order
@@ -164,6 +165,7 @@ struct TailArgs {
   bf16_t* dy2; int64_t d2gs; int ldd2;
   float* dgamma; float* dbeta; float* dgamma2; float* dbeta2; int64_t pgs;
   uint64_t* tsc;                    // optional phase timestamps (profiling; null in production)
+  uint64_t* ptm;                    // optional per-block phase timers (common.h ptick; profiling only)
   // apply-only backward (fused = 2) of a multi-source tail: no reduce pass ran, so the apply pass stores
   // the side output itself (apply_side)
   int apply_side;
@@ -272,7 +274,8 @@ constexpr int WGRAD_PATCH_CFG0 = 12, WGRAD_PATCH_NCFG = 8;  // wgrad cfgs 12-19:
 constexpr int WGRAD_BIG_CFG0 = 32, WGRAD_BIG_NCFG = 4;  // wgrad cfgs 32-35: 32x32x16 large-tile kernels
 int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8, int& R);
 int wgrad_ntiles(int cfg, const WgradArgs& a);  // tiles per group of a wgrad launch, < 0: cfg invalid for a
-int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st);
+// cap > 0: at most cap hardware blocks walk the nblocks virtual blocks (persistent grid)
+int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st, int64_t cap = 0);
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);
 int launch_tail_fwd_batched(int kind, const TailJob* d_jobs, int nj, int nblocks, int maxC, hipStream_t st);

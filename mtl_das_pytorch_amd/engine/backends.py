@@ -215,7 +215,8 @@ class EngineBackend(Backend):
             self.prog.enable_sync_bn(ctx.all_reduce_ordered_)
             if not ctx.capturable_collectives:
                 use_graph = False
-        self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world)
+        self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world,
+                                data_parallel=ctx.enabled)
         if hasattr(self.prog, "set_rng_stream"):
             self.prog.set_rng_stream(seed, ctx.rank)
         self.prog.segment_backward(self.prog.dp_buckets(ctx.world))

@@ -505,6 +505,9 @@ class LoweredProgram:
         return ph
 
     WGRAD_MAX_BATCHES = 3
+    # hardware blocks of a side stream's batched weight-gradient launch (0: one per virtual block): a capped,
+    # persistent grid leaves CU slots free for the critical chain's kernels (csrc/conv.hip WGRAD_FOR_VBLOCKS)
+    SIDE_WGRAD_GRID = 0
 
     def merge_wgrad_cfgs(self, max_batches: Optional[int] = None) -> int:
         """Cap the number of distinct weight-gradient tile configs per stream (= batched launches, which run
@@ -651,10 +654,10 @@ class LoweredProgram:
             if side and rest:
                 ls[fin].owner = rest
                 ls[fin].args = self._wgfin_args(rest)
-            if side and self.EARLY_ADAM and self._opt_hparams.get("grad_scale", 1.0) == 1.0:
+            if side and self.EARLY_ADAM and not self.data_parallel and self._opt_hparams.get("grad_scale", 1.0) == 1.0:
                 # single process: the side convs' Adam + re-pack right after their finalize, on their stream
-                # (the optimizer phase then covers the rest); with gradient averaging (DP) the update must wait
-                # for the all-reduce, so it stays in the optimizer phase
+                # (the optimizer phase then covers the rest); with gradient averaging (DP, set_optimizer's
+                # data_parallel) the update must wait for the all-reduce, so it stays in the optimizer phase
                 early = set()
                 for pos_batched in inserts:
                     batched = pos_batched[1]
@@ -690,7 +693,8 @@ class LoweredProgram:
         raw, nblocks = lib().wgrad_table(cfg, [l.args[2] for l in group], [l.args[1] for l in group])
         table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         self.wgrad_tables.append(table)
-        return Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, stream=st, bucket=bucket)
+        cap = self.SIDE_WGRAD_GRID if st != 0 else 0
+        return Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, cap, stream=st, bucket=bucket)
 
     def _batch_wgrads_segmented(self):
         """batch_wgrads for a backward cut into gradient-bucket pieces (segment_backward): in every piece,
@@ -761,16 +765,23 @@ class LoweredProgram:
         self._opt_base = base
         self._opt_hparams = dict(b1=0.9, b2=0.999, eps=1e-8, wd=0.0, grad_scale=grad_scale)
         self._opt_kwargs = dict(betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, grad_scale=grad_scale)
+        self.data_parallel = False
         upd = Phase("adam")
         upd.add("adam_pack", k_adam, dict(base, update=1, **self._opt_hparams))
         pack = Phase("pack")
         pack.add("pack", k_adam, dict(base, update=0))
         return {"adam": upd, "pack": pack}
 
-    def set_optimizer(self, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, grad_scale: float = 1.0):
-        self._opt_kwargs = dict(betas=betas, eps=eps, weight_decay=weight_decay, grad_scale=grad_scale)
+    def set_optimizer(self, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, grad_scale: float = 1.0,
+                      data_parallel: bool = False):
+        """Adam hyper-parameters.  ``data_parallel``: the gradients are all-reduced across processes before the
+        update (any DP group, also a 1-rank one), so no weight may be updated inside the backward (early Adam
+        is then never emitted; ``grad_scale`` = 1/world folds the averaging into the update)."""
+        self._opt_kwargs = dict(betas=betas, eps=eps, weight_decay=weight_decay, grad_scale=grad_scale,
+                                data_parallel=data_parallel)
         self._opt_hparams = dict(b1=betas[0], b2=betas[1], eps=eps, wd=weight_decay, grad_scale=grad_scale)
-        if getattr(self, "_early_adam", None) and grad_scale != 1.0:
+        self.data_parallel = bool(data_parallel)
+        if getattr(self, "_early_adam", None) and (grad_scale != 1.0 or data_parallel):
             raise RuntimeError("the weight updates already run inside the backward: gradient averaging would miss them")
         for d in getattr(self, "_early_adam", []):  # the side streams' partial updates (batch_wgrads)
             d.update(self._opt_hparams)

@@ -39,6 +39,10 @@ class MTLProgram(LoweredProgram):
     # DP: the task-branch gradients (38% of the 4.5 MB buffer) are all-reduced while RB1, the stem and
     # the backbone's weight gradients still run; the backbone bucket follows (bucket_cut_candidates)
     default_buckets = 2
+    # the level branches' weight-gradient batches on a persistent grid of 512 blocks: the backbone's data-
+    # gradient chain finds CU slots for its blocks (in-step ramp of a 33x83 dgrad 10-16 us beside an uncapped
+    # batch, tools/kernel_phases.py); A 34.71-34.91 k -> 35.08-35.34 k (5 pairs, docs/PERF.md round 5)
+    SIDE_WGRAD_GRID = 512
 
     def __init__(self, model: MTLNet, batch: int, device, in_hw=(100, 250), loss_weights: Optional[Sequence[float]] = None,
                  sync_world: int = 1):

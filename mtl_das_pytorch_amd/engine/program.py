@@ -341,8 +341,8 @@ def k_pool(is_max, bwd, d, st):
     lib().pool3(is_max, bwd, st, d)
 
 
-def k_wgrad_batched(cfg, table, nj, nblocks, st):
-    lib().wgrad_batched(cfg, table.data_ptr(), nj, nblocks, st)
+def k_wgrad_batched(cfg, table, nj, nblocks, cap, st):
+    lib().wgrad_batched(cfg, table.data_ptr(), nj, nblocks, st, cap)
 
 
 def k_wgfin(table, nd, nblocks, st):

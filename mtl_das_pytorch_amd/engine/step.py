@@ -68,7 +68,7 @@ class StepRunner:
     # rewrite each captured graph's edge order so that the HIP graph executor runs every engine stream on a
     # stream of its own (engine/graphsched.py: the executor otherwise re-derives streams from the DAG and
     # mixes the critical chain with side work)
-    RESTREAM = True
+    RESTREAM = False
 
     def __init__(self, program, X: torch.Tensor, labels: torch.Tensor, use_graph: bool = True,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None, X_eval: torch.Tensor = None,
@@ -90,6 +90,11 @@ class StepRunner:
         self._bwd_dp = None
         # the DP step as one graph with the bucket collectives captured in it (FlatGradAllReducer.capturable)
         self.capture_dp = self.use_graph and allreduce is not None and getattr(allreduce, "capturable", False)
+        reducing = allreduce is not None and getattr(getattr(allreduce, "ctx", None), "enabled", False)
+        if reducing and any(l.name == "adam_pack_early" for l in program.bwd.launches):
+            # an update inside the backward would use local, un-reduced gradients
+            raise ValueError("data-parallel step with weight updates inside the backward: call "
+                             "set_optimizer(data_parallel=True) before autotune_program")
         self.buckets = list(getattr(program, "buckets", None) or [(0, program.flat.numel)])
 
     # -------------------------------------------------------------------------------------------

@@ -58,7 +58,7 @@ def main():
     world, dev = ctx.world, ctx.device
     B = 32
     prog, joint = build(model_type, B, dev, nbuckets)
-    prog.set_optimizer(betas=(B1, B2), eps=EPS, weight_decay=WD, grad_scale=1.0 / world)
+    prog.set_optimizer(betas=(B1, B2), eps=EPS, weight_decay=WD, grad_scale=1.0 / world, data_parallel=True)
     buckets = prog.segment_backward(nbuckets)
     autotune_program(prog, measure=False)
     f = prog.flat

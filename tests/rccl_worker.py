@@ -5,11 +5,14 @@ communicator on cuda:0 (``torch.distributed`` backend "nccl" is RCCL on ROCm), s
 an actual RCCL launch on the GPU -- only its peer count is 1.  Checks, for the model given on the command
 line (bench.py's flagship step at per-GPU batch 32, tuned kernel configs):
 
-  dp         the bench/trainer DP step -- backward cut into gradient-bucket pieces, each bucket's async
-             all-reduce (``FlatGradAllReducer.start``) issued on RCCL's stream while the next piece's graph
-             runs, ``finish`` making the compute stream wait, then the optimizer graph -- against the same
-             lowered program replayed as ONE graph without collectives: bitwise equal after 3 steps
-             (a 1-rank sum is exact), for 1 and 2 (A) / 4 (C) buckets;
+  dp         the DP step in both forms, against the same lowered program replayed as ONE graph without
+             collectives -- bitwise equal after 3 steps (a 1-rank sum is exact), for 1 and 2 (A) / 4 (C) buckets:
+             * captured (the 1-rank default, DistContext.capture_group): the buckets' all-reduces inside the
+               step graph on the communication stream;
+             * pieces (the world > 1 default; ``FlatGradAllReducer.capturable = False`` here): the backward
+               cut into gradient-bucket piece graphs, each bucket's async all-reduce
+               (``FlatGradAllReducer.start``) issued on RCCL's stream while the next piece's graph runs,
+               ``finish`` making the compute stream wait (Work.wait), then the optimizer graph;
   syncbn     ``enable_sync_bn``: every BN's replica sums all-reduced by RCCL inside the step, CAPTURED in the
              step's HIP graph (no eager fallback on RCCL): graph == eager bitwise; after one step the BN running
              statistics equal plain BN's bitwise and the gradients agree to summation order;
@@ -38,18 +41,25 @@ from mtl_das_pytorch_amd.parallel.dist import FlatGradAllReducer, average_, init
 B = 32
 
 
-def run(ctx, model_type, X, labels, *, buckets=1, dp=False, sync_bn=False, graph=True, steps=3, time_steps=0):
+def run(ctx, model_type, X, labels, *, buckets=1, dp=False, sync_bn=False, graph=True, steps=3, time_steps=0,
+        capture_dp=True):
     torch.manual_seed(1234)
     m = build_model(model_type)
     joint = model_type == "multi_classifier"
     prog = (InceptionProgram(m, B, ctx.device) if joint else MTLProgram(m, B, ctx.device))
     n_ar = prog.enable_sync_bn(ctx.all_reduce_ordered_) if sync_bn else 0
-    prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / ctx.world)
+    prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / ctx.world,
+                       data_parallel=dp)
     if joint:
         prog.set_rng_stream(0, ctx.rank)
     nb = len(prog.segment_backward(buckets))
     autotune_program(prog, measure=False)
-    runner = StepRunner(prog, X, labels, use_graph=graph, allreduce=FlatGradAllReducer(ctx) if dp else None)
+    ar = FlatGradAllReducer(ctx) if dp else None
+    if ar is not None and not capture_dp:
+        # the multi-rank default (collectives not capturable): per-bucket piece graphs, each bucket's RCCL
+        # all-reduce issued asynchronously between them (FlatGradAllReducer.start / finish)
+        ar.capturable = False
+    runner = StepRunner(prog, X, labels, use_graph=graph, allreduce=ar)
     runner.set_lr(1e-3)
     for i in range(steps):
         runner.train_step(torch.arange(B * i, B * (i + 1), device=ctx.device) % X.shape[0])
@@ -65,7 +75,10 @@ def run(ctx, model_type, X, labels, *, buckets=1, dp=False, sync_bn=False, graph
     state = {k: t.detach().clone() for k, t in (("params", f.params), ("grads", f.grads), ("exp_avg", f.exp_avg),
                                                 ("exp_avg_sq", f.exp_avg_sq), ("bn_mean", f.bn_mean),
                                                 ("bn_var", f.bn_var), ("step", f.step))}
-    return state, {"buckets": nb, "collectives_per_step": n_ar, "ms_per_step": ms, "graphs": sorted(runner.graphs)}
+    info = {"buckets": nb, "collectives_per_step": n_ar, "ms_per_step": ms, "graphs": sorted(runner.graphs),
+            "captured_dp": runner.capture_dp}
+    runner.close()
+    return state, info
 
 
 def rel(a, b):
@@ -84,6 +97,9 @@ def main():
         ref, _ = run(ctx, model_type, X, labels, buckets=buckets, dp=False)
         got, info = run(ctx, model_type, X, labels, buckets=buckets, dp=True)
         out[f"dp{buckets}"] = dict(info, bitwise={k: bool(torch.equal(ref[k], got[k])) for k in ref})
+        # the world > 1 default path on RCCL: piece graphs + async bucket all-reduces + Work.wait
+        got, info = run(ctx, model_type, X, labels, buckets=buckets, dp=True, capture_dp=False)
+        out[f"dp{buckets}_pieces"] = dict(info, bitwise={k: bool(torch.equal(ref[k], got[k])) for k in ref})
     # SyncBN: collectives inside the step's graph
     eager, _ = run(ctx, model_type, X, labels, sync_bn=True, graph=False, steps=2)
     graph, info = run(ctx, model_type, X, labels, sync_bn=True, graph=True, steps=2)

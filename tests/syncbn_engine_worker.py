@@ -143,7 +143,7 @@ def main():
     lab = encode_joint(d, e) if joint else torch.stack([d, e], 1)
     mine = torch.arange(ctx.rank * B, (ctx.rank + 1) * B, device=dev)
     prog = build(model_type, B, dev, world if sync else 1)
-    prog.set_optimizer(weight_decay=0.0, grad_scale=1.0 / world)
+    prog.set_optimizer(weight_decay=0.0, grad_scale=1.0 / world, data_parallel=True)
     if sync:
         prog.enable_sync_bn(ctx.all_reduce_ordered_)
     autotune_program(prog, measure=False)

@@ -200,13 +200,17 @@ def _force_big_wgrad(prog):
 
 @pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
 @pytest.mark.parametrize("big", [False, True])
-def test_batched_wgrad_bitwise_equal(model_name, big):
+def test_batched_wgrad_bitwise_equal(model_name, big, monkeypatch):
     """One launch per tile config computes exactly what the per-conv launches compute (also with every
-    conv on the large-tile configs, whose gradients must match the default configs' to fp32 order)."""
+    conv on the large-tile configs, whose gradients must match the default configs' to fp32 order), and so
+    does a side stream's batch on a capped persistent grid (LoweredProgram.SIDE_WGRAD_GRID: 7 hardware
+    blocks walking all virtual blocks)."""
+    from mtl_das_pytorch_amd.engine.lowering import LoweredProgram
     from mtl_das_pytorch_amd.models import build_model, encode_joint
     from mtl_das_pytorch_amd.data.synthetic import generate
     grads = []
-    for batched in (False, True):
+    for batched in (False, True, "capped"):
+        monkeypatch.setattr(LoweredProgram, "SIDE_WGRAD_GRID", 7 if batched == "capped" else 0)
         torch.manual_seed(0)
         m = build_model(model_name)
         if model_name == "multi_classifier":
@@ -223,7 +227,10 @@ def test_batched_wgrad_bitwise_equal(model_name, big):
         lab = encode_joint(d, e) if model_name == "multi_classifier" else torch.stack([d, e], 1)
         _engine_step(prog, X, lab, torch.arange(8, device="cuda"))
         grads.append(prog.flat.grads.clone())
+        if batched == "capped":
+            assert any(l.name == "wgrad_batched" and l.args[4] == 7 for l in prog.bwd.launches)
     assert torch.equal(grads[0], grads[1])
+    assert torch.equal(grads[0], grads[2])
 
 
 @pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])

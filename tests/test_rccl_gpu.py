@@ -1,6 +1,7 @@
-"""The RCCL collective path executed on one MI355X: a 1-rank RCCL process group
-(MDA_DIST_BACKEND=nccl, WORLD_SIZE=1) carries bench.py's DP step -- per-bucket backward graphs with
-asynchronous RCCL all-reduces -- and graph-captured SyncBN.  Multi-rank correctness is covered by the gloo
+"""The RCCL collective path executed on one MI355X: a 1-rank RCCL process
+group (MDA_DIST_BACKEND=nccl, WORLD_SIZE=1) carries bench.py's DP step in both of its forms -- the bucket
+all-reduces captured inside the step graph (the 1-rank default) and the world > 1 default, per-bucket
+backward piece graphs with asynchronous RCCL all-reduces and Work.wait -- and graph-captured SyncBN.  Multi-rank correctness is covered by the gloo
 tests (tests/test_dp_engine_gpu.py, tests/test_dist.py); this one proves the RCCL-specific code: the
 communicator, stream-ordered collectives, Work.wait stream semantics, barrier(device_ids) and collective
 capture inside a HIP graph."""
@@ -34,9 +35,13 @@ def test_rccl_one_rank_dp_and_syncbn(model):
     assert res["enabled"] and res["backend"] == "nccl" and res["world"] == 1
     nbk = 4 if model == "multi_classifier" else 2
     for b in (1, nbk):
-        r = res[f"dp{b}"]
-        assert r["buckets"] == b
-        assert all(r["bitwise"].values()), r  # 1-rank RCCL sums are exact: same bits as no collective
+        for form in ("", "_pieces"):
+            r = res[f"dp{b}{form}"]
+            assert r["buckets"] == b
+            assert r["captured_dp"] == (form == ""), r
+            assert all(r["bitwise"].values()), r  # 1-rank RCCL sums are exact: same bits as no collective
+        if b > 1:  # the piece path really ran as per-bucket graphs
+            assert sum(k.startswith("train_piece") for k in res[f"dp{b}_pieces"]["graphs"]) == b
     s = res["syncbn"]
     assert s["collectives_per_step"] > 40  # one per BN forward + one per BN backward
     assert "train_full" in s["graphs"]  # SyncBN stays on the single-graph step: collectives captured
