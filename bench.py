@@ -90,7 +90,8 @@ def main():
             else MTLProgram(model, args.batch, dev, sync_world=sw))
     if sync:  # the statistics collectives are captured into the step's HIP graph (RCCL)
         prog.enable_sync_bn(ctx.all_reduce_ordered_)
-    prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world)
+    prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world,
+                       data_parallel=ctx.enabled)
     if hasattr(prog, "set_rng_stream"):  # Model C dropout: an independent mask stream per rank
         prog.set_rng_stream(0, ctx.rank)
     # DP: gradient buckets whose all-reduces overlap the rest of the backward (engine/step.py)
