@@ -61,6 +61,10 @@ def main():
     ap.add_argument("--sync_bn", action="store_true",
                     help="SyncBN: BN statistics all-reduced inside the step (one GPU: run with MDA_DIST_BACKEND=nccl "
                          "for a 1-rank RCCL group, so the collectives execute)")
+    ap.add_argument("--dp-shape", type=int, default=0,
+                    help="rehearse the per-rank program of an N-GPU data-parallel run on this rank's group (run with "
+                         "MDA_DIST_BACKEND=nccl for a 1-rank RCCL group): N's gradient buckets, updates only after "
+                         "the all-reduce, and the world > 1 collective path (per-bucket piece graphs, async RCCL)")
     args = ap.parse_args()
 
     import torch
@@ -91,12 +95,13 @@ def main():
     if sync:  # the statistics collectives are captured into the step's HIP graph (RCCL)
         prog.enable_sync_bn(ctx.all_reduce_ordered_)
     prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world,
-                       data_parallel=ctx.enabled)
+                       data_parallel=ctx.enabled or args.dp_shape > 1)
     if hasattr(prog, "set_rng_stream"):  # Model C dropout: an independent mask stream per rank
         prog.set_rng_stream(0, ctx.rank)
     # DP: gradient buckets whose all-reduces overlap the rest of the backward (engine/step.py)
     # (--buckets K on one GPU runs the same split graphs with no-op collectives: measures the split's cost)
-    nb = prog.dp_buckets(world) if args.buckets is None else args.buckets
+    shape = max(world, args.dp_shape)
+    nb = prog.dp_buckets(shape) if args.buckets is None else args.buckets
     buckets = prog.segment_backward(nb)
     autotune_program(prog, out_path=os.path.join("gpurun_out", "tuned_cfgs.json") if ctx.is_main else None,
                      measure=not args.no_tune)
@@ -104,8 +109,11 @@ def main():
     broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
     X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev, in_channels=args.in_channels)
     labels = encode_joint(d, e) if joint else torch.stack([d, e], 1)
+    reducer = FlatGradAllReducer(ctx) if (ctx.enabled or len(buckets) > 1) else None
+    if reducer is not None and args.dp_shape > 1:
+        reducer.capturable = False  # what a multi-rank group runs (DistContext.capturable_collectives)
     runner = StepRunner(prog, X, labels, use_graph=not args.no_graph and (not sync or ctx.capturable_collectives),
-                        allreduce=FlatGradAllReducer(ctx) if (ctx.enabled or len(buckets) > 1) else None)
+                        allreduce=reducer)
     runner.set_lr(1e-3 / 1.5)  # reference: lr/1.5 applied at the epoch-0 validation
     sampler = ShardedIndexSampler(args.dataset_size * world, args.batch, ctx, seed=7)
     # indices address this rank's resident shard
@@ -170,6 +178,8 @@ def main():
         "sync_bn": sync,
         "grad_buckets_mb": [round((hi - lo) * 4 / 2 ** 20, 2) for lo, hi in buckets],
         "dist_backend": ctx.backend,
+        "dp_shape": shape,
+        "captured_collectives": runner.capture_dp,
         "rccl_ranks": dist.get_world_size() if ctx.backend == "nccl" else 0,
         "baseline_note": "vs_baseline divides by BASELINE.md's 176.1 samples/s (reference on CPU, the only "
                          "throughput number it has); vs_eager_pytorch_mi355x divides by the reference-style "

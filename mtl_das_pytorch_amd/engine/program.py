@@ -96,7 +96,8 @@ class EngineStreams:
     created with ``hipStreamCreateWithPriority`` by the extension (not drawn from torch's 32-entry
     round-robin pool, whose streams a phase could share with the graph-capture stream or another phase's
     streams), and released by :func:`release_streams` (atexit).  Index 0..MAX_STREAMS-2 are the compute
-    side streams, then the communication and the spill stream."""
+    side streams, then the communication and the spill stream; ``capture`` is the stream graphs are captured
+    on."""
 
     _by_device = {}
 
@@ -104,8 +105,11 @@ class EngineStreams:
         import torch
         self.device = device
         n = MAX_STREAMS - 1 + 2
-        self.handles = [lib().stream_create(0) for _ in range(n)]
-        self.streams = [torch.cuda.ExternalStream(h, device=device) for h in self.handles]
+        self.handles = [lib().stream_create(0) for _ in range(n + 1)]
+        self.streams = [torch.cuda.ExternalStream(h, device=device) for h in self.handles[:n]]
+        # graph captures and their eager warm-up runs (StepRunner, capture_graph): never a pool stream, so a
+        # communicator's pool stream can never be the stream a graph is captured on
+        self.capture = torch.cuda.ExternalStream(self.handles[n], device=device)
 
     @classmethod
     def get(cls, device):
@@ -117,7 +121,7 @@ class EngineStreams:
     def destroy(self):
         for h in self.handles:
             lib().stream_destroy(h)
-        self.handles, self.streams = [], []
+        self.handles, self.streams, self.capture = [], [], None
 
 
 def release_streams():

@@ -25,7 +25,7 @@ from typing import Callable, Dict, List, Optional
 
 import torch
 
-from .program import EventKeeper, Phase
+from .program import EngineStreams, EventKeeper, Phase
 from ..ops.hip import lib
 
 
@@ -49,7 +49,8 @@ def capture_graph(fns, restream: Optional[bool] = None, error_mode: str = "globa
     restream = StepRunner.RESTREAM if restream is None else restream
     keeper = EventKeeper(track=restream)
     g = torch.cuda.CUDAGraph(keep_graph=True) if restream else torch.cuda.CUDAGraph()
-    with keeper, torch.cuda.graph(g, capture_error_mode=error_mode):
+    cap = EngineStreams.get(torch.cuda.current_stream().device).capture if StepRunner.ENGINE_CAPTURE_STREAM else None
+    with keeper, torch.cuda.graph(g, stream=cap, capture_error_mode=error_mode):
         for f in fns:
             f()
     info = None
@@ -69,6 +70,10 @@ class StepRunner:
     # stream of its own (engine/graphsched.py: the executor otherwise re-derives streams from the DAG and
     # mixes the critical chain with side work)
     RESTREAM = False
+    # graphs are captured (and warmed up) on the engine's own capture stream, not on torch's pool streams:
+    # the world > 1 data-parallel step (per-bucket piece graphs + async RCCL) ran 2.7x slower with pool
+    # capture streams (bench.py --dp-shape 8 on Model A: 11.3 k -> 30.3 k samples/s, docs/PERF.md round 5)
+    ENGINE_CAPTURE_STREAM = True
 
     def __init__(self, program, X: torch.Tensor, labels: torch.Tensor, use_graph: bool = True,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None, X_eval: torch.Tensor = None,
@@ -171,7 +176,8 @@ class StepRunner:
         if g is None:
             fns = self._phases(kind)
             snap = StateSnapshot(self._mutable_state())
-            s = torch.cuda.Stream()
+            s = (EngineStreams.get(torch.cuda.current_stream().device).capture if self.ENGINE_CAPTURE_STREAM
+                 else torch.cuda.Stream())
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):  # warm-up (loads code objects); side effects are rolled back
                 for f in fns:

@@ -161,15 +161,19 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[int] = N
     return _with_capture_group(DistContext(rank, world, local_rank, device, backend))
 
 
+# communicator streams from torch's high-priority pool (see _rccl_options; a class-free switch for A/B runs)
+RCCL_HIGH_PRIORITY = True
+
+
 def _rccl_options():
-    """RCCL communicators run on HIGH-priority pool streams.  PyTorch hands out the normal-priority pool's 32
+    """RCCL communicators run on HIGH-priority pool streams (RCCL_HIGH_PRIORITY).  PyTorch hands out the normal-priority pool's 32
     streams round robin to every ``torch.cuda.Stream()`` -- the engine's phase streams and the graph-capture
     stream among them -- and to the process group's communication stream alike; once the pool wraps, a
     communicator's stream can BE a stream the step graph captures on, and the watchdog's poll of an eager
     collective's event recorded there fails during the capture ("event last recorded in a capturing stream",
     seen on Model C's 4-stream step).  A separate pool keeps them apart; priority also puts the collectives'
     kernels ahead of compute in the queues, as wanted for overlapped gradient buckets."""
-    return dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
+    return dist.ProcessGroupNCCL.Options(is_high_priority_stream=RCCL_HIGH_PRIORITY)
 
 
 def _with_capture_group(ctx: DistContext) -> DistContext:
