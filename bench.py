@@ -101,7 +101,8 @@ def main():
     # DP: gradient buckets whose all-reduces overlap the rest of the backward (engine/step.py)
     # (--buckets K on one GPU runs the same split graphs with no-op collectives: measures the split's cost)
     shape = max(world, args.dp_shape)
-    nb = prog.dp_buckets(shape) if args.buckets is None else args.buckets
+    captured = ctx.capturable_collectives and args.dp_shape <= 1  # the form the step's collectives take
+    nb = prog.dp_buckets(shape, captured) if args.buckets is None else args.buckets
     buckets = prog.segment_backward(nb)
     autotune_program(prog, out_path=os.path.join("gpurun_out", "tuned_cfgs.json") if ctx.is_main else None,
                      measure=not args.no_tune)

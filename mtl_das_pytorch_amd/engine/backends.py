@@ -219,7 +219,7 @@ class EngineBackend(Backend):
                                 data_parallel=ctx.enabled)
         if hasattr(self.prog, "set_rng_stream"):
             self.prog.set_rng_stream(seed, ctx.rank)
-        self.prog.segment_backward(self.prog.dp_buckets(ctx.world))
+        self.prog.segment_backward(self.prog.dp_buckets(ctx.world, ctx.capturable_collectives))
         autotune_program(self.prog, measure=tune)
         f = self.prog.flat
         broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])

@@ -69,9 +69,20 @@ class LoweredProgram:
     label_width = 2
     default_buckets = 1  # gradient buckets under data parallelism (segment_backward); MDA_BUCKETS overrides
 
-    def dp_buckets(self, world: int) -> int:
+    def dp_buckets(self, world: int, captured: bool = True) -> int:
+        """Gradient buckets of a data-parallel step.  Overlapped buckets only pay inside ONE captured graph
+        (backward_with_allreduce: the collectives are graph nodes on the communication stream).  When the
+        collectives run eagerly between graphs (``captured`` False: the multi-rank default) every bucket cuts
+        the backward into piece graphs whose boundaries join all streams -- measured on one MI355X with the
+        per-rank program of an 8-GPU run (bench.py --dp-shape 8, 1-rank RCCL): Model A 30.1 k (2 buckets)
+        vs 34.3 k samples/s (1), Model C 6.2 k (2) / 6.7 k (4) vs 8.3 k (1) -- more than the unoverlapped
+        all-reduce costs, so that path uses one bucket."""
         import os
-        return 1 if world <= 1 else int(os.environ.get("MDA_BUCKETS", str(self.default_buckets)))
+        if world <= 1:
+            return 1
+        if not captured:
+            return int(os.environ.get("MDA_BUCKETS", "1"))
+        return int(os.environ.get("MDA_BUCKETS", str(self.default_buckets)))
 
     # -------------------------------------------------------------------------------------------
     def _tail_args(self, y: Act, bn: BNLayer, out: Act, training: bool, H=None, W=None) -> tuple:
