@@ -516,6 +516,8 @@ class LoweredProgram:
         return ph
 
     WGRAD_MAX_BATCHES = 3
+    # the same cap for stream 0 only (its batches run serially after the data-gradient chain); None: as above
+    WGRAD_MAX_BATCHES_S0 = None
     # hardware blocks of a side stream's batched weight-gradient launch (0: one per virtual block): a capped,
     # persistent grid leaves CU slots free for the critical chain's kernels (csrc/conv.hip WGRAD_FOR_VBLOCKS)
     SIDE_WGRAD_GRID = 0
@@ -534,11 +536,12 @@ class LoweredProgram:
         # one batch set per (gradient bucket, stream): a segmented backward batches each bucket separately
         for bk, st in sorted({(l.bucket, l.stream) for l in wg}):
             mine = [l for l in wg if l.stream == st and l.bucket == bk]
+            cap = self.WGRAD_MAX_BATCHES_S0 if st == 0 and self.WGRAD_MAX_BATCHES_S0 else max_batches
             while True:
                 groups = {}
                 for l in mine:
                     groups.setdefault(l.args[0], []).append(l)
-                if len(groups) <= max_batches:
+                if len(groups) <= cap:
                     break
                 cost = {c: sum(_wgrad_cost(c, l.args[1], l.args[2]) for l in ls) for c, ls in groups.items()}
                 move = None

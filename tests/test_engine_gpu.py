@@ -200,17 +200,15 @@ def _force_big_wgrad(prog):
 
 @pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
 @pytest.mark.parametrize("big", [False, True])
-def test_batched_wgrad_bitwise_equal(model_name, big, monkeypatch):
+def test_batched_wgrad_bitwise_equal(model_name, big):
     """One launch per tile config computes exactly what the per-conv launches compute (also with every
     conv on the large-tile configs, whose gradients must match the default configs' to fp32 order), and so
     does a side stream's batch on a capped persistent grid (LoweredProgram.SIDE_WGRAD_GRID: 7 hardware
     blocks walking all virtual blocks)."""
-    from mtl_das_pytorch_amd.engine.lowering import LoweredProgram
     from mtl_das_pytorch_amd.models import build_model, encode_joint
     from mtl_das_pytorch_amd.data.synthetic import generate
     grads = []
     for batched in (False, True, "capped"):
-        monkeypatch.setattr(LoweredProgram, "SIDE_WGRAD_GRID", 7 if batched == "capped" else 0)
         torch.manual_seed(0)
         m = build_model(model_name)
         if model_name == "multi_classifier":
@@ -221,6 +219,7 @@ def test_batched_wgrad_bitwise_equal(model_name, big, monkeypatch):
             prog = MTLProgram(m, 8, "cuda")
         if big:
             assert _force_big_wgrad(prog) > 0
+        prog.SIDE_WGRAD_GRID = 7 if batched == "capped" else 0  # (Model A ships 512)
         if batched:
             prog.batch_wgrads()
         X, d, e = generate(16, seed=1, device="cuda")

@@ -315,3 +315,57 @@ def test_inception_tail_backward_batches(monkeypatch):
         assert rel(out[1][n], out[0][n]) < 1e-4, n
     flat = [torch.cat([o[n].flatten() for n in o]) for o in out]
     assert F.cosine_similarity(flat[0], flat[1], dim=0).item() > 0.999
+
+
+def test_inception_training_trajectory_matches_fp32_oracle(monkeypatch):
+    """Three full training steps of Model C (forward, backward, Adam at the reference's lr 1e-3 / coupled
+    weight decay 1e-5) on the engine's step runner and on the fp32 reference module (bf16 activation storage
+    emulated, as in test_inception_train_step_matches_autograd), from the same bf16-rounded weights and
+    batches, dropout off.  Bounds are the oracle's own sensitivity (the Model A form is
+    tests/test_engine_gpu.py::test_training_trajectory_matches_fp32_oracle): a copy of the reference with one
+    bf16 ulp of relative weight noise is stepped alongside; per step the engine's joint CE loss must stay
+    within 1.5x that copy's distance from the oracle (+ 2 % + 1e-3), and after the last step the accumulated
+    parameter update within 1.5x (+ 0.05)."""
+    from mtl_das_pytorch_amd.engine.step import StepRunner
+    model, ref, prog, X, labels = _setup(B=8)
+    _emulate_bf16_storage(ref, monkeypatch)
+    ref.dropout.p = 0.0
+    B, steps, lr, wd = prog.B, 3, 1e-3, 1e-5
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_(p.bfloat16().float())
+        prog.flat.params.copy_(prog.flat.params.bfloat16().float())
+    noisy = copy.deepcopy(ref)
+    torch.manual_seed(321)
+    with torch.no_grad():
+        for p in noisy.parameters():
+            p.mul_(1 + 4e-3 * torch.randn_like(p))
+    p0 = {n: p.detach().clone() for n, p in ref.named_parameters()}
+    pn0 = {n: p.detach().clone() for n, p in noisy.named_parameters()}
+    prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=wd)
+    runner = StepRunner(prog, X, labels, use_graph=False)
+    runner.set_lr(lr)
+    opts = [torch.optim.Adam(m.parameters(), lr=lr, weight_decay=wd, foreach=False) for m in (ref, noisy)]
+    for s in range(steps):
+        idx = torch.arange(s * B, (s + 1) * B, device="cuda") % X.shape[0]
+        runner.reset_metrics()
+        runner.train_step(idx)
+        torch.cuda.synchronize()
+        eng = prog.metrics[0, 0].item() / B
+        losses = []
+        for m, opt in zip((ref, noisy), opts):
+            m.train()
+            opt.zero_grad()
+            loss = F.cross_entropy(m(X[idx].bfloat16().float()), labels[idx])
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+        tol = 1.5 * abs(losses[1] - losses[0]) + 0.02 * abs(losses[0]) + 1e-3
+        print(f"step {s}: engine {eng:.4f}  oracle {losses[0]:.4f}  noisy oracle {losses[1]:.4f}")
+        assert abs(eng - losses[0]) <= tol, (s, eng, losses)
+    upd_e = torch.cat([(p.detach() - p0[n]).flatten() for n, p in model.named_parameters()])
+    upd_r = torch.cat([(p.detach() - p0[n]).flatten() for n, p in ref.named_parameters()])
+    upd_n = torch.cat([(p.detach() - pn0[n]).flatten() for n, p in noisy.named_parameters()])
+    e, bound = rel(upd_e, upd_r), 1.5 * rel(upd_n, upd_r) + 0.05
+    print(f"3-step update: engine vs oracle {e:.3f}, noisy oracle vs oracle {rel(upd_n, upd_r):.3f}")
+    assert e <= bound, (e, bound)
