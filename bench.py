@@ -113,8 +113,7 @@ def main():
     reducer = FlatGradAllReducer(ctx) if (ctx.enabled or len(buckets) > 1) else None
     if reducer is not None and args.dp_shape > 1:
         reducer.capturable = False  # what a multi-rank group runs (DistContext.capturable_collectives)
-    runner = StepRunner(prog, X, labels, use_graph=not args.no_graph and (not sync or ctx.capturable_collectives),
-                        allreduce=reducer)
+    runner = StepRunner(prog, X, labels, use_graph=not args.no_graph and (not sync or captured), allreduce=reducer)
     runner.set_lr(1e-3 / 1.5)  # reference: lr/1.5 applied at the epoch-0 validation
     sampler = ShardedIndexSampler(args.dataset_size * world, args.batch, ctx, seed=7)
     # indices address this rank's resident shard

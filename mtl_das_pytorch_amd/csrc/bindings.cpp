@@ -275,7 +275,8 @@ py::tuple tail_table(py::list dicts, py::list blocks, bool bwd) {
     j.a = parse_tail(dicts[i].cast<py::dict>());
     j.blocks = blocks[i].cast<int>();
     if (j.blocks <= 0 || j.a.C % 8 || j.a.r || j.a.r_bn) throw std::runtime_error("tail_table: unsupported tail");
-    if (bwd && (!j.a.part || j.a.chunk_px <= 0 || j.a.side || j.a.gscale != 1.f))
+    // (gscale != 1: SyncBN's batched apply writes d(gamma), d(beta) / world -- bnb_apply_impl reads it)
+    if (bwd && (!j.a.part || j.a.chunk_px <= 0 || j.a.side || !(j.a.gscale > 0.f)))
       throw std::runtime_error("tail_table: unsupported backward tail");
     j.block0 = (int)b0;
     b0 += j.blocks;

@@ -214,6 +214,11 @@ class EngineBackend(Backend):
         if sync:  # SyncBN: BN statistics all-reduced inside the step (captured into the HIP graph on RCCL)
             self.prog.enable_sync_bn(ctx.all_reduce_ordered_)
             if not ctx.capturable_collectives:
+                # gloo, or RCCL with several ranks (capture opt-in: MDA_CAPTURE_COLLECTIVES=1): the step runs
+                # its launches and collectives eagerly -- say so, this is several times slower
+                if ctx.is_main:
+                    print("SyncBN: collectives are not captured on this process group; the training step runs "
+                          "eagerly (set MDA_CAPTURE_COLLECTIVES=1 on RCCL to capture them)", flush=True)
                 use_graph = False
         self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world,
                                 data_parallel=ctx.enabled)

@@ -318,6 +318,23 @@ class BNLayer:
         self.pnrep = max(self.nrep, min(NREP, 1 << max(0, math.ceil(math.log2(max(1, self.nchunk))))))
         self.arena = arena
         self.dzbuf = None
+        self.part_off = 0            # element offset of this BN's rows in ``part`` (coalesce_replicas)
+        self.coalesced = set()       # {"stats", "part"}: rows live in a buffer shared with sibling BNs
+
+    def used_stats(self):
+        """The forward replica rows that hold data (what a SyncBN collective reduces): this BN's region of a
+        coalesced buffer, else its first ``nrep`` replicas (all groups for a grouped BN)."""
+        t = self.stats.t if hasattr(self.stats, "bind") else self.stats
+        if "stats" in self.coalesced:
+            return t[self.stats_off:self.stats_off + self.nrep * 2 * self.C]
+        return t[0, :self.nrep] if t.shape[0] == 1 else t
+
+    def used_part(self):
+        """The backward partial-sum rows that hold data (see used_stats)."""
+        t = self.part.t if hasattr(self.part, "bind") else self.part
+        if "part" in self.coalesced:
+            return t[self.part_off:self.part_off + self.pnrep * 3 * self.C]
+        return t[0, :self.pnrep] if t.shape[0] == 1 else t
 
     def args(self, training: bool) -> dict:
         f = self.flat
@@ -333,6 +350,31 @@ class BNLayer:
         f = self.flat
         m0 = self.mods[0]
         return {"dgamma": P(f.grads, f.off(m0.weight)), "dbeta": P(f.grads, f.off(m0.bias)), "pgs": self.pstride}
+
+
+def coalesce_replicas(bns: Sequence["BNLayer"], which: str, arena: "Arena"):
+    """Give the ``which`` ("stats": forward sums, "part": backward partial sums) replica rows of ``bns`` ONE
+    contiguous zeroed buffer, each BN's used replicas (nrep / pnrep rows of C) back to back, so that a SyncBN
+    step all-reduces them with a single collective (engine/inception.py: the branch-output BNs of an
+    Inception block, whose statistics complete together at the block's join).  Kernels index only the used
+    replicas of a one-group BN, so the region of each BN is exactly what they touch.  Returns the buffer.
+    Must run before the arena is finalized."""
+    rows = 2 if which == "stats" else 3
+    sizes = []
+    for bn in bns:
+        if bn.G != 1 or (which == "stats" and bn.sld != bn.C) or which in bn.coalesced:
+            raise ValueError("only one-group BNs with their own replica rows can be coalesced")
+        sizes.append((bn.nrep if which == "stats" else bn.pnrep) * rows * bn.C)
+    buf = arena.zeroed((sum(sizes),), torch.float64)
+    off = 0
+    for bn, n in zip(bns, sizes):
+        if which == "stats":
+            bn.stats, bn.stats_off = buf, off
+        else:
+            bn.part, bn.part_off = buf, off
+        bn.coalesced.add(which)
+        off += n
+    return buf
 
 
 def stem_pack_geom(m: nn.Conv2d, Hi: int, Wi: int) -> Optional[dict]:
@@ -535,7 +577,7 @@ class ConvLayer:
         d = {"src": src, "w": P(self.wf), "wgs": self.Npad * self.Kpad if self.G > 1 else 0,
              "bias": P(f.params, f.off(self.mods[0].bias)) if self.has_bias else 0, "bgs": self.bstride,
              "out": out.p, "ogs": out.gs, "ldo": out.ld,
-             "stats": P(bn.stats) if (bn is not None and training) else 0,
+             "stats": P(bn.stats, bn.stats_off) if (bn is not None and training) else 0,
              "stats_nrep": bn.nrep if bn is not None else NREP,
              "B": self.B, "Hs": self.Hi, "Ws": self.Wi, "Ho": self.Ho, "Wo": self.Wo, "N": self.Co, "Npad": self.Npad,
              "Cs": self.Cs, "KH": self.KH, "KW": self.KW, "sh": self.sh, "sw": self.sw, "ph": self.ph, "pw": self.pw,

@@ -19,17 +19,18 @@ Launch counts per training step (B fixed): forward 94 conv + 94 tails + 13 pools
 from __future__ import annotations
 
 import os
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import torch
 
 from ..models.multi_classifier import (BasicConv2d, InceptionA, InceptionB, InceptionC, InceptionD, InceptionE,
                                        Multi_Classifier)
 from . import guard
-from .core import GRAD_DT, NREP, Act, Arena, BNLayer, ConvLayer, FlatState, P, grads_of, new_act, src_dict, stem_pack_geom
+from .core import (GRAD_DT, NREP, Act, Arena, BNLayer, ConvLayer, FlatState, P, coalesce_replicas, grads_of, new_act,
+                   src_dict, stem_pack_geom)
 from .lowering import ACT_RELU, LoweredProgram
 from ..ops.hip import lib
-from .program import Phase, k_cls_head, k_pool, k_wgfin
+from .program import Phase, k_allreduce, k_cls_head, k_pool, k_wgfin
 
 
 class Val:
@@ -415,11 +416,25 @@ class InceptionProgram(LoweredProgram):
         self.n_tail_batched = 0
         if not self.tail_batch_enabled():
             return
+        by_block: Dict[int, List[CBR]] = {}
         for i, op in enumerate(self.ops):
             if (isinstance(op, CBR) and not op.skip_tail and op.out.parent is not None
                     and self.op_meta[i] is not None):
                 op.defer_tail = True
                 self.n_tail_batched += 1
+                by_block.setdefault(self.op_meta[i][0], []).append(op)
+        # the block's branch-output BNs complete together (forward: at the join, before the batched tail;
+        # backward: the batched reduce): their replica rows share one buffer each way, so SyncBN all-reduces
+        # them with ONE collective per block and direction (enable_sync_bn, batch_tails).  Members of a
+        # horizontally fused conv keep the fused conv's forward rows (reduced when that conv ran).
+        self._stat_groups, self._part_groups = [], {}
+        for blk, ops in by_block.items():
+            own = [op.bn for op in ops if op.fused is None]
+            if len(own) >= 2:
+                self._stat_groups.append((coalesce_replicas(own, "stats", self.arena), own))
+            if len(ops) >= 2:
+                bns = [op.bn for op in ops]
+                self._part_groups[blk] = (coalesce_replicas(bns, "part", self.arena), bns)
 
     def batch_tails(self) -> int:
         """The backward of the branch-output BN+ReLU tails of each Inception block as ONE reduce and ONE apply
@@ -429,20 +444,13 @@ class InceptionProgram(LoweredProgram):
         launch waits for the batch.  Runs after the autotuner (which picks the per-tail variants the batch
         replaces); not with SyncBN (its collectives sit between the passes).  Returns the tails batched."""
         from .program import Launch, k_tail_bwd_batched
-        if not self.tail_batch_enabled() or getattr(self, "sync_bn_world", None) is not None:
+        sync = getattr(self, "sync_bn_world", None) is not None
+        if not self.tail_batch_enabled():
             return 0
         ls = self.bwd.launches
-        fork_at = {}
-        blk = None
-        groups = {}
-        for i, l in enumerate(ls):
-            if l.name.startswith("fork:backward_f"):
-                blk = l.name
-                fork_at[blk] = i
-            elif (l.name.startswith("tailbwd") and isinstance(l.owner, CBR) and l.owner.defer_tail and blk is not None
-                  and l.args[3].get("fused", 0) in (0, 1) and l.args[0] == ACT_RELU and l.args[1] == 1
-                  and not l.args[3].get("side")):
-                groups.setdefault(blk, []).append(l)
+        fork_at, groups = self._tail_bwd_groups()
+        if sync:  # only the blocks whose collective enable_sync_bn left to this batch (one per block)
+            groups = {b: t for b, t in groups.items() if b in self._sync_part_groups}
         n = 0
         removed = set()
         inserts = []
@@ -451,6 +459,9 @@ class InceptionProgram(LoweredProgram):
             while any((t.args[3]["C"] // 8) % cgb for t in tails):
                 cgb //= 2
             jobs = [dict(t.args[3], fused=0) for t in tails]
+            if sync:  # the apply writes d(gamma), d(beta) / world (enable_sync_bn)
+                for j in jobs:
+                    j["gscale"] = 1.0 / self.sync_bn_world
             blocks = [t.args[2] * (t.args[3]["C"] // (8 * cgb)) for t in tails]
             raw, nblocks, _ = lib().tail_table(jobs, blocks, True)
             table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
@@ -461,7 +472,11 @@ class InceptionProgram(LoweredProgram):
                          owner=tails, stream=0)
             app = Launch("tailbatchbwd_apply", k_tail_bwd_batched, ACT_RELU, cgb, 0, table, len(jobs), nblocks,
                          owner=tails, stream=0, record=tag)
-            inserts.append((fork_at[blk] + 1, [red, app]))
+            mid = []
+            if sync:  # the block's partial sums all-reduced between the passes: one collective
+                mid = [Launch("allreduce_bn", k_allreduce, self._sync_allreduce, self._sync_part_groups[blk].t,
+                              stream=0)]
+            inserts.append((fork_at[blk] + 1, [red] + mid + [app]))
             for t in tails:
                 if t.record is not None:
                     raise RuntimeError(f"batched tail backward records event {t.record}")
@@ -481,6 +496,53 @@ class InceptionProgram(LoweredProgram):
         self.bwd.launches = out
         self.n_tail_bwd_batched = n
         return n
+
+    def _tail_bwd_groups(self):
+        """The block-output BN-tail backward launches batch_tails batches, per block (keyed by the block's
+        backward fork pseudo-launch), and the index of each fork."""
+        fork_at, groups, blk = {}, {}, None
+        for i, l in enumerate(self.bwd.launches):
+            if l.name.startswith("fork:backward_f"):
+                blk = l.name
+                fork_at[blk] = i
+            elif (l.name.startswith("tailbwd") and isinstance(l.owner, CBR) and l.owner.defer_tail and blk is not None
+                  and l.args[3].get("fused", 0) in (0, 1) and l.args[0] == ACT_RELU and l.args[1] == 1
+                  and not l.args[3].get("side")):
+                groups.setdefault(blk, []).append(l)
+        return fork_at, groups
+
+    def enable_sync_bn(self, allreduce) -> int:
+        """SyncBN (LoweredProgram.enable_sync_bn) with the branch-output BNs of every Inception block coalesced:
+        forward, one all-reduce of the block's own replica rows right before its batched BN+ReLU tail (after
+        the join, where all of them are complete); backward, one all-reduce of the block's partial sums
+        between the batched reduce and apply passes (batch_tails).  Blocks whose tails do not all batch
+        (e.g. statistics fused into a data gradient) keep one collective per BN.  Returns the all-reduces per
+        training step (Model C: 188 -> 126)."""
+        from .program import Launch
+        skip_fwd = {P(bn.stats, bn.stats_off) for _, g in self._stat_groups for bn in g}
+        _, groups = self._tail_bwd_groups()
+        self._sync_part_groups = {}
+        by_buf = {id(buf): (buf, bns) for buf, bns in self._part_groups.values()}
+        for blk, tails in groups.items():
+            bufs = {id(t.owner.bn.part) for t in tails}
+            if len(bufs) == 1 and len(by_buf[next(iter(bufs))][1]) == len(tails):
+                self._sync_part_groups[blk] = by_buf[next(iter(bufs))][0]
+        skip_bwd = {P(t.owner.bn.part, t.owner.bn.part_off) for blk in self._sync_part_groups for t in groups[blk]}
+        n = super().enable_sync_bn(allreduce, skip_fwd=skip_fwd, skip_bwd=skip_bwd)
+        self._sync_allreduce = allreduce
+        new = []
+        for l in self.fwd_train.launches:
+            if l.name.startswith("tailbatch") and isinstance(l.owner, list):
+                ptrs = {d["bn"]["stats"] for d, _ in l.owner}
+                for buf, bns in self._stat_groups:
+                    if {P(bn.stats, bn.stats_off) for bn in bns} <= ptrs:
+                        # after the join events (the branches' convs), before the tail that normalises
+                        new.append(Launch("allreduce_bn", k_allreduce, allreduce, buf.t, stream=0, waits=l.waits))
+                        l.waits = ()
+                        n += 1
+            new.append(l)
+        self.fwd_train.launches = new
+        return n + len(self._sync_part_groups)
 
     def _patch_forward(self, conv: ConvLayer) -> bool:
         """The conv's training forward runs a 3x3 patch config in the shipped table: its input strip is staged

@@ -115,7 +115,8 @@ class LoweredProgram:
         """BN-tail backward launch (reduce + apply, or the single-launch kernel; fuse_dgrad_bn_stats may
         later turn it into an apply-only pass)."""
         d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(True), "B": self.B, "H": y.H, "W": y.W, "C": y.C,
-             "g": g, "part": P(bn.part), "chunk_px": bn.chunk_px, "dy": dy.p, "dgs": dy.gs, "ldd": dy.ld}
+             "g": g, "part": P(bn.part, bn.part_off), "chunk_px": bn.chunk_px, "dy": dy.p, "dgs": dy.gs,
+             "ldd": dy.ld}
         if kind in (SIGMUL, POOL_RELU) or len(g) > 1:
             # the apply pass reads the stored dz instead of re-reading several gradient sources /
             # re-evaluating the pool window
@@ -135,7 +136,7 @@ class LoweredProgram:
             raise ValueError("BN backward chunking assumes the BN pixel count equals the tail's pixel count")
         ph.add(f"tailbwd{kind}", k_tail_bwd, kind, G, bn.nchunk, d)
 
-    def enable_sync_bn(self, allreduce) -> int:
+    def enable_sync_bn(self, allreduce, skip_fwd=(), skip_bwd=()) -> int:
         """SyncBN across data-parallel ranks (``--sync_bn`` with the engine).
 
         The program must have been lowered with ``flat.bn_world = world`` (BN counts are global).  Then
@@ -148,25 +149,34 @@ class LoweredProgram:
             sums (torch.nn.SyncBatchNorm); the apply writes d(gamma), d(beta) scaled by 1/world, so after
             the data-parallel gradient average they equal torch's mean of the per-rank local sums.
         Single-launch BN backwards (fused = 1) cannot be split and are replaced by reduce + apply.
-        On RCCL the collectives are captured into the step's HIP graph (stream-ordered; those of BNs on
-        streams >= COLLECTIVE_STREAMS go through stream 0); gloo runs the step eagerly.  Returns the number
-        of all-reduces inserted per training step."""
+        ``skip_fwd`` / ``skip_bwd``: replica-row pointers (forward stats / backward part) of BNs whose
+        collective a subclass emits itself, coalesced with their siblings' (engine/inception.py).
+        Where the process group's collectives are capturable (DistContext.capturable_collectives: a 1-rank
+        RCCL group, or several ranks with MDA_CAPTURE_COLLECTIVES=1) they are captured into the step's HIP
+        graph (stream-ordered; those of BNs on streams >= COLLECTIVE_STREAMS go through stream 0); otherwise
+        -- gloo, and RCCL with several ranks by default -- the step runs eagerly (EngineBackend warns;
+        bench.py --dp-shape 8 --sync_bn measures that form on one GPU).  Returns the number of all-reduces
+        inserted per training step."""
         world = self.flat.bn_world
-        by_stats = {P(bn.stats): bn for bn in self.flat.bn_layers}
-        by_part = {P(bn.part): bn for bn in self.flat.bn_layers}
+        by_stats = {}
+        for bn in self.flat.bn_layers:  # a fused conv's members share its rows: the member at offset 0 stands for all
+            by_stats.setdefault(P(bn.stats, bn.stats_off if "stats" in bn.coalesced else 0), bn)
+        by_part = {P(bn.part, bn.part_off): bn for bn in self.flat.bn_layers}
+        skip_fwd, skip_bwd = set(skip_fwd), set(skip_bwd)
         n = 0
         new = []
         for l in self.fwd_train.launches:
             new.append(l)
-            bn = by_stats.get(l.args[3].get("stats") or 0) if l.name == "conv_fwd" else None
+            st = l.args[3].get("stats") or 0 if l.name == "conv_fwd" else 0
+            bn = by_stats.get(st) if st not in skip_fwd else None
             if bn is not None:
-                new += self._collective(allreduce, self._used_replicas(bn.stats, bn.nrep), l.stream, l.bucket, l.record)
+                new += self._collective(allreduce, bn.used_stats(), l.stream, l.bucket, l.record)
                 l.record = None
                 n += 1
         self.fwd_train.launches = new
         new = []
         for l in self.bwd.launches:
-            if not l.name.startswith("tailbwd") or l.args[3].get("fused") == 3:
+            if not l.name.startswith("tailbwd") or l.args[3].get("fused") == 3 or l.args[3]["part"] in skip_bwd:
                 new.append(l)
                 continue
             kind, G, nchunk, d = l.args
@@ -181,13 +191,13 @@ class LoweredProgram:
                                                                 "dy2", "d2gs", "ldd2", "pgs")}
                 red["fused"] = 3
                 l.name, l.args = f"tailpart{kind}", (kind, G, nchunk, red)
-                new += [l] + self._collective(allreduce, self._used_replicas(bn.part, bn.pnrep), l.stream, l.bucket)
+                new += [l] + self._collective(allreduce, bn.used_part(), l.stream, l.bucket)
             elif l.stream < self.COLLECTIVE_STREAMS:  # statistics from the producing dgrad's epilogue
-                l.name, l.fn, l.args = "allreduce_bn", k_allreduce, (allreduce, self._used_replicas(bn.part, bn.pnrep))
+                l.name, l.fn, l.args = "allreduce_bn", k_allreduce, (allreduce, bn.used_part())
                 new.append(l)
             else:  # (the launch keeps its waits as a kernel-free fork point in front of the collective)
                 l.name, l.fn, l.args = f"fork:{l.name}", None, ()
-                new += [l] + self._collective(allreduce, self._used_replicas(bn.part, bn.pnrep), l.stream, l.bucket)
+                new += [l] + self._collective(allreduce, bn.used_part(), l.stream, l.bucket)
             d = {k: v for k, v in d.items() if k not in ("dzbuf", "dzgs", "lddz")}
             d["fused"], d["gscale"] = 2, 1.0 / world
             new.append(Launch(name, k_tail_bwd, kind, G, nchunk, d, owner=l.owner, stream=l.stream, record=record,
@@ -196,14 +206,6 @@ class LoweredProgram:
         self.bwd.launches = new
         self.sync_bn_world = world
         return n
-
-    @staticmethod
-    def _used_replicas(buf, nrep: int):
-        """The part of a BN replica buffer ([G][NREP][rows][C], arena-bound) that holds data: its first ``nrep``
-        replicas when there is one group (a contiguous slice -- small maps use few replicas, and Model C's 1x6
-        layers would otherwise all-reduce 32x the bytes), the whole buffer for grouped (per-task) BNs."""
-        t = buf.t if hasattr(buf, "bind") else buf
-        return t[0, :nrep] if t.shape[0] == 1 else t
 
     # Collectives captured into the step graph from at most these streams (0 and 1: Model A's backbone and
     # level branches); a collective of a BN on a later stream (Model C's Inception branches) runs on stream 0

@@ -309,6 +309,74 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
     return cache
 
 
+def tune_wgrad_in_step(make_prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str, int], top: int = 10,
+                       topk: int = 3, margin: float = 0.003, verbose: bool = True) -> Dict[str, int]:
+    """Choose the weight-gradient configs of the ``top`` heaviest weight-gradient signatures by the time of
+    the WHOLE captured training step (the isolated ranking favours the tile with the most
+    blocks, and the batch-level ranking of tune_wgrad_batches times the batches alone -- on Model A neither
+    reproduces the step-level choice).  The batched launches are built from the per-conv choices, so every
+    candidate gets its own lowering: ``make_prog()`` builds a fresh, un-tuned program.  Candidates per
+    signature: the ``topk`` configs of the isolated ranking and the signature's large-tile config; one is
+    kept when two re-timings both beat the incumbent (re-timed right before) by ``margin``.  Updates and
+    returns ``cache``."""
+    L = lib()
+    base = make_prog()
+    wg = [l for l in base.bwd.launches if l.name == "conv_wgrad" and l.owner is not None]
+    groups: Dict[str, list] = {}
+    for l in wg:
+        groups.setdefault(wgrad_signature(l.args[1], l.args[2]), []).append(l)
+
+    def weight(sig):
+        d = groups[sig][0].args[2]
+        return len(groups[sig]) * d["B"] * d["Ho"] * d["Wo"] * d["Npad"] * d["Kpad"]
+
+    order = sorted(groups, key=weight, reverse=True)[:top]
+    ranked = {}
+    for sig in order:  # isolated ranking of the signature's valid configs (first launch of the group)
+        l = groups[sig][0]
+        cfg0, G, d = l.args
+        conv, res = l.owner, []
+        for c in WGRAD_CFGS:
+            if all(k.owner.wgrad_valid(c) for k in groups[sig]):
+                conv.set_wgrad_cfg(c)
+                res.append((_time(lambda c=c: L.wgrad(c, G, torch.cuda.current_stream().cuda_stream, d)), c))
+        conv.set_wgrad_cfg(cfg0)
+        res.sort()
+        big = WGRAD_BIG0 + 2 * (conv.Npad > 64) + (conv.Kpad_w > 64)
+        cands = [c for _, c in res[:topk]]
+        if big in {c for _, c in res} and big not in cands:
+            cands.append(big)
+        ranked[sig] = cands
+    del base
+    torch.cuda.empty_cache()
+
+    def step_with(over: Dict[str, int]) -> float:
+        prog = make_prog()
+        cc = dict(cache)
+        cc.update(over)
+        autotune_program(prog, cache=cc, measure=False)
+        t = step_time_us(prog, X, labels, reps=40, rounds=3)
+        del prog
+        torch.cuda.empty_cache()
+        return t
+
+    t0 = step_with({})
+    for sig in order:
+        cur = cache.get(sig)
+        for c in ranked[sig]:
+            if c == cache.get(sig):
+                continue
+            t_inc = step_with({})
+            t = step_with({sig: c})
+            if t < t_inc * (1.0 - margin) and step_with({sig: c}) < step_with({}) * (1.0 - margin):
+                cache[sig] = c
+                if verbose:
+                    print(f"  {sig}: wgrad cfg {cur} -> {c}, step {t:.1f} us (incumbent {t_inc:.1f})", flush=True)
+    if verbose:
+        print(f"weight gradients in the step: {t0:.1f} -> {step_with({}):.1f} us", flush=True)
+    return cache
+
+
 def step_time_us(prog, X: torch.Tensor, labels: torch.Tensor, reps: int = 100, rounds: int = 3) -> float:
     """Best-of-``rounds`` mean time of the training step (gather, forward, backward, Adam + re-pack at
     learning rate 0) captured as one HIP graph; the program's mutable state is restored afterwards."""
@@ -390,7 +458,7 @@ def _set_conv_cfg(launch, cfg: int, keep: dict) -> bool:
 def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str, int], topk: int = 3,
                     reps: int = 15, rounds: int = 3, margin: float = 0.002, verbose: bool = True,
                     on_change=None, cfg_pass: bool = True, xcd_pass: bool = True,
-                    tail_pass: bool = True) -> Dict[str, int]:
+                    tail_pass: bool = True, confirm_rounds: int = 3) -> Dict[str, int]:
     """Refine the conv configs (and the BN-tail backward variants) of a lowered program by timing the WHOLE
     training step, not the isolated launch.
 
@@ -400,8 +468,9 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
     weight gradients, Adam + re-pack, learning rate 0) is captured as one HIP graph and replayed; for every
     conv signature (all launches sharing it change together, so the table stays one config per signature),
     largest isolated time first, each of its ``topk`` best isolated configs is tried and kept when the
-    replayed step gets faster by more than ``margin``.  The program's mutable state is restored afterwards.
-    Updates and returns ``cache``."""
+    replayed step gets faster by more than ``margin``; finally the whole tuned set must beat the starting
+    choices in ``confirm_rounds`` interleaved re-timings, or it is reverted.  The program's mutable state is
+    restored afterwards.  Updates and returns ``cache``."""
     from .step import StateSnapshot, capture_graph
     f = prog.flat
     snap = StateSnapshot([f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step,
@@ -418,7 +487,7 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
         for fn_ in fns:  # eager pass: code objects of a new config loaded before capture
             fn_()
         torch.cuda.synchronize()
-        g, keep, _ = capture_graph(fns)
+        g, events, _ = capture_graph(fns)
         g.replay()
         torch.cuda.synchronize()
         best = float("inf")
@@ -431,7 +500,7 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
             torch.cuda.synchronize()
             best = min(best, s.elapsed_time(e) / reps)
         g.reset()  # release the graph and its executable now (hundreds of captures per tuning run)
-        del g, keep
+        del g, events
         return best
 
     groups: Dict[str, list] = {}
@@ -447,6 +516,12 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
         cur = next((t for t, c in iso if c == cfg & ~CONV_XCD), iso[0][0] if iso else 0.0)
         order.append((cur * len(ls), sig))
     order.sort(reverse=True)
+    # the starting choices, for the closing confirmation (every accepted toggle beat the incumbent measured
+    # right before it, but many toggles at a small margin can still add up to drift -- round 4 accepted 24
+    # changes whose sum was 1.9 % SLOWER)
+    start_cfg = {id(l): l.args[1] for ls in groups.values() for l in ls}
+    start_fused = {id(l): l.args[3].get("fused", 0) for l in prog.bwd.launches if l.name.startswith("tailbwd")}
+    cache_before = dict(cache)
     base = step_ms()
     t0 = base
     if verbose:
@@ -529,6 +604,37 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
         else:
             for l in ls:
                 l.args[3]["fused"] = cur
+    # closing confirmation: the final choices against the starting ones, interleaved rounds; the tuned set is
+    # kept only if it is faster in every round by ``margin`` (else the starting table is restored)
+    changed = [l for ls in groups.values() for l in ls if l.args[1] != start_cfg[id(l)]]
+    ch_tails = [l for l in prog.bwd.launches if l.name.startswith("tailbwd")
+                and l.args[3].get("fused", 0) != start_fused.get(id(l), l.args[3].get("fused", 0))]
+    if changed or ch_tails:
+        final_cfg = {id(l): l.args[1] for l in changed}
+        final_fused = {id(l): l.args[3].get("fused", 0) for l in ch_tails}
+
+        def apply(start: bool):
+            for l in changed:
+                _set_conv_cfg(l, start_cfg[id(l)] if start else final_cfg[id(l)], keep)
+            for l in ch_tails:
+                l.args[3]["fused"] = start_fused[id(l)] if start else final_fused[id(l)]
+        wins = []
+        for _ in range(confirm_rounds):
+            apply(True)
+            t_start = step_ms()
+            apply(False)
+            t_final = step_ms()
+            wins.append(t_final < t_start * (1.0 - margin))
+            if verbose:
+                print(f"  confirmation: start table {t_start * 1e3:.1f} us, tuned {t_final * 1e3:.1f} us", flush=True)
+        if not all(wins):
+            apply(True)
+            cache.clear()
+            cache.update(cache_before)
+            base = t0
+            if verbose:
+                print(f"in-context tuning: {len(changed)} conv / {len(ch_tails)} tail changes not confirmed "
+                      f"against the starting table -- reverted", flush=True)
     for ph in (prog.fwd_train, prog.bwd, prog.fwd_eval):
         ph.__dict__["ws_keep"].update(keep)
     if verbose:

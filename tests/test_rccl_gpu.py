@@ -43,7 +43,9 @@ def test_rccl_one_rank_dp_and_syncbn(model):
         if b > 1:  # the piece path really ran as per-bucket graphs
             assert sum(k.startswith("train_piece") for k in res[f"dp{b}_pieces"]["graphs"]) == b
     s = res["syncbn"]
-    assert s["collectives_per_step"] > 40  # one per BN forward + one per BN backward
+    assert s["collectives_per_step"] > 40  # one per BN forward + one per BN backward ...
+    if model == "multi_classifier":  # ... except the Inception blocks' branch outputs: one per block and direction
+        assert s["collectives_per_step"] <= 115, s["collectives_per_step"]
     assert "train_full" in s["graphs"]  # SyncBN stays on the single-graph step: collectives captured
     assert all(s["graph_eq_eager"].values()), s
     # one step vs plain BN: forward bitwise (BN statistics); backward summation order amplified by the chaotic

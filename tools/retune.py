@@ -8,9 +8,11 @@ Starts from an empty table (``--keep`` starts from the shipped one and only fill
 every conv forward / data-gradient / weight-gradient launch and BN-backward variant of each model's
 program by isolated timing (engine/tune.py autotune_phases); ``--wgrad-batches`` re-chooses the weight-
 gradient configs of A and C by the time of the batched launches they run in (tune_wgrad_batches; Model B
-shares A's backbone signatures and keeps A's choices); ``--spill`` picks the weight-gradient spill fraction
+shares A's backbone signatures and keeps A's choices); ``--wgrad-in-step`` then re-times the heaviest of them
+in the captured step (tune_wgrad_in_step); ``--spill`` picks the weight-gradient spill fraction
 of A and C in the captured step (tune_spill); ``--in-context`` then refines the conv choices by
-timing the whole captured training step per candidate (engine/tune.py tune_in_context).
+timing the whole captured training step per candidate (engine/tune.py tune_in_context; the tuned set is kept
+only if it beats the starting choices in interleaved re-timings).
 Writes the merged table; copy it over mtl_das_pytorch_amd/engine/tuned_cfgs.json to ship it.
 """
 import argparse
@@ -25,7 +27,8 @@ from mtl_das_pytorch_amd.engine.inception import InceptionProgram  # noqa: E402
 from mtl_das_pytorch_amd.engine.mtl import MTLProgram  # noqa: E402
 from mtl_das_pytorch_amd.data.synthetic import generate  # noqa: E402
 from mtl_das_pytorch_amd.engine.tune import (autotune_phases, autotune_program, conv_signature, load_cache,  # noqa: E402
-                                             save_cache, tune_in_context, tune_spill, tune_wgrad_batches)
+                                             save_cache, tune_in_context, tune_spill, tune_wgrad_batches,
+                                             tune_wgrad_in_step)
 from mtl_das_pytorch_amd.ops.functional import CONV_XCD  # noqa: E402
 from mtl_das_pytorch_amd.models import build_model, encode_joint  # noqa: E402
 
@@ -67,6 +70,10 @@ def main():
                     help="--wgrad-batches starts from every im2col conv on its large tile")
     ap.add_argument("--wgrad-batches", action="store_true",
                     help="re-choose the weight-gradient configs by their batched launches' time (tune_wgrad_batches)")
+    ap.add_argument("--wgrad-in-step", action="store_true",
+                    help="then re-choose the heaviest weight-gradient configs by the captured step's time "
+                         "(tune_wgrad_in_step; A and C)")
+    ap.add_argument("--wgrad-top", type=int, default=10, help="--wgrad-in-step: signatures to re-time")
     ap.add_argument("--spill", action="store_true",
                     help="choose the weight-gradient spill fraction in the step (tune_spill)")
     ap.add_argument("--passes", default="cfg,xcd,tail", help="in-context passes: conv configs, tile order, BN tails")
@@ -87,6 +94,12 @@ def main():
             _warm_step(prog, name, args.batch)
             tune_wgrad_batches(prog, cache, verbose=True, passes=2, init_big=args.wgrad_big_init)
             print(f"{name}: weight-gradient batches tuned at {time.time() - t0:.1f} s", flush=True)
+        if args.wgrad_in_step and name in ("MTL", "multi_classifier"):
+            X, d, e = generate(4 * args.batch, seed=3, device="cuda")
+            labels = encode_joint(d, e) if name == "multi_classifier" else torch.stack([d, e], 1)
+            tune_wgrad_in_step(lambda: _make(name, args.batch), X, labels, cache, top=args.wgrad_top)
+            save_cache(cache, args.out)
+            print(f"{name}: weight gradients tuned in the step at {time.time() - t0:.1f} s", flush=True)
         if args.spill and name in ("MTL", "multi_classifier"):
             X, d, e = generate(4 * args.batch, seed=3, device="cuda")
             labels = encode_joint(d, e) if name == "multi_classifier" else torch.stack([d, e], 1)
