@@ -23,7 +23,10 @@ from typing import Dict, List, Sequence
 
 from .program import Phase, stream_slots
 
-EXEC_STREAMS = 4  # the executor's stream count (DEBUG_HIP_FORCE_GRAPH_QUEUES, runtime default 4)
+import os  # noqa: E402
+
+# the executor's stream count (DEBUG_HIP_FORCE_GRAPH_QUEUES: runtime default 4, the package sets 2)
+EXEC_STREAMS = int(os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES", "4"))
 
 
 def launch_records(phases: Sequence[Phase]) -> List[dict]:

@@ -68,6 +68,7 @@ class LoweredProgram:
 
     label_width = 2
     default_buckets = 1  # gradient buckets under data parallelism (segment_backward); MDA_BUCKETS overrides
+    LOCAL_BUCKETS = 1    # the same segmentation of the backward in a single process (no collectives)
 
     def dp_buckets(self, world: int, captured: bool = True) -> int:
         """Gradient buckets of a data-parallel step.  Overlapped buckets only pay inside ONE captured graph
@@ -79,7 +80,7 @@ class LoweredProgram:
         all-reduce costs, so that path uses one bucket."""
         import os
         if world <= 1:
-            return 1
+            return self.LOCAL_BUCKETS
         if not captured:
             return int(os.environ.get("MDA_BUCKETS", "1"))
         return int(os.environ.get("MDA_BUCKETS", str(self.default_buckets)))

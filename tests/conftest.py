@@ -4,6 +4,7 @@ import sys
 import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import mtl_das_pytorch_amd  # noqa: E402,F401  (its HIP runtime settings precede the first HIP call)
 
 
 def pytest_configure(config):

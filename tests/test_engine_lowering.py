@@ -411,7 +411,7 @@ def test_executor_schedule_rule_on_a_recorded_dot():
     ch = [[] for _ in range(16)]
     for a, b in edges:
         ch[a].append(b)
-    assert gs.schedule(ch) == truth
+    assert gs.schedule(ch, 4) == truth  # recorded with the runtime's default 4 executor streams
 
 
 @pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
@@ -429,10 +429,10 @@ def test_restream_plan_puts_every_engine_stream_on_its_own_executor_stream(model
     for r in recs:
         ranks.setdefault(r["phase"], set()).add(r["stream"])
     tgt = [sorted(ranks[r["phase"]]).index(r["stream"]) for r in nodes]
-    n, bad = gs.restream_check(ch, tgt)
+    n, bad = gs.restream_check(ch, tgt, 4)
     assert bad > 0  # the capture order alone leaves streams mixed (what the timelines showed)
-    new, _ = gs.plan_children(ch, tgt)
-    assert gs.restream_check(new, tgt) == (n, 0)
+    new, _ = gs.plan_children(ch, tgt, 4)
+    assert gs.restream_check(new, tgt, 4) == (n, 0)
     assert all(set(a) <= set(b) for a, b in zip(ch, new))  # every dependency kept
     # the added edges are redundant: each new child was already a descendant
     desc = [None] * len(ch)
