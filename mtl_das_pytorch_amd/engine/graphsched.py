@@ -245,7 +245,9 @@ def restream(graph: int, tracker) -> dict:
     emulated assignment is then exact; returns what was done."""
     from ..ops.hip import lib
     _, children = lib().graph_structure(graph)
-    targets = tracker.targets(graph)
+    # more engine streams than executor streams: stream 0 keeps an executor stream of its own, the side
+    # streams fold onto the others
+    targets = [None if t is None else min(t, EXEC_STREAMS - 1) for t in tracker.targets(graph)]
     known, before = restream_check(children, targets)
     new, fillers = plan_children(children, targets)
     _, after = restream_check(new, targets)
