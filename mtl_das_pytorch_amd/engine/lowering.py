@@ -606,6 +606,9 @@ class LoweredProgram:
     # C +0.6-7.5 % / A neutral, and A +0.3-0.6 % / C neutral (docs/PERF.md round 4); class switches for A/B runs
     SIDE_FINALIZE = True
     EARLY_ADAM = True
+    # stream 0's weight-gradient batches (after its last data gradient, the step's serial tail): the
+    # finalize + Adam of every batch but the last runs on a side stream while stream 0 computes the next batch
+    PIPELINE_S0 = False
 
     def batch_wgrads(self):
         """Replace the per-conv weight-gradient launches by batched launches, one per (stream, tile
@@ -667,11 +670,15 @@ class LoweredProgram:
                     batched.append(Launch("wgrad_finalize", k_wgfin, *self._wgfin_args(convs), owner=convs, stream=st,
                                           record=tag))
                     tags = [t for t in tags if t != batched[-2].record] + [tag]
-            rest = [c for c in self.convs if not any(c in v for v in side.values())]
-            if side and rest:
+            early_ok = self.EARLY_ADAM and not self.data_parallel and self._opt_hparams.get("grad_scale", 1.0) == 1.0
+            piped = self._pipeline_s0(inserts, keep, wg) if early_ok and self.PIPELINE_S0 else []
+            done = [c for v in side.values() for c in v] + [c for convs, _ in piped for c in convs]
+            rest = [c for c in self.convs if c not in done]
+            if (side or piped) and rest:
                 ls[fin].owner = rest
                 ls[fin].args = self._wgfin_args(rest)
-            if side and self.EARLY_ADAM and not self.data_parallel and self._opt_hparams.get("grad_scale", 1.0) == 1.0:
+            tags += [tag for _, tag in piped]
+            if (side or piped) and early_ok:
                 # single process: the side convs' Adam + re-pack right after their finalize, on their stream
                 # (the optimizer phase then covers the rest); with gradient averaging (DP, set_optimizer's
                 # data_parallel) the update must wait for the all-reduce, so it stays in the optimizer phase
@@ -692,6 +699,8 @@ class LoweredProgram:
                     batched.append(Launch("adam_pack_early", k_adam, d, stream=st, record=tag))
                     tags = [t for t in tags if t != f"wgfin_s{st}"] + [tag]
                     self._early_adam = getattr(self, "_early_adam", []) + [d]
+                for convs, _ in piped:
+                    early |= {self.flat.off(m.weight) for c in convs for m in c.mods}
                 segs = [g for g in self.opt_segs if not (g["kind"] == 3 and g["off"] in early)]
                 table, ns, nb = build_optseg_table(segs, self.device)
                 self._opt_tables = getattr(self, "_opt_tables", []) + [table]
@@ -705,6 +714,45 @@ class LoweredProgram:
         ls[fin].waits = tuple(tags)
         self.bwd.launches = keep + ls[fin:]
         self.wgrads_batched = True
+
+    def _pipeline_s0(self, inserts, keep: List[Launch], wg: List[Launch]):
+        """PIPELINE_S0: after each of stream 0's weight-gradient batches but the last, a side stream reduces
+        that batch's split slabs (finalize) and runs the Adam + re-pack of its convs while stream 0 computes
+        the next batch, so the tail after stream 0's last batch only finalizes and updates the last batch's
+        convs.  A batch is pipelined only if none of its convs has a data gradient on another stream (its
+        weights must be dead once stream 0 reaches the batch).  Appends the launches to stream 0's insert
+        list; returns [(convs, event tag)] of the pipelined batches."""
+        s0 = next((b for _, b in inserts if b[0].stream == 0), None)
+        streams = {l.stream for l in keep}
+        if s0 is None or len(s0) < 2 or 1 not in streams:
+            return []
+        dgrad_streams = {}
+        for l in keep:
+            if l.name.startswith("conv_dgrad") and l.owner is not None:
+                dgrad_streams.setdefault(id(l.owner), set()).add(l.stream)
+        out, new = [], []
+        for i, b in enumerate(s0):
+            new.append(b)
+            if i == len(s0) - 1:
+                break
+            convs = list(dict.fromkeys(l.owner for l in wg if l.stream == 0 and l.args[0] == b.args[0]
+                                       and l.owner is not None))
+            if not convs or any(dgrad_streams.get(id(c), {0}) != {0} for c in convs):
+                continue
+            b.record = f"wgb0_{i}"
+            tag = f"adam_p{i}"
+            offs = {self.flat.off(m.weight) for c in convs for m in c.mods}
+            segs = [g for g in self.opt_segs if g["kind"] == 3 and g["off"] in offs]
+            table, ns, nb = build_optseg_table(segs, self.device)
+            self._opt_tables = getattr(self, "_opt_tables", []) + [table]
+            d = dict(self._opt_base, segs=P(table), nsegs=ns, nblocks=nb, update=1, inc_step=0, **self._opt_hparams)
+            self._early_adam = getattr(self, "_early_adam", []) + [d]
+            new += [Launch("wgrad_finalize", k_wgfin, *self._wgfin_args(convs), owner=convs, stream=1,
+                           waits=(b.record,)),
+                    Launch("adam_pack_early", k_adam, d, stream=1, record=tag)]
+            out.append((convs, tag))
+        s0[:] = new
+        return out
 
     def _wgrad_batch_launch(self, cfg: int, group: List[Launch], st: int, bucket: int = 0) -> Launch:
         raw, nblocks = lib().wgrad_table(cfg, [l.args[2] for l in group], [l.args[1] for l in group])

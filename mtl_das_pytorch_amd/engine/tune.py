@@ -54,11 +54,14 @@ def wgrad_signature(G: int, d: dict) -> str:
 
 def load_cache(path: Optional[str] = None) -> Dict[str, int]:
     """The shipped table, or the one named by MDA_TUNED_CFGS (A/B runs of two tables on one box)."""
-    path = path or os.environ.get("MDA_TUNED_CFGS") or _CACHE_PATH
+    named = path or os.environ.get("MDA_TUNED_CFGS")
+    path = named or _CACHE_PATH
     try:
         with open(path) as f:
             return json.load(f)
     except (OSError, ValueError):
+        if named:  # an explicitly named table that cannot be read must not silently become an empty one
+            raise
         return {}
 
 
