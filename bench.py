@@ -93,7 +93,7 @@ def main():
     prog = (InceptionProgram(model, args.batch, dev, sync_world=sw) if joint
             else MTLProgram(model, args.batch, dev, sync_world=sw))
     if sync:  # the statistics collectives are captured into the step's HIP graph (RCCL)
-        prog.enable_sync_bn(ctx.all_reduce_ordered_)
+        n_sync = prog.enable_sync_bn(ctx.all_reduce_ordered_)
     prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world,
                        data_parallel=ctx.enabled or args.dp_shape > 1)
     if hasattr(prog, "set_rng_stream"):  # Model C dropout: an independent mask stream per rank
@@ -176,6 +176,7 @@ def main():
                                     if args.model in EAGER_BY_MODEL else None),
         "hip_graph": runner.use_graph,
         "sync_bn": sync,
+        "sync_bn_collectives_per_step": n_sync if sync else 0,
         "grad_buckets_mb": [round((hi - lo) * 4 / 2 ** 20, 2) for lo, hi in buckets],
         "dist_backend": ctx.backend,
         "dp_shape": shape,

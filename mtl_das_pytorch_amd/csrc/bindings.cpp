@@ -201,9 +201,9 @@ py::tuple wgrad_table(int cfg, py::list dicts, py::list groups) {
   return py::make_tuple(py::bytes(reinterpret_cast<const char*>(jobs.data()), jobs.size() * sizeof(WgradJob)), b0);
 }
 
-void wgrad_batched(int cfg, int64_t table, int nj, int64_t nblocks, int64_t stream, int64_t cap) {
+void wgrad_batched(int cfg, int64_t table, int nj, int64_t nblocks, int64_t stream, int64_t cap, int xcd) {
   check(launch_wgrad_batched(cfg, reinterpret_cast<const WgradJob*>(static_cast<intptr_t>(table)), nj, nblocks,
-                             S(stream), cap), "wgrad_batched");
+                             S(stream), cap, xcd), "wgrad_batched");
 }
 
 WgradArgs parse_wgrad(const py::dict& d) {
@@ -431,7 +431,7 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("pool3", &pool3);
   m.def("wgrad_table", &wgrad_table);
   m.def("wgrad_batched", &wgrad_batched, py::arg("cfg"), py::arg("table"), py::arg("nj"), py::arg("nblocks"),
-        py::arg("stream"), py::arg("cap") = 0);
+        py::arg("stream"), py::arg("cap") = 0, py::arg("xcd") = 0);
   m.def("grad_sum", &grad_sum);
   m.def("synth_das", &synth_das);
   m.def("philox_kat", [](int64_t ctr, uint64_t key, int64_t out, int n, int64_t stream) {

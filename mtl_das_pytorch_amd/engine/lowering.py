@@ -521,6 +521,9 @@ class LoweredProgram:
     WGRAD_MAX_BATCHES = 3
     # the same cap for stream 0 only (its batches run serially after the data-gradient chain); None: as above
     WGRAD_MAX_BATCHES_S0 = None
+    # batched weight-gradient launches walk their virtual blocks in XCD-contiguous order (csrc/conv.hip
+    # wgrad_vblock): the tiles and neighbouring M splits that read the same rows share one L2
+    WGRAD_XCD = 0
     # hardware blocks of a side stream's batched weight-gradient launch (0: one per virtual block): a capped,
     # persistent grid leaves CU slots free for the critical chain's kernels (csrc/conv.hip WGRAD_FOR_VBLOCKS)
     SIDE_WGRAD_GRID = 0
@@ -759,7 +762,8 @@ class LoweredProgram:
         table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         self.wgrad_tables.append(table)
         cap = self.SIDE_WGRAD_GRID if st != 0 else 0
-        return Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, cap, stream=st, bucket=bucket)
+        return Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, cap, self.WGRAD_XCD, stream=st,
+                      bucket=bucket)
 
     def _batch_wgrads_segmented(self):
         """batch_wgrads for a backward cut into gradient-bucket pieces (segment_backward): in every piece,

@@ -345,8 +345,8 @@ def k_pool(is_max, bwd, d, st):
     lib().pool3(is_max, bwd, st, d)
 
 
-def k_wgrad_batched(cfg, table, nj, nblocks, cap, st):
-    lib().wgrad_batched(cfg, table.data_ptr(), nj, nblocks, st, cap)
+def k_wgrad_batched(cfg, table, nj, nblocks, cap, xcd, st):
+    lib().wgrad_batched(cfg, table.data_ptr(), nj, nblocks, st, cap, xcd)
 
 
 def k_wgfin(table, nd, nblocks, st):

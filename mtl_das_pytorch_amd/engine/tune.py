@@ -268,7 +268,8 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
             t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(prog.device)
             tables.append(t)
             total += _time(lambda c=key[2], t=t, n=len(job), nb=nblocks:
-                           L.wgrad_batched(c, t.data_ptr(), n, nb, torch.cuda.current_stream().cuda_stream))
+                           L.wgrad_batched(c, t.data_ptr(), n, nb, torch.cuda.current_stream().cuda_stream, 0,
+                                           prog.WGRAD_XCD))
         for f in fin:
             total += _time(lambda f=f: f.fn(*f.args, torch.cuda.current_stream().cuda_stream))
         return total

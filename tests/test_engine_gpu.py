@@ -204,11 +204,12 @@ def test_batched_wgrad_bitwise_equal(model_name, big):
     """One launch per tile config computes exactly what the per-conv launches compute (also with every
     conv on the large-tile configs, whose gradients must match the default configs' to fp32 order), and so
     does a side stream's batch on a capped persistent grid (LoweredProgram.SIDE_WGRAD_GRID: 7 hardware
-    blocks walking all virtual blocks)."""
+    blocks walking all virtual blocks), with the virtual blocks in XCD-contiguous order or in launch order
+    (LoweredProgram.WGRAD_XCD)."""
     from mtl_das_pytorch_amd.models import build_model, encode_joint
     from mtl_das_pytorch_amd.data.synthetic import generate
     grads = []
-    for batched in (False, True, "capped"):
+    for batched in (False, True, "capped", "capped_linear", "linear"):
         torch.manual_seed(0)
         m = build_model(model_name)
         if model_name == "multi_classifier":
@@ -219,7 +220,8 @@ def test_batched_wgrad_bitwise_equal(model_name, big):
             prog = MTLProgram(m, 8, "cuda")
         if big:
             assert _force_big_wgrad(prog) > 0
-        prog.SIDE_WGRAD_GRID = 7 if batched == "capped" else 0  # (Model A ships 512)
+        prog.SIDE_WGRAD_GRID = 7 if batched in ("capped", "capped_linear") else 0  # (Model A ships 512)
+        prog.WGRAD_XCD = 0 if batched in ("capped_linear", "linear") else 1
         if batched:
             prog.batch_wgrads()
         X, d, e = generate(16, seed=1, device="cuda")
@@ -228,8 +230,10 @@ def test_batched_wgrad_bitwise_equal(model_name, big):
         grads.append(prog.flat.grads.clone())
         if batched == "capped":
             assert any(l.name == "wgrad_batched" and l.args[4] == 7 for l in prog.bwd.launches)
-    assert torch.equal(grads[0], grads[1])
-    assert torch.equal(grads[0], grads[2])
+        if batched:
+            assert all(l.args[5] == prog.WGRAD_XCD for l in prog.bwd.launches if l.name == "wgrad_batched")
+    for g in grads[1:]:
+        assert torch.equal(grads[0], g)
 
 
 @pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
