@@ -757,12 +757,16 @@ class LoweredProgram:
         s0[:] = new
         return out
 
+    def wgrad_flags(self) -> int:
+        """Flag word of the batched weight-gradient launches (csrc/conv.hip wgrad_vblock)."""
+        return 1 if self.WGRAD_XCD else 0
+
     def _wgrad_batch_launch(self, cfg: int, group: List[Launch], st: int, bucket: int = 0) -> Launch:
         raw, nblocks = lib().wgrad_table(cfg, [l.args[2] for l in group], [l.args[1] for l in group])
         table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         self.wgrad_tables.append(table)
         cap = self.SIDE_WGRAD_GRID if st != 0 else 0
-        return Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, cap, self.WGRAD_XCD, stream=st,
+        return Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, cap, self.wgrad_flags(), stream=st,
                       bucket=bucket)
 
     def _batch_wgrads_segmented(self):

@@ -269,7 +269,7 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
             tables.append(t)
             total += _time(lambda c=key[2], t=t, n=len(job), nb=nblocks:
                            L.wgrad_batched(c, t.data_ptr(), n, nb, torch.cuda.current_stream().cuda_stream, 0,
-                                           prog.WGRAD_XCD))
+                                           prog.wgrad_flags()))
         for f in fin:
             total += _time(lambda f=f: f.fn(*f.args, torch.cuda.current_stream().cuda_stream))
         return total

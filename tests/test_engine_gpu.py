@@ -231,7 +231,7 @@ def test_batched_wgrad_bitwise_equal(model_name, big):
         if batched == "capped":
             assert any(l.name == "wgrad_batched" and l.args[4] == 7 for l in prog.bwd.launches)
         if batched:
-            assert all(l.args[5] == prog.WGRAD_XCD for l in prog.bwd.launches if l.name == "wgrad_batched")
+            assert all(l.args[5] == prog.wgrad_flags() for l in prog.bwd.launches if l.name == "wgrad_batched")
     for g in grads[1:]:
         assert torch.equal(grads[0], g)
 
