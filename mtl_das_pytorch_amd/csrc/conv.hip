@@ -431,6 +431,7 @@ DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
 // transform applied on the way (the forward conv read act(BN(y)) on load: rebuild the operand the same way).
 struct WgCtx {
   int n0, mend, HWo;
+  float ihwo, iwo;  // 1 / HWo, 1 / Wo (fdiv24); ihwo = 0: M >= 2^24, integer division
   const bf16_t *base0, *base1, *dyz;
 };
 
@@ -462,8 +463,8 @@ struct WgStage {
         const int m = mc + p;
         const int e = s_tab[g];
         if (m < c.mend && ((e >> 29) & 1)) {
-          const int b = m / c.HWo, r = m - b * c.HWo;
-          const int oh = r / a.Wo, ow = r - oh * a.Wo;
+          const int b = c.ihwo != 0.f ? fdiv24(m, c.HWo, c.ihwo) : m / c.HWo, r = m - b * c.HWo;
+          const int oh = c.ihwo != 0.f ? fdiv24(r, a.Wo, c.iwo) : r / a.Wo, ow = r - oh * a.Wo;
           const int ih = oh * a.sh - a.ph + ((e >> 21) & 127);
           const int iw = ow * a.sw - a.pw + ((e >> 14) & 127);
           if (ih >= 0 && ih < a.Hi && iw >= 0 && iw < a.Wi) {
@@ -530,6 +531,8 @@ DEV WgCtx wgrad_tile_setup(const WgradArgs& a, int n0, int k0, int split, int z,
   WgCtx c;
   c.n0 = n0;
   c.HWo = a.Ho * a.Wo;
+  c.ihwo = (int64_t)a.B * c.HWo < (1 << 24) ? 1.f / (float)c.HWo : 0.f;
+  c.iwo = 1.f / (float)a.Wo;
   c.mend = min(a.B * c.HWo, (split + 1) * a.m_per_split);
   c.base0 = a.src.p[0] + a.src.gs[0] * z;
   c.base1 = a.src.p[1] ? a.src.p[1] + a.src.gs[1] * z : c.base0;
