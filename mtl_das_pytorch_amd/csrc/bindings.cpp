@@ -310,6 +310,10 @@ void mtl_head(int64_t stream, py::dict d) {
   a.logp = P<float>(d, "logp"); a.dfeat = P<bf16_t>(d, "dfeat"); a.dgs = I(d, "dgs");
   a.metrics = P<float>(d, "metrics"); a.confusion = P<int>(d, "confusion");
   a.nvalid = P<const int64_t>(d, "nvalid");
+  if (d.contains("my") && !d["my"].is_none()) {
+    a.my = P<const bf16_t>(d, "my"); a.mygs = I(d, "mygs"); a.ldmy = (int)I(d, "ldmy");
+    a.mbn = parse_bn(d["mbn"].cast<py::dict>());
+  }
   check(launch_mtl_head(a, S(stream)), "mtl_head");
 }
 

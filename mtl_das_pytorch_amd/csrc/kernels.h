@@ -190,6 +190,12 @@ struct HeadArgs {
   float* metrics;   // [T][4]: loss_sum, correct, count, abs_err_sum
   int* confusion;   // [T][16][16]
   const int64_t* nvalid;  // samples b >= *nvalid are padding: no metrics, no gradient (may be null)
+  // optional (my null = off): the features are the attention product sigmoid(BN(my)) * feat computed on load
+  // -- the last level's SIGMUL tail folded into the head (feat is then the shared feature, fgs 0; my the
+  // mask generator's pre-BN output per task, + t * mygs).  Block (0, t) updates that BN's running statistics
+  // and publishes its constants for the backward, as the tail's block 0 did.
+  const bf16_t* my; int64_t mygs; int ldmy;
+  BNArgs mbn;
 };
 
 struct ClsArgs {

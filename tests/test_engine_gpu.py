@@ -56,15 +56,19 @@ def _ref_grads(m, x, labels, idx, cols):
     return outs, {n: p.grad.detach().clone() for n, p in m.named_parameters()}
 
 
-@pytest.mark.parametrize("which", ["MTL", "single_distance", "single_event"])
-def test_engine_train_step_matches_autograd(which):
+@pytest.mark.parametrize("which", ["MTL", "MTL_headmask", "single_distance", "single_event"])
+def test_engine_train_step_matches_autograd(which, monkeypatch):
     """The engine's gradients are compared with fp32 autograd on the SAME bf16-rounded weights.  The
     reference network at random init is ill-conditioned (0.1% weight noise moves early-layer gradients
     by ~15-20%, measured with a launch-by-launch comparison), so the bound for each tensor is derived from the reference's
     own sensitivity to a bf16-sized (4e-3) weight perturbation; well-conditioned tensors (head, level 4) are held
-    to a tight absolute bound."""
+    to a tight absolute bound.  MTL_headmask: the last level's attention product computed on load by the head
+    kernel (MTLProgram.HEAD_MASK, off by default)."""
+    from mtl_das_pytorch_amd.engine.mtl import MTLProgram
     from mtl_das_pytorch_amd.models import MTL_Net, Single_Task_Net
-    if which == "MTL":
+    if which == "MTL_headmask":
+        monkeypatch.setattr(MTLProgram, "HEAD_MASK", True)
+    if which.startswith("MTL"):
         model, ref, prog, X, labels = _setup(MTL_Net)
         cols = [0, 1]
     else:
