@@ -449,3 +449,18 @@ def test_restream_plan_puts_every_engine_stream_on_its_own_executor_stream(model
     sys.setrecursionlimit(10000)
     for v, (a, b) in enumerate(zip(ch, new)):
         assert set(b) - set(a) <= reach(v)
+
+
+@pytest.mark.parametrize("model", ["A", "C"])
+def test_executor_schedule_rule_on_recorded_step_dumps_at_two_streams(model):
+    """The executor rule at the package's 2 executor streams: every node's StreamId of the recorded Model A
+    (120 nodes) and Model C (292 nodes) step graphs (tests/data/graph_dot_2streams.json, recorded on MI355X
+    with tools/graph_dot.py) -- and the 4-stream rule does NOT reproduce C's dump, so the dump really is
+    the 2-stream executor."""
+    import json
+    import os
+    from mtl_das_pytorch_amd.engine import graphsched as gs
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "data", "graph_dot_2streams.json")))[model]
+    assert gs.schedule(d["children"], 2) == d["stream"]
+    if model == "C":
+        assert gs.schedule(d["children"], 4) != d["stream"]
