@@ -181,6 +181,7 @@ def main():
         "dist_backend": ctx.backend,
         "dp_shape": shape,
         "captured_collectives": runner.capture_dp,
+        **({"restream": runner.restream_info} if runner.restream_info else {}),
         "rccl_ranks": dist.get_world_size() if ctx.backend == "nccl" else 0,
         "baseline_note": "vs_baseline divides by BASELINE.md's 176.1 samples/s (reference on CPU, the only "
                          "throughput number it has); vs_eager_pytorch_mi355x divides by the reference-style "
