@@ -106,3 +106,20 @@ def test_engine_sync_bn_trainer(tmp_path):
     log = open(os.path.join(runs[0], "console output.log"), encoding="utf-8").read()
     assert "backend: engine" in log and "world: 2" in log, log[:2000]
     assert log.count("Validation Accuracy") == 2
+
+
+@pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
+def test_bench_contract_two_ranks(model):
+    """The driver's multi-GPU bench invocation (torchrun ... bench.py --gpus N --steps K --warmup W), rehearsed
+    with 2 ranks on one GPU: exactly ONE JSON line (rank 0) with the whole-job value, n_gpus 2, a dp2 config,
+    the eager per-bucket step form a multi-rank group runs, and timing fields consistent with each other."""
+    out = _torchrun([os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", model, "--steps", "6", "--warmup", "3",
+                     "--heldout", "0"], ROOT, timeout=400)
+    lines = [json.loads(l) for l in out.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1, out[-3000:]
+    r = lines[0]
+    assert r["n_gpus"] == 2 and r["steps"] == 6 and r["warmup"] == 3, r
+    assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 64, r
+    assert r["value"] > 0 and r["higher_is_better"] is True and r["scaling"] == "weak", r
+    assert abs(r["value"] - 64 / (r["ms_per_step"] / 1e3)) / r["value"] < 0.02, r
+    assert r["captured_collectives"] is False and r["dist_backend"] == "gloo", r
