@@ -280,6 +280,11 @@ def grads_of(acts: Sequence[Act]) -> List[tuple]:
 class BNLayer:
     """Training-mode BatchNorm state for one BN module or a group of identically shaped per-task BNs."""
 
+    # upper bound of the backward replica count: every backward consumer block (BN-tail apply, fused dgrad
+    # prologue) reads pnrep x 3 x C fp64, every producer spreads its atomics over them.  Same box, interleaved
+    # (docs/PERF.md round 5): 32 / 16 / 8 -> A 35,403 / 35,556 / 35,483 (4 pairs), C 9,331 / 9,410 / 9,439 (3)
+    PNREP_MAX = 16
+
     def __init__(self, mods: Sequence[nn.BatchNorm2d], flat: FlatState, arena: Arena, count: int,
                  stats_share: Optional[tuple] = None):
         """``stats_share`` = (combined replica buffer [G][NREP][2][W], channel offset, W): the forward sums of this
@@ -315,7 +320,7 @@ class BNLayer:
         self.nrep = min(NREP, 1 << max(0, math.ceil(math.log2(max(1, count) / BN_PX_PER_REP))))
         # backward partial sums (bnb reduce chunks, dgrad epilogues): the same count, and every chunk of
         # the reduce pass in a replica of its own when there are few
-        self.pnrep = max(self.nrep, min(NREP, 1 << max(0, math.ceil(math.log2(max(1, self.nchunk))))))
+        self.pnrep = min(self.PNREP_MAX, max(self.nrep, min(NREP, 1 << max(0, math.ceil(math.log2(max(1, self.nchunk)))))))
         self.arena = arena
         self.dzbuf = None
         self.part_off = 0            # element offset of this BN's rows in ``part`` (coalesce_replicas)
