@@ -43,6 +43,10 @@ class MTLProgram(LoweredProgram):
     # gradient chain finds CU slots for its blocks (in-step ramp of a 33x83 dgrad 10-16 us beside an uncapped
     # batch, tools/kernel_phases.py); A 34.71-34.91 k -> 35.08-35.34 k (5 pairs, docs/PERF.md round 5)
     SIDE_WGRAD_GRID = 512
+    # stream 0's weight gradients (after its data-gradient chain, the step's serial tail) in 2 batched launches
+    # instead of 3: A 35,502 -> 35,700 (4 pairs), B_event 37,784 -> 38,246 (2 pairs); all streams at 2: A
+    # 35,676, B 38,112 (docs/PERF.md round 5)
+    WGRAD_MAX_BATCHES_S0 = 2
     # the last level's attention product sigmoid(BN(y)) * F8 is computed on load by the head kernel
     # (csrc/head.hip MASK): its SIGMUL tail launch leaves the end-of-forward critical path
     HEAD_MASK = False
