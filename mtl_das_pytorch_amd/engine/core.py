@@ -33,7 +33,9 @@ NREP = 32  # must match csrc/common.h
 # buffers): bf16 as under autocast -- producers accumulate in fp32 and round once at the store, consumers sum
 # their sources in fp32 (csrc/common.h); half the bytes of the fp32 gradients every backward kernel moved
 GRAD_DT = torch.bfloat16
-BN_PX_PER_REP = 256  # forward BN-statistic replicas: about one per this many pixels
+# forward BN-statistic replicas: about one per this many pixels.  512 vs 256: A +0.3 % (6 of 6 interleaved
+# pairs over two calls, round 5), C neutral
+BN_PX_PER_REP = 512
 
 
 def pad_to(x: int, m: int) -> int:
@@ -316,7 +318,7 @@ class BNLayer:
         self.consts = arena.empty((self.G, 4, self.C), torch.float32)
         # forward replicas in use: about one per BN_PX_PER_REP pixels (the producing conv then has at most
         # ~16 blocks per replica address), so small maps are not read back as 32 mostly-empty replicas by
-        # every consumer block (256 / 1,024 / 4,096 measured within noise, docs/PERF.md)
+        # every consumer block (BN_PX_PER_REP above)
         self.nrep = min(NREP, 1 << max(0, math.ceil(math.log2(max(1, count) / BN_PX_PER_REP))))
         # backward partial sums (bnb reduce chunks, dgrad epilogues): the same count, and every chunk of
         # the reduce pass in a replica of its own when there are few
