@@ -55,6 +55,10 @@ def _grad_offsets(l, gbase: int, numel: int) -> List[int]:
     return out
 
 
+# pixels per thread of a forward BN-tail launch (its grid size; the kernel handles two per iteration)
+TAIL_PX_PER_THREAD = 2
+
+
 def _blocks(M: int, C: int, cap: int = 1024, per_thread: int = 4) -> int:
     cg = max(1, C // 8)
     pl = max(1, 256 // cg)
@@ -89,7 +93,7 @@ class LoweredProgram:
     def _tail_args(self, y: Act, bn: BNLayer, out: Act, training: bool, H=None, W=None) -> tuple:
         d = {"y": y.p, "ygs": y.gs, "ldy": y.ld, "bn": bn.args(training), "out": out.p, "ogs": out.gs, "ldo": out.ld,
              "B": self.B, "H": y.H if H is None else H, "W": y.W if W is None else W, "C": y.C}
-        return d, _blocks(self.B * d["H"] * d["W"], y.C, per_thread=2)
+        return d, _blocks(self.B * d["H"] * d["W"], y.C, per_thread=TAIL_PX_PER_THREAD)
 
     def _tail_batch(self, ph: Phase, kind: int, jobs: List[tuple]):
         """One launch for several single-group forward tails of one kind (``jobs``: (args, blocks) from
@@ -109,7 +113,7 @@ class LoweredProgram:
         if bn2 is not None:
             d["bn2"] = bn2.args(training)
         M = self.B * d["H"] * d["W"]
-        ph.add(f"tail{kind}", k_tail_fwd, kind, G, _blocks(M, y.C, per_thread=2), d)
+        ph.add(f"tail{kind}", k_tail_fwd, kind, G, _blocks(M, y.C, per_thread=TAIL_PX_PER_THREAD), d)
 
     def _tail_bwd(self, ph: Phase, kind: int, G: int, y: Act, bn: BNLayer, g: list, dy: Act, r: Act = None,
                   bn2: BNLayer = None, side: Act = None, dy2: Act = None):
