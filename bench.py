@@ -119,8 +119,12 @@ def main():
     # indices address this rank's resident shard
     batches = [b % args.dataset_size for b in sampler.epoch(0, dev)]
 
+    # the epoch's batch indices stay on the device: each step's gather reads the next row of the schedule
+    # (StepRunner.set_index_schedule), no host-issued index copy before a replay
+    runner.set_index_schedule(torch.stack(batches))
+
     def step(i):
-        runner.train_step(batches[i % len(batches)])
+        runner.train_step()
 
     for i in range(args.warmup):
         step(i)

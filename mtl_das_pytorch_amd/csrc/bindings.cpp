@@ -333,7 +333,8 @@ void cls_head(int64_t stream, py::dict d) {
 }
 
 void gather_batch(int64_t X, int64_t idx, int64_t lab, int lab_w, int64_t out, int64_t lab_out, int B, int Cin, int H,
-                  int W, int64_t stream, int taps, int off, py::list zero) {
+                  int W, int64_t stream, int taps, int off, py::list zero, int64_t cursor, int nrows) {
+  if (cursor && nrows <= 0) throw std::runtime_error("gather_batch: a schedule cursor needs its row count");
   ZeroRanges z{};
   if (zero.size() > 4) throw std::runtime_error("gather_batch: at most 4 zero ranges");
   for (size_t i = 0; i < zero.size(); ++i) {
@@ -346,7 +347,9 @@ void gather_batch(int64_t X, int64_t idx, int64_t lab, int lab_w, int64_t out, i
   z.n = (int)zero.size();
   check(launch_gather_batch(reinterpret_cast<const float*>(X), reinterpret_cast<const int64_t*>(idx),
                             reinterpret_cast<const int64_t*>(lab), lab_w, reinterpret_cast<bf16_t*>(out),
-                            reinterpret_cast<int64_t*>(lab_out), B, Cin, H, W, taps, off, z, S(stream)), "gather_batch");
+                            reinterpret_cast<int64_t*>(lab_out), B, Cin, H, W, taps, off, z,
+                            reinterpret_cast<const int64_t*>(static_cast<intptr_t>(cursor)), nrows, S(stream)),
+        "gather_batch");
 }
 
 void pool3(int is_max, int backward, int64_t stream, py::dict d) {
@@ -390,6 +393,7 @@ void adam_pack(int64_t stream, py::dict d) {
   a.wd = (float)F(d, "wd", 0.0); a.grad_scale = (float)F(d, "grad_scale", 1.0);
   a.update = (int)I(d, "update", 1);
   a.inc_step = (int)I(d, "inc_step", 1);
+  a.cursor = P<int64_t>(d, "cursor");
   check(launch_adam_pack(a, P<const OptSeg>(d, "segs"), (int)I(d, "nsegs"), I(d, "nblocks"), S(stream)), "adam_pack");
 }
 
@@ -431,7 +435,8 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("cls_head", &cls_head);
   m.def("gather_batch", &gather_batch, py::arg("X"), py::arg("idx"), py::arg("lab"), py::arg("lab_w"), py::arg("out"),
         py::arg("lab_out"), py::arg("B"), py::arg("Cin"), py::arg("H"), py::arg("W"), py::arg("stream"),
-        py::arg("taps") = 0, py::arg("off") = 0, py::arg("zero") = py::list());
+        py::arg("taps") = 0, py::arg("off") = 0, py::arg("zero") = py::list(), py::arg("cursor") = 0,
+        py::arg("nrows") = 0);
   m.def("pool3", &pool3);
   m.def("wgrad_table", &wgrad_table);
   m.def("wgrad_batched", &wgrad_batched, py::arg("cfg"), py::arg("table"), py::arg("nj"), py::arg("nblocks"),

@@ -253,6 +253,7 @@ struct AdamArgs {
   float b1, b2, eps, wd, grad_scale;
   int update;  // 0: pack only
   int inc_step;  // advance the step counter after the update (0: a partial update -- another launch of the step does)
+  int64_t* cursor;  // optional: the batch-index schedule's cursor (gather_batch), advanced with the step counter
 };
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
@@ -297,6 +298,7 @@ struct ZeroRanges {  // up to 4 16-byte-aligned regions a launch zeroes (gather_
 };
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
                         int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, const ZeroRanges& zero,
+                        const int64_t* cursor, int nrows,
                         hipStream_t st);
 int launch_pool3(int is_max, int backward, const PoolArgs& a, hipStream_t st);
 // synth.hip: on-device synthetic DAS samples (data/synthetic.py physical model, Philox noise)

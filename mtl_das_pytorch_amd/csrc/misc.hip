@@ -22,7 +22,12 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restri
                                                            const int64_t* __restrict__ lab, int lab_w,
                                                            bf16_t* __restrict__ out, int64_t* __restrict__ lab_out,
                                                            int B, int Cin, int H, int W, int taps, int off,
-                                                           ZeroRanges zero) {
+                                                           ZeroRanges zero, const int64_t* __restrict__ cursor,
+                                                           int nrows) {
+  // batch-index schedule (cursor set): this step's indices are row (*cursor mod nrows) of a [nrows][B] table;
+  // the optimizer's step-counter kernel advances the cursor at the end of the step, so no host copy of the
+  // indices precedes each replay
+  if (cursor) idx += (*cursor % nrows) * (int64_t)B;
   {
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, nt = (int64_t)gridDim.x * 256;
     for (int r = 0; r < zero.n; ++r)
@@ -57,13 +62,13 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restri
 
 int launch_gather_batch(const float* X, const int64_t* idx, const int64_t* lab, int lab_w, bf16_t* out,
                         int64_t* lab_out, int B, int Cin, int H, int W, int taps, int off, const ZeroRanges& zero,
-                        hipStream_t st) {
+                        const int64_t* cursor, int nrows, hipStream_t st) {
   if (Cin > 8 || taps > 8 || (taps > 0 && Cin != 1) || (int64_t)B * H * W >= (1ll << 31)) return -2;
   const int64_t M = (int64_t)B * H * W;
   // one pixel per thread (no grid-stride second round: the idx -> X -> store chain is latency-bound)
   int blocks = (int)std::min<int64_t>((M + 255) / 256, 65535);
   hipLaunchKernelGGL(gather_batch_kernel, dim3(blocks), dim3(256), 0, st, X, idx, lab, lab_w, out, lab_out, B, Cin, H, W,
-                     taps, off, zero);
+                     taps, off, zero, cursor, nrows);
   return (int)hipGetLastError();
 }
 

@@ -147,14 +147,17 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamArgs a, const OptSeg
   }
 }
 
-__global__ void step_inc_kernel(float* step) { step[0] += 1.f; }
+__global__ void step_inc_kernel(float* step, int64_t* cursor) {
+  step[0] += 1.f;
+  if (cursor) cursor[0] += 1;  // the next step gathers the next row of the batch-index schedule
+}
 
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st) {
   if (nblocks <= 0 || nblocks >= (1ll << 31)) return -2;
   hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, a, d_segs, ns);
   int rc = (int)hipGetLastError();
   if (rc || !a.update || !a.inc_step) return rc;
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, const_cast<float*>(a.step));
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, const_cast<float*>(a.step), a.cursor);
   return (int)hipGetLastError();
 }
 

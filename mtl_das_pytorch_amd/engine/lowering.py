@@ -362,10 +362,14 @@ class LoweredProgram:
 
     stem_pack = (0, 0)  # (taps, offset) of the gather's vertical tap packing (core.stem_pack_geom)
 
-    def gather_phase(self, X, labels, idx, clear: bool = False) -> Phase:
+    def gather_phase(self, X, labels, idx, clear: bool = False, cursor=None) -> Phase:
         """The batch gather; ``clear``: the same launch also zeroes the arena's zeroed region (what
         ``arena.clear`` does at the start of a training step), unless the guard allocator keeps every zeroed
-        view in its own banded buffer -- then ``arena.clear`` runs first."""
+        view in its own banded buffer -- then ``arena.clear`` runs first.  ``cursor``: ``idx`` is a
+        [nrows][B] batch-index schedule and the gather takes row ``cursor`` mod nrows (the optimizer's
+        step-counter kernel advances the cursor: set_step_cursor)."""
+        if cursor is not None and (idx.dim() != 2 or idx.shape[1] != self.B):
+            raise ValueError(f"index schedule must be [nrows][{self.B}], got {tuple(idx.shape)}")
         ph = Phase("gather")
         if self.stem_pack[0] and X.shape[1] != 1:
             raise ValueError("stem tap packing needs a single-channel input")
@@ -376,7 +380,7 @@ class LoweredProgram:
                 ph.add("clear", lambda st: self.arena.clear())
                 zero = []
         ph.add("gather", k_gather, X, idx, labels, self.label_width, self.x, self.labels, self.B, X.shape[1], self.H0,
-               self.W0, *self.stem_pack, zero)
+               self.W0, *self.stem_pack, zero, cursor)
         return ph
 
     def _wgfin_args(self, convs=None):
@@ -865,6 +869,20 @@ class LoweredProgram:
         upd = Phase("adam")
         upd.add("adam_pack", k_adam, dict(self._opt_base, update=1, **self._opt_hparams))
         self.opt["adam"] = upd
+        self.set_step_cursor(getattr(self, "_step_cursor", None))
+
+    def set_step_cursor(self, cursor: Optional[torch.Tensor]):
+        """The device int64 cursor of a batch-index schedule (gather_phase ``cursor``): the optimizer's
+        step-counter kernel advances it together with the Adam step count (csrc/optim.hip step_inc_kernel),
+        at the end of the training step, after every gather block has read it.  None detaches it."""
+        self._step_cursor = cursor
+        for l in self.opt["adam"].launches:
+            if l.name == "adam_pack":
+                d = l.args[0]
+                if cursor is None:
+                    d.pop("cursor", None)
+                else:
+                    d["cursor"] = cursor.data_ptr()
 
     # -------------------------------------------------------------------------------------------
     def num_launches(self) -> dict:

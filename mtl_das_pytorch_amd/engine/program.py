@@ -364,6 +364,9 @@ def k_allreduce(fn, t, st):
     fn(t.t if hasattr(t, "bind") else t)  # arena LazyView -> its bound tensor
 
 
-def k_gather(X, idx, lab, lab_w, out, lab_out, B, Cin, H, W, taps, off, zero, st):
+def k_gather(X, idx, lab, lab_w, out, lab_out, B, Cin, H, W, taps, off, zero, cursor, st):
+    """``cursor``: None, or the device int64 cursor of a [nrows][B] batch-index schedule ``idx`` (StepRunner
+    set_index_schedule): the kernel gathers row cursor mod nrows."""
     lib().gather_batch(X.data_ptr(), idx.data_ptr(), lab.data_ptr(), lab_w, out.data_ptr(), lab_out.data_ptr(),
-                       B, Cin, H, W, st, taps, off, zero)
+                       B, Cin, H, W, st, taps, off, zero, cursor.data_ptr() if cursor is not None else 0,
+                       idx.shape[0] if cursor is not None else 0)

@@ -101,12 +101,32 @@ class StepRunner:
             raise ValueError("data-parallel step with weight updates inside the backward: call "
                              "set_optimizer(data_parallel=True) before autotune_program")
         self.buckets = list(getattr(program, "buckets", None) or [(0, program.flat.numel)])
+        self.schedule = None  # [nrows][B] batch-index schedule (set_index_schedule)
+        self.cursor = None
+
+    def set_index_schedule(self, schedule: Optional[torch.Tensor]):
+        """Train from a device-resident [nrows][B] batch-index schedule: ``train_step()`` without indices then
+        gathers row (cursor mod nrows) and the step's optimizer kernel advances the cursor, so a replay is not
+        preceded by a host-issued index copy (A: 6 us per step, tools/step_overhead.py).  The cursor restarts at
+        row 0; None returns to per-call indices.  The training graphs are re-captured."""
+        for kind in [k for k in self.graphs if k.startswith("train")]:
+            self._drop_graph(kind)
+        if schedule is None:
+            self.schedule = self.cursor = None
+            self.p.set_step_cursor(None)
+            return
+        if schedule.dim() != 2 or schedule.shape[1] != self.p.B or schedule.dtype != torch.int64:
+            raise ValueError(f"index schedule must be int64 [nrows][{self.p.B}]")
+        self.schedule = schedule.to(self.p.device).contiguous()
+        self.cursor = torch.zeros(1, dtype=torch.int64, device=self.p.device)
+        self.p.set_step_cursor(self.cursor)
 
     # -------------------------------------------------------------------------------------------
     def _mutable_state(self) -> List[torch.Tensor]:
         f = self.p.flat
-        return [f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step, self.p.metrics,
-                self.p.confusion, self.p.logp] + list(getattr(self.p, "extra_state", []))
+        return ([f.params, f.grads, f.exp_avg, f.exp_avg_sq, f.bn_mean, f.bn_var, f.bn_nbt, f.step, self.p.metrics,
+                 self.p.confusion, self.p.logp] + list(getattr(self.p, "extra_state", []))
+                + ([self.cursor] if self.cursor is not None else []))
 
     def pack_weights(self):
         """(Re)build the bf16 MFMA weight images from the fp32 masters (after init / load_state_dict)."""
@@ -123,7 +143,9 @@ class StepRunner:
         p = self.p
         X, lab = self.sources["train" if kind.startswith("train") else "eval"]
         # a training step's gather also zeroes the arena's accumulators (one launch; arena.clear otherwise)
-        gather = p.gather_phase(X, lab, self.idx, clear=kind.startswith("train"))
+        sched = self.schedule is not None and kind.startswith("train")
+        gather = p.gather_phase(X, lab, self.schedule if sched else self.idx, clear=kind.startswith("train"),
+                                cursor=self.cursor if sched else None)
         if kind.startswith("train_piece"):
             k = int(kind[len("train_piece"):])
             pieces = self._pieces()
@@ -200,10 +222,17 @@ class StepRunner:
     def set_lr(self, lr: float):
         self.p.flat.lr.fill_(float(lr))
 
-    def train_step(self, idx: torch.Tensor):
+    def train_step(self, idx: Optional[torch.Tensor] = None):
+        """One training step on the batch ``idx`` -- or, with an index schedule set (set_index_schedule) and
+        no ``idx``, on the schedule's next row."""
         if not self._packed:
             self.pack_weights()
-        self.idx.copy_(idx, non_blocking=True)
+        if idx is not None:
+            if self.schedule is not None:
+                raise ValueError("an index schedule is set: call train_step() without indices")
+            self.idx.copy_(idx, non_blocking=True)
+        elif self.schedule is None:
+            raise ValueError("train_step() without indices needs set_index_schedule")
         if self.allreduce is None:
             self._run("train_full")
         elif self.capture_dp:

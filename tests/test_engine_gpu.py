@@ -374,3 +374,49 @@ def test_early_adam_matches_optimizer_phase(model_name, monkeypatch):
                    + [c.wf.clone() for c in prog.convs] + [c.wd.clone() for c in prog.convs])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
+def test_index_schedule_matches_per_step_indices(model_name):
+    """StepRunner.set_index_schedule: steps that gather the next row of a device-resident [nrows][B] index table
+    (cursor advanced by the optimizer's step-counter kernel) train exactly like steps handed the same indices
+    one by one -- bitwise equal weights and moments after more steps than the table has rows, equal metric
+    counts (the loss sums are fp32 atomics over blocks: order-dependent in the last bits, also between two
+    runs of the same path)."""
+    from mtl_das_pytorch_amd.data.synthetic import generate
+    from mtl_das_pytorch_amd.engine.step import StepRunner
+    from mtl_das_pytorch_amd.engine.tune import autotune_program
+    from mtl_das_pytorch_amd.models import build_model, encode_joint
+    X, d, e = generate(64, seed=4, device="cuda")
+    joint = model_name == "multi_classifier"
+    lab = encode_joint(d, e) if joint else torch.stack([d, e], 1)
+    sched = torch.randperm(64, device="cuda")[:24].view(3, 8)
+    out = []
+    for use_sched in (False, True):
+        torch.manual_seed(0)
+        m = build_model(model_name)
+        if joint:
+            from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+            prog = InceptionProgram(m, 8, "cuda", p_drop=0.0)
+        else:
+            from mtl_das_pytorch_amd.engine.mtl import MTLProgram
+            prog = MTLProgram(m, 8, "cuda")
+        prog.set_optimizer(weight_decay=1e-5)
+        autotune_program(prog, measure=False)
+        r = StepRunner(prog, X, lab)
+        r.set_lr(1e-3)
+        if use_sched:
+            r.set_index_schedule(sched)
+        for i in range(5):
+            r.train_step() if use_sched else r.train_step(sched[i % 3])
+        torch.cuda.synchronize()
+        f = prog.flat
+        out.append([f.params.clone(), f.exp_avg.clone(), f.exp_avg_sq.clone(), prog.metrics.clone()])
+        if use_sched:
+            assert int(r.cursor.item()) == 5
+        r.close()
+    for a, b in zip(out[0][:3], out[1][:3]):
+        assert torch.equal(a, b)
+    ma, mb = out[0][3], out[1][3]
+    assert torch.equal(ma[:, 1:3], mb[:, 1:3])  # correct / count
+    assert torch.allclose(ma, mb, rtol=1e-5, atol=1e-4)
