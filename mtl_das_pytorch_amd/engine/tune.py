@@ -364,6 +364,7 @@ def tune_wgrad_in_step(make_prog, X: torch.Tensor, labels: torch.Tensor, cache: 
         torch.cuda.empty_cache()
         return t
 
+    start = {sig: cache.get(sig) for sig in order}
     t0 = step_with({})
     for sig in order:
         cur = cache.get(sig)
@@ -376,6 +377,25 @@ def tune_wgrad_in_step(make_prog, X: torch.Tensor, labels: torch.Tensor, cache: 
                 cache[sig] = c
                 if verbose:
                     print(f"  {sig}: wgrad cfg {cur} -> {c}, step {t:.1f} us (incumbent {t_inc:.1f})", flush=True)
+    changed = {sig: cache[sig] for sig in order if cache.get(sig) != start[sig]}
+    if changed:
+        # closing confirmation, as in tune_in_context: the accepted set against the starting one, interleaved;
+        # a set that does not win 2 of 3 rounds is drift of the per-candidate re-timings -- revert it
+        back = {sig: start[sig] for sig in changed if start[sig] is not None}
+        wins = 0
+        for _ in range(3):
+            ts, tt = step_with(back), step_with({})
+            wins += tt < ts
+            if verbose:
+                print(f"  confirmation: start configs {ts:.1f} us, tuned {tt:.1f} us", flush=True)
+        if wins < 2:
+            for sig in changed:
+                if start[sig] is None:
+                    cache.pop(sig, None)
+                else:
+                    cache[sig] = start[sig]
+            if verbose:
+                print(f"weight gradients in the step: {len(changed)} changes not confirmed -- reverted", flush=True)
     if verbose:
         print(f"weight gradients in the step: {t0:.1f} -> {step_with({}):.1f} us", flush=True)
     return cache
