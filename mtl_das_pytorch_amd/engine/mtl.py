@@ -47,6 +47,13 @@ class MTLProgram(LoweredProgram):
     # instead of 3: A 35,502 -> 35,700 (4 pairs), B_event 37,784 -> 38,246 (2 pairs); all streams at 2: A
     # 35,676, B 38,112 (docs/PERF.md round 5)
     WGRAD_MAX_BATCHES_S0 = 2
+    # normalise-on-load only for consumer convs of at most this many output pixels: the 33x83 convs (87,648
+    # px at batch 32) read a materialised BN+ReLU output instead -- the im2col's KH*KW-fold on-load transform
+    # costs them more than the tail launch it saves.  Large-tile weight-gradient splits of >= 2048 pixels
+    # (fewer split slabs for the finalize).  Together A +0.45 % (3 of 4 interleaved pairs), B_distance +1 %
+    # (docs/PERF.md round 5); Model C keeps its own values (its weight gradients lose 0.9 % at 2048)
+    NOL_MAX_PX = 60000
+    WGRAD_MIN_SPLIT_PX_BIG = 2048
     # the last level's attention product sigmoid(BN(y)) * F8 is computed on load by the head kernel
     # (csrc/head.hip MASK): its SIGMUL tail launch leaves the end-of-forward critical path
     HEAD_MASK = False
@@ -198,6 +205,11 @@ class MTLProgram(LoweredProgram):
         self.nvalid = torch.full((1,), B, device=self.device, dtype=torch.int64)
         self.convs: List[ConvLayer] = self._backbone_convs() + \
                                       [L[k] for L in self.levels for k in ("c0", "c3", "co") if k in L]
+        if self.WGRAD_MIN_SPLIT_PX_BIG < ConvLayer.MIN_SPLIT_PX_BIG:  # the slabs are sized for the default
+            raise ValueError("WGRAD_MIN_SPLIT_PX_BIG below ConvLayer.MIN_SPLIT_PX_BIG")
+        for c in self.convs:
+            c.MIN_SPLIT_PX_BIG = self.WGRAD_MIN_SPLIT_PX_BIG
+            c.set_wgrad_cfg(c.wcfg)
 
     @staticmethod
     def hfuse_enabled() -> bool:

@@ -199,6 +199,7 @@ def _force_big_wgrad(prog):
             if l.owner.wgrad_valid(c):
                 l.owner.set_wgrad_cfg(c)
                 l.args = (c,) + tuple(l.args[1:])
+    prog.refresh_wgrad_finalize()  # the split counts changed with the configs (as autotune_program does)
     return i
 
 
