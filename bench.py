@@ -11,12 +11,21 @@ reference architecture; data is synthetic DAS time-space matrices of the paper's
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+``--gpus N > 1`` without a launcher (no WORLD_SIZE in the environment) starts the N rank processes itself
+(``_self_launch``: child processes, one per GPU, rendezvous on 127.0.0.1, before anything touches the GPU)
+and exits with the first failing rank's status; under torchrun each process is one rank.
+
 Weak scaling: per-GPU batch fixed at 32, global batch 32*N.  Rank 0 prints one JSON line; the time is
 the max over ranks of K steps bracketed by barrier + device synchronize.
+
+Without a GPU (CPU container, tests) the same contract runs the reference-math fp32 PyTorch step over gloo
+(``_cpu_bench``): it checks the launch / rendezvous / one-JSON-line plumbing, not performance.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -43,6 +52,105 @@ def _accs(m, joint):
     return {"distance": round(float(m[0, 1] / m[0, 2]), 4), "event": round(float(m[-1, 1] / m[-1, 2]), 4)}
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(n: int) -> int:
+    """Run this script as ``n`` rank processes (RANK = LOCAL_RANK = i, WORLD_SIZE = n, rendezvous on
+    127.0.0.1) and return the first non-zero exit status (0 if every rank succeeded).  The parent never
+    imports torch or touches the GPU: the ranks are fresh interpreters, not forks of a HIP process.  When a
+    rank fails the others are terminated, so a dead peer cannot leave the rest waiting in a collective."""
+    port = _free_port()
+    procs = []
+    for i in range(n):
+        env = dict(os.environ, RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc
+
+
+def _cpu_bench(args, ctx):
+    """The bench contract without a GPU: the reference-math fp32 PyTorch training step (forward, the model's
+    losses, backward, gradient all-reduce over gloo with 1/world averaging, torch Adam) on synthetic data,
+    K timed steps, rank 0 prints one JSON line.  Plumbing only (multi-process launch, rendezvous, timing,
+    the JSON contract): the numbers say nothing about MI355X."""
+    import torch
+    import torch.nn.functional as F
+    from mtl_das_pytorch_amd.data.synthetic import generate
+    from mtl_das_pytorch_amd.models import build_model, encode_joint
+    from mtl_das_pytorch_amd.parallel.dist import FlatGradAllReducer, broadcast_module_state
+
+    torch.set_num_threads(max(1, (os.cpu_count() or 1) // ctx.world))  # the ranks share the host's cores
+    torch.manual_seed(1234)
+    model = build_model(args.model, in_channels=args.in_channels)
+    with torch.no_grad():
+        broadcast_module_state(ctx, list(model.parameters()) + list(model.buffers()))
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3 / 1.5, weight_decay=1e-5)
+    n = max(args.batch, min(args.dataset_size, 4 * args.batch))
+    X, d, e = generate(n, seed=1000 + ctx.rank, in_channels=args.in_channels)
+    joint = args.model == "multi_classifier"
+    red = FlatGradAllReducer(ctx)
+    g = torch.Generator().manual_seed(7 + ctx.rank)
+
+    def step():
+        idx = torch.randint(0, n, (args.batch,), generator=g)
+        out = model(X[idx])
+        if joint:
+            loss = F.cross_entropy(out[0] if isinstance(out, tuple) else out, encode_joint(d[idx], e[idx]))
+        elif args.model == "MTL":
+            loss = F.nll_loss(out[0], d[idx]) + F.nll_loss(out[1], e[idx])
+        else:
+            loss = F.nll_loss(out, d[idx] if args.model == "single_distance" else e[idx])
+        opt.zero_grad(set_to_none=False)
+        loss.backward()
+        params = [p for p in model.parameters() if p.grad is not None]
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        red(flat)
+        flat /= ctx.world
+        o = 0
+        for p in params:
+            p.grad.copy_(flat[o:o + p.numel()].view_as(p))
+            o += p.numel()
+        opt.step()
+
+    model.train()
+    for _ in range(args.warmup):
+        step()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.barrier()
+    dt = ctx.max_scalar(time.perf_counter() - t0)
+    value = ctx.world * args.batch * args.steps / dt
+    return {
+        "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": ctx.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": round(value / BASELINE_VALUE, 3), "dtype": "fp32",
+        "data": f"synthetic (DAS time-space matrices {args.in_channels}x100x250, random-init weights)",
+        "config": {"model": MODEL_NAMES.get(args.model, args.model), "global_batch": args.batch * ctx.world,
+                   "seq_len": 250, "input_shape": [args.in_channels, 100, 250], "parallelism": f"dp{ctx.world}"},
+        "device": "cpu", "engine": "torch-eager fp32 (no GPU: launch / rendezvous plumbing only)",
+        "dist_backend": ctx.backend,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,6 +175,13 @@ def main():
                          "the all-reduce, and the world > 1 collective path (per-bucket piece graphs, async RCCL)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args.gpus))
+    # HIP graph executor streams (read by the runtime when it initialises, i.e. before the first HIP call):
+    # the engine's latency-bound steps run best on 2 (docs/PERF.md round 5); an explicit setting wins
+    from mtl_das_pytorch_amd import use_engine_graph_queues
+    graph_queues = use_engine_graph_queues()
+
     import torch
     import torch.distributed as dist
     from mtl_das_pytorch_amd.data.synthetic import generate
@@ -85,6 +200,12 @@ def main():
     ctx = init_distributed()
     world = ctx.world
     dev = ctx.device
+    if dev.type != "cuda":
+        out = _cpu_bench(args, ctx)
+        if ctx.is_main:
+            print(json.dumps(out), flush=True)
+        shutdown(ctx)
+        return
     torch.manual_seed(1234)  # identical init on every rank (then broadcast for certainty)
     model = build_model(args.model, in_channels=args.in_channels)
     joint = args.model == "multi_classifier"
@@ -179,6 +300,7 @@ def main():
         "vs_eager_pytorch_mi355x": (round(value / (EAGER_BY_MODEL[args.model] * world), 3)
                                     if args.model in EAGER_BY_MODEL else None),
         "hip_graph": runner.use_graph,
+        "hip_graph_executor_streams": int(graph_queues),  # DEBUG_HIP_FORCE_GRAPH_QUEUES in effect at HIP init
         "sync_bn": sync,
         "sync_bn_collectives_per_step": n_sync if sync else 0,
         "grad_buckets_mb": [round((hi - lo) * 4 / 2 ** 20, 2) for lo, hi in buckets],

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--out", default="predictions.csv")
     args = ap.parse_args()
 
+    from mtl_das_pytorch_amd import use_engine_graph_queues
+    use_engine_graph_queues()  # before the first HIP call
     import numpy as np
     import torch
     from mtl_das_pytorch_amd.data.mat_dataset import load_mat

@@ -150,8 +150,11 @@ def config_from_args(args: argparse.Namespace, is_test: bool) -> TrainConfig:
 def apply_debug_env(argv) -> None:
     """--debug must take effect before the HIP runtime initialises: called by train.py / test.py before
     importing torch.  Serialised kernels + blocking launches make a faulting kernel report at its own
-    launch."""
+    launch.  Also selects the engine's HIP graph executor stream count for the process
+    (mtl_das_pytorch_amd.use_engine_graph_queues)."""
     import os
+    from .. import use_engine_graph_queues
+    use_engine_graph_queues()
     for i, a in enumerate(argv):
         val = a.split("=", 1)[1] if a.startswith("--debug=") else (argv[i + 1] if a == "--debug" and i + 1 < len(argv) else None)
         if val is not None and str2bool(val):

@@ -4,7 +4,9 @@ import sys
 import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import mtl_das_pytorch_amd  # noqa: E402,F401  (its HIP runtime settings precede the first HIP call)
+import mtl_das_pytorch_amd  # noqa: E402
+
+mtl_das_pytorch_amd.use_engine_graph_queues()  # the GPU suites run the executor setting the entry points use
 
 
 def pytest_configure(config):
