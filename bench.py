@@ -190,8 +190,8 @@ def main():
     from mtl_das_pytorch_amd.engine.step import StepRunner
     from mtl_das_pytorch_amd.engine.tune import autotune_program
     from mtl_das_pytorch_amd.models import build_model, encode_joint
-    from mtl_das_pytorch_amd.parallel.dist import (FlatGradAllReducer, ShardedIndexSampler,
-                                                   broadcast_module_state, init_distributed, shutdown)
+    from mtl_das_pytorch_amd.parallel.dist import (FlatGradAllReducer, ShardedIndexSampler, broadcast_module_state,
+                                                   calibrate_allreduce, init_distributed, shutdown)
 
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws != args.gpus:  # fail before touching the GPU: a mislaunch would report the wrong n_gpus
@@ -219,14 +219,22 @@ def main():
                        data_parallel=ctx.enabled or args.dp_shape > 1)
     if hasattr(prog, "set_rng_stream"):  # Model C dropout: an independent mask stream per rank
         prog.set_rng_stream(0, ctx.rank)
-    # DP: gradient buckets whose all-reduces overlap the rest of the backward (engine/step.py)
-    # (--buckets K on one GPU runs the same split graphs with no-op collectives: measures the split's cost)
+    # DP: gradient buckets whose all-reduces overlap the rest of the backward (engine/step.py), sized from the
+    # all-reduce time of the whole flat gradient on the live group (a 1-rank rehearsal of N ranks, --dp-shape,
+    # cannot measure N's all-reduce: it takes the model's default bucket count)
+    # (--buckets K on one GPU runs the same bucketed graph with no-op collectives: measures the split's cost)
     shape = max(world, args.dp_shape)
     captured = ctx.capturable_collectives and args.dp_shape <= 1  # the form the step's collectives take
-    nb = prog.dp_buckets(shape, captured) if args.buckets is None else args.buckets
-    buckets = prog.segment_backward(nb)
+    ar_ms = calibrate_allreduce(ctx, prog.flat.numel)
+    nb = prog.dp_buckets(shape, ar_ms if world > 1 else None) if args.buckets is None else args.buckets
+    # captured collectives: the backward cut at the bucket boundaries (segment_backward); eager RCCL behind the
+    # graph's external events (the multi-rank default): buckets completed by side streams, no cut (stream_buckets)
+    ext_form = not captured and (ctx.enabled or nb > 1)
+    buckets = prog.segment_backward(1 if ext_form else nb)
     autotune_program(prog, out_path=os.path.join("gpurun_out", "tuned_cfgs.json") if ctx.is_main else None,
                      measure=not args.no_tune)
+    if ext_form and nb > 1:
+        buckets = prog.stream_buckets(nb)
     f = prog.flat
     broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
     X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev, in_channels=args.in_channels)
@@ -307,7 +315,10 @@ def main():
         "dist_backend": ctx.backend,
         "dp_shape": shape,
         "captured_collectives": runner.capture_dp,
-        **({"restream": runner.restream_info} if runner.restream_info else {}),
+        # how the bucket all-reduces overlap the backward: captured in the step graph, or eager RCCL behind the
+        # graph's external bucket events (the multi-rank default)
+        "dp_overlap": "captured" if runner.capture_dp else ("ext_events" if runner.ext_dp else None),
+        "allreduce_ms": None if ar_ms is None else round(ar_ms, 4),
         "rccl_ranks": dist.get_world_size() if ctx.backend == "nccl" else 0,
         "baseline_note": "vs_baseline divides by BASELINE.md's 176.1 samples/s (reference on CPU, the only "
                          "throughput number it has); vs_eager_pytorch_mi355x divides by the reference-style "

@@ -201,9 +201,9 @@ py::tuple wgrad_table(int cfg, py::list dicts, py::list groups) {
   return py::make_tuple(py::bytes(reinterpret_cast<const char*>(jobs.data()), jobs.size() * sizeof(WgradJob)), b0);
 }
 
-void wgrad_batched(int cfg, int64_t table, int nj, int64_t nblocks, int64_t stream, int64_t cap, int xcd) {
+void wgrad_batched(int cfg, int64_t table, int nj, int64_t nblocks, int64_t stream, int64_t cap) {
   check(launch_wgrad_batched(cfg, reinterpret_cast<const WgradJob*>(static_cast<intptr_t>(table)), nj, nblocks,
-                             S(stream), cap, xcd), "wgrad_batched");
+                             S(stream), cap), "wgrad_batched");
 }
 
 WgradArgs parse_wgrad(const py::dict& d) {
@@ -310,10 +310,6 @@ void mtl_head(int64_t stream, py::dict d) {
   a.logp = P<float>(d, "logp"); a.dfeat = P<bf16_t>(d, "dfeat"); a.dgs = I(d, "dgs");
   a.metrics = P<float>(d, "metrics"); a.confusion = P<int>(d, "confusion");
   a.nvalid = P<const int64_t>(d, "nvalid");
-  if (d.contains("my") && !d["my"].is_none()) {
-    a.my = P<const bf16_t>(d, "my"); a.mygs = I(d, "mygs"); a.ldmy = (int)I(d, "ldmy");
-    a.mbn = parse_bn(d["mbn"].cast<py::dict>());
-  }
   check(launch_mtl_head(a, S(stream)), "mtl_head");
 }
 
@@ -440,7 +436,7 @@ PYBIND11_MODULE(_mda_hip, m) {
   m.def("pool3", &pool3);
   m.def("wgrad_table", &wgrad_table);
   m.def("wgrad_batched", &wgrad_batched, py::arg("cfg"), py::arg("table"), py::arg("nj"), py::arg("nblocks"),
-        py::arg("stream"), py::arg("cap") = 0, py::arg("xcd") = 0);
+        py::arg("stream"), py::arg("cap") = 0);
   m.def("grad_sum", &grad_sum);
   m.def("synth_das", &synth_das);
   m.def("philox_kat", [](int64_t ctr, uint64_t key, int64_t out, int n, int64_t stream) {
@@ -460,117 +456,42 @@ PYBIND11_MODULE(_mda_hip, m) {
     return static_cast<int64_t>(reinterpret_cast<intptr_t>(s));
   });
   m.def("stream_destroy", [](int64_t s) { check((int)hipStreamDestroy(S(s)), "hipStreamDestroy"); });
+  // events recorded as EXTERNAL event-record nodes when the stream is capturing (hipEventRecordExternal):
+  // the host orders work issued after a graph launch behind a point inside the graph (engine/step.py, the
+  // world > 1 data-parallel step; torch.cuda.Event(external=True) is refused on ROCm builds of PyTorch)
+  m.def("event_create", []() {
+    hipEvent_t e = nullptr;
+    check((int)hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreateWithFlags");
+    return static_cast<int64_t>(reinterpret_cast<intptr_t>(e));
+  });
+  m.def("event_destroy", [](int64_t e) {
+    check((int)hipEventDestroy(reinterpret_cast<hipEvent_t>(static_cast<intptr_t>(e))), "hipEventDestroy");
+  });
+  m.def("event_record_external", [](int64_t e, int64_t stream) {
+    hipEvent_t ev = reinterpret_cast<hipEvent_t>(static_cast<intptr_t>(e));
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    check((int)hipStreamGetCaptureInfo_v2(S(stream), &st, nullptr, &g, &deps, &nd), "hipStreamGetCaptureInfo_v2");
+    if (st != hipStreamCaptureStatusActive) {
+      check((int)hipEventRecord(ev, S(stream)), "hipEventRecord");
+      return;
+    }
+    // capturing: an explicit event-record node after the stream's current tail, which becomes the new tail
+    hipGraphNode_t node = nullptr;
+    check((int)hipGraphAddEventRecordNode(&node, g, deps, nd, ev), "hipGraphAddEventRecordNode");
+    check((int)hipStreamUpdateCaptureDependencies(S(stream), &node, 1, hipStreamSetCaptureDependencies),
+          "hipStreamUpdateCaptureDependencies");
+  });
+  m.def("stream_wait_event", [](int64_t stream, int64_t e) {
+    check((int)hipStreamWaitEvent(S(stream), reinterpret_cast<hipEvent_t>(static_cast<intptr_t>(e)), 0),
+          "hipStreamWaitEvent");
+  });
   m.def("stream_priority_range", []() {
     int least = 0, greatest = 0;
     check((int)hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
     return py::make_tuple(least, greatest);
-  });
-  // ---- captured-graph surgery (engine/graphsched.py): read a capture's DAG, rewrite its edge order ----
-  // the graph a stream is capturing into, and the node count so far (0, 0 when not capturing)
-  m.def("capture_graph_count", [](int64_t stream) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    hipGraph_t g = nullptr;
-    check((int)hipStreamGetCaptureInfo_v2(S(stream), &st, nullptr, &g, nullptr, nullptr), "hipStreamGetCaptureInfo_v2");
-    if (st != hipStreamCaptureStatusActive || g == nullptr) return py::make_tuple((int64_t)0, (int64_t)0);
-    size_t n = 0;
-    check((int)hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
-    return py::make_tuple(static_cast<int64_t>(reinterpret_cast<intptr_t>(g)), (int64_t)n);
-  });
-  // the last node(s) a capturing stream's next node will depend on
-  m.def("capture_tail", [](int64_t stream) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    const hipGraphNode_t* deps = nullptr;
-    size_t nd = 0;
-    check((int)hipStreamGetCaptureInfo_v2(S(stream), &st, nullptr, nullptr, &deps, &nd), "hipStreamGetCaptureInfo_v2");
-    py::list out;
-    for (size_t i = 0; i < nd; ++i) out.append(static_cast<int64_t>(reinterpret_cast<intptr_t>(deps[i])));
-    return out;
-  });
-  // which logical (engine) stream created each node of a capture: note() after every launch tags the
-  // nodes that appeared since the previous note with that launch's target stream
-  struct CaptureTracker {
-    std::unordered_map<hipGraphNode_t, int> tag;
-    void note(int64_t stream, int target) {
-      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-      hipGraph_t g = nullptr;
-      check((int)hipStreamGetCaptureInfo_v2(S(stream), &st, nullptr, &g, nullptr, nullptr), "hipStreamGetCaptureInfo_v2");
-      if (st != hipStreamCaptureStatusActive || g == nullptr) return;
-      size_t n = 0;
-      check((int)hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
-      if (n == tag.size()) return;
-      std::vector<hipGraphNode_t> nodes(n);
-      check((int)hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
-      for (auto x : nodes) tag.emplace(x, target);  // only inserts the new ones
-    }
-    py::list targets(int64_t graph) const {
-      hipGraph_t g = reinterpret_cast<hipGraph_t>(static_cast<intptr_t>(graph));
-      size_t n = 0;
-      check((int)hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
-      std::vector<hipGraphNode_t> nodes(n);
-      check((int)hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
-      py::list out;
-      for (auto x : nodes) {
-        auto it = tag.find(x);
-        if (it == tag.end()) out.append(py::none()); else out.append(it->second);
-      }
-      return out;
-    }
-  };
-  py::class_<CaptureTracker>(m, "CaptureTracker")
-      .def(py::init<>())
-      .def("note", &CaptureTracker::note)
-      .def("targets", &CaptureTracker::targets)
-      .def("size", [](const CaptureTracker& t) { return t.tag.size(); });
-  // nodes (runtime order) and, per node, its children in edge-insertion order as node indices
-  m.def("graph_structure", [](int64_t graph) {
-    hipGraph_t g = reinterpret_cast<hipGraph_t>(static_cast<intptr_t>(graph));
-    size_t n = 0;
-    check((int)hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
-    std::vector<hipGraphNode_t> nodes(n);
-    check((int)hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
-    py::list handles, children;
-    std::vector<std::pair<hipGraphNode_t, int64_t>> idx;
-    idx.reserve(n);
-    for (size_t i = 0; i < n; ++i) idx.emplace_back(nodes[i], (int64_t)i);
-    std::sort(idx.begin(), idx.end());
-    auto find = [&](hipGraphNode_t x) {
-      auto it = std::lower_bound(idx.begin(), idx.end(), std::make_pair(x, (int64_t)-1));
-      if (it == idx.end() || it->first != x) throw std::runtime_error("graph_structure: unknown node");
-      return it->second;
-    };
-    for (size_t i = 0; i < n; ++i) {
-      handles.append(static_cast<int64_t>(reinterpret_cast<intptr_t>(nodes[i])));
-      size_t nc = 0;
-      check((int)hipGraphNodeGetDependentNodes(nodes[i], nullptr, &nc), "hipGraphNodeGetDependentNodes");
-      std::vector<hipGraphNode_t> ch(nc);
-      if (nc) check((int)hipGraphNodeGetDependentNodes(nodes[i], ch.data(), &nc), "hipGraphNodeGetDependentNodes");
-      py::list row;
-      for (size_t j = 0; j < nc; ++j) row.append(find(ch[j]));
-      children.append(row);
-    }
-    return py::make_tuple(handles, children);
-  });
-  // replace every edge of the graph by ``children`` (per node index, in the wanted insertion order)
-  m.def("graph_set_children", [](int64_t graph, py::list children) {
-    hipGraph_t g = reinterpret_cast<hipGraph_t>(static_cast<intptr_t>(graph));
-    size_t n = 0;
-    check((int)hipGraphGetNodes(g, nullptr, &n), "hipGraphGetNodes");
-    std::vector<hipGraphNode_t> nodes(n);
-    check((int)hipGraphGetNodes(g, nodes.data(), &n), "hipGraphGetNodes");
-    if ((size_t)children.size() != n) throw std::runtime_error("graph_set_children: node count mismatch");
-    size_t ne = 0;
-    check((int)hipGraphGetEdges(g, nullptr, nullptr, &ne), "hipGraphGetEdges");
-    std::vector<hipGraphNode_t> from(ne), to(ne);
-    if (ne) {
-      check((int)hipGraphGetEdges(g, from.data(), to.data(), &ne), "hipGraphGetEdges");
-      check((int)hipGraphRemoveDependencies(g, from.data(), to.data(), ne), "hipGraphRemoveDependencies");
-    }
-    for (size_t i = 0; i < n; ++i) {
-      for (auto c : py::list(children[i])) {
-        hipGraphNode_t a = nodes[i], b = nodes[c.cast<size_t>()];
-        check((int)hipGraphAddDependencies(g, &a, &b, 1), "hipGraphAddDependencies");
-      }
-    }
   });
   register_matio(m);
 }

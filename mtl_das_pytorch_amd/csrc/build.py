@@ -1,8 +1,8 @@
 """Builds the in-tree HIP extension ``mtl_das_pytorch_amd/_mda_hip*.so`` with hipcc for gfx950 only.
 
 No torch C++ headers and no hipify step: the kernels are plain HIP C++ and the bindings use pybind11,
-so a full rebuild takes a few seconds per translation unit.  Objects are compiled in parallel and
-only rebuilt when a source or header is newer than the shared object.
+so a full rebuild takes a few seconds per translation unit.  Objects are compiled in parallel; a
+translation unit is recompiled when it or any header is newer than its object (``--force``: all of them).
 
     python -m mtl_das_pytorch_amd.csrc.build [--force] [--debug]
 """
@@ -53,8 +53,13 @@ def build(force: bool = False, debug: bool = False, verbose: bool = True, jobs: 
     if debug:
         common += ["-g"]
 
+    headers = glob.glob(os.path.join(HERE, "*.h"))
+    newest_dep = max([os.path.getmtime(h) for h in headers] + [os.path.getmtime(__file__)])
+
     def compile_one(src):
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(src), newest_dep):
+            return obj  # incremental: this translation unit and every header are older than its object
         cmd = [HIPCC] + common + ["-c", src, "-o", obj]
         if src.endswith("bindings.cpp"):
             cmd = [HIPCC] + common + ["-x", "hip", "-c", src, "-o", obj]

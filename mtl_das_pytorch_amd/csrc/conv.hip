@@ -622,22 +622,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 // batch may run on a capped, persistent grid (launch_wgrad_batched ``cap``), so that it never fills every CU
 // slot while the critical data-gradient chain needs blocks (tools/kernel_phases.py: chain kernels waited up
 // to 16 us for their blocks to start beside an uncapped batch).
-// xcd != 0: within every pass of the grid over the virtual blocks, the hardware blocks that share an XCD (b,
-// b + 8, ...) take one contiguous range of virtual blocks (block_coords' order): consecutive virtual blocks
-// are the tiles of one M split and then the neighbouring splits, which read the same dy rows and the same
-// (halo-overlapping) input rows -- through one L2 instead of eight.
-DEV int64_t wgrad_vblock(int64_t vb, int64_t nvb, int xcd) {
-  if (!xcd) return vb;
-  const int64_t base = vb - blockIdx.x;  // first virtual block of this pass
-  const int64_t rem = nvb - base;
-  const unsigned n = (unsigned)(rem < (int64_t)gridDim.x ? rem : (int64_t)gridDim.x);
-  const unsigned b = blockIdx.x, q = n >> 3, r = n & 7, xc = b & 7;
-  return base + xc * q + (xc < r ? xc : r) + (b >> 3);
-}
-
 #define WGRAD_FOR_VBLOCKS(BODY)                                                                            \
-  for (int64_t vb0 = blockIdx.x; vb0 < nvb; vb0 += gridDim.x) {                                           \
-    const int64_t vb = wgrad_vblock(vb0, nvb, xcd);                                                        \
+  for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {                                            \
     int lo = 0, hi = nj - 1;                                                                               \
     while (lo < hi) { int mid = (lo + hi + 1) >> 1; if (jobs[mid].block0 <= vb) lo = mid; else hi = mid - 1; } \
     const WgradJob& J = jobs[lo];                                                                          \
@@ -649,7 +635,7 @@ DEV int64_t wgrad_vblock(int64_t vb, int64_t nvb, int xcd) {
   }
 
 template <int TN, int TK, int MCH>
-__global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob* __restrict__ jobs, int nj, int64_t nvb, int xcd) {
+__global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob* __restrict__ jobs, int nj, int64_t nvb) {
   WGRAD_FOR_VBLOCKS((wgrad_block<TN, TK, MCH>(J.a, r % J.ntiles, r / J.ntiles, z)))
 }
 
@@ -744,7 +730,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_big_kernel(WgradArgs a) {
 }
 
 template <int TN, int TK>
-__global__ __launch_bounds__(256) void conv_wgrad_big_batched_kernel(const WgradJob* __restrict__ jobs, int nj, int64_t nvb, int xcd) {
+__global__ __launch_bounds__(256) void conv_wgrad_big_batched_kernel(const WgradJob* __restrict__ jobs, int nj, int64_t nvb) {
   WGRAD_FOR_VBLOCKS((wgrad_big_block<TN, TK>(J.a, r % J.ntiles, r / J.ntiles, z)))
 }
 
@@ -903,7 +889,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_patch_kernel(WgradArgs a) {
 }
 
 template <int TN, int CB, int W8, int R>
-__global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const WgradJob* __restrict__ jobs, int nj, int64_t nvb, int xcd) {
+__global__ __launch_bounds__(256) void conv_wgrad_patch_batched_kernel(const WgradJob* __restrict__ jobs, int nj, int64_t nvb) {
   WGRAD_FOR_VBLOCKS((wgrad_patch_block<TN, CB, W8, R>(J.a, r % J.ntiles, r / J.ntiles, z)))
 }
 
@@ -1168,13 +1154,12 @@ int wgrad_tile_shape(int cfg, int& TN, int& TK) {
   return 0;
 }
 
-int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st, int64_t cap,
-                         int xcd) {
+int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st, int64_t cap) {
   if (nblocks <= 0) return 0;
   dim3 grid((unsigned)(cap > 0 && cap < nblocks ? cap : nblocks));
   if (cfg >= WGRAD_BIG_CFG0) {
 #define LAUNCH_WGBIGB(TN, TK)                                                                                 \
-  hipLaunchKernelGGL((conv_wgrad_big_batched_kernel<TN, TK>), grid, dim3(256), 0, st, d_jobs, nj, nblocks, xcd); \
+  hipLaunchKernelGGL((conv_wgrad_big_batched_kernel<TN, TK>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \
   break;
     switch (cfg) {
       WGRAD_BIG_CASES(LAUNCH_WGBIGB)
@@ -1185,7 +1170,7 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
   }
   if (cfg >= WGRAD_PATCH_CFG0) {
 #define LAUNCH_WGPB(TN, CB, W8, R)                                                                              \
-  hipLaunchKernelGGL((conv_wgrad_patch_batched_kernel<TN, CB, W8, R>), grid, dim3(256), 0, st, d_jobs, nj, nblocks, xcd); \
+  hipLaunchKernelGGL((conv_wgrad_patch_batched_kernel<TN, CB, W8, R>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \
   break;
     switch (cfg) {
       WGRAD_PATCH_CASES(LAUNCH_WGPB)
@@ -1195,7 +1180,7 @@ int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblock
     return (int)hipGetLastError();
   }
 #define LAUNCH_WGB(TN, TK, MCH)                                                                              \
-  hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, d_jobs, nj, nblocks, xcd); \
+  hipLaunchKernelGGL((conv_wgrad_batched_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \
   break;
   switch (cfg) {
     WGRAD_CFG_CASES(LAUNCH_WGB)

@@ -17,59 +17,32 @@ namespace mda {
 
 // One block per (sample, task): the tasks' dependent chains (GAP -> group mean -> softmax -> gradient)
 // run side by side instead of one after the other, and the label is fetched before the GAP.
-// MASK: the features are sigmoid(BN(my)) * feat, computed on load (HeadArgs::my)
-template <bool MASK>
 __global__ __launch_bounds__(256) void mtl_head_kernel(HeadArgs a) {
   __shared__ float s_gap[256];
   __shared__ float s_part8[2048];  // [256 / (C/8) lanes][C]
   __shared__ float s_logit[16], s_prob[16];
-  __shared__ float s_msc[MASK ? 256 : 1], s_msh[MASK ? 256 : 1];
   __shared__ int s_lab;
   const int b = blockIdx.x, t = blockIdx.y;
   if (threadIdx.x == 0) s_lab = (int)a.labels[(int64_t)b * a.lab_stride + a.lab_off + t];
   const bool valid = a.nvalid == nullptr || b < *a.nvalid;
-  if (MASK) {
-    bn_prepare(a.mbn, t, s_msc, s_msh, nullptr, nullptr, b == 0);
-    __syncthreads();
-  }
   {
     const bf16_t* f = a.feat + a.fgs * t + (int64_t)b * a.HW * a.ldf;
-    const bf16_t* my = MASK ? a.my + a.mygs * t + (int64_t)b * a.HW * a.ldmy : nullptr;
     // GAP: thread -> (8-channel group, pixel lane), 16-byte loads, 4 independent pixels in flight
     const int ng = a.C >> 3, lanes = 256 / ng;
     const int cg = threadIdx.x % ng, pl = threadIdx.x / ng;
     float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float msc[8], msh[8];
-    if (MASK) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { msc[j] = s_msc[cg * 8 + j]; msh[j] = s_msh[cg * 8 + j]; }
-    }
     if (pl < lanes) {
       int p = pl;
       for (; p + 3 * lanes < a.HW; p += 4 * lanes) {
-        float v[4][8], m[4][8];
+        float v[4][8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          load8(f + (int64_t)(p + u * lanes) * a.ldf + cg * 8, v[u]);
-          if (MASK) load8(my + (int64_t)(p + u * lanes) * a.ldmy + cg * 8, m[u]);
-        }
-        if (MASK) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[u][j] *= sigmoidf_(m[u][j] * msc[j] + msh[j]);
-        }
+        for (int u = 0; u < 4; ++u) load8(f + (int64_t)(p + u * lanes) * a.ldf + cg * 8, v[u]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) s8[j] += (v[0][j] + v[1][j]) + (v[2][j] + v[3][j]);
       }
       for (; p < a.HW; p += lanes) {
-        float v[8], m[8];
+        float v[8];
         load8(f + (int64_t)p * a.ldf + cg * 8, v);
-        if (MASK) {
-          load8(my + (int64_t)p * a.ldmy + cg * 8, m);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] *= sigmoidf_(m[j] * msc[j] + msh[j]);
-        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) s8[j] += v[j];
       }
@@ -136,12 +109,7 @@ int launch_mtl_head(const HeadArgs& a, hipStream_t st) {
   if (a.C > 256 || 256 % a.C || a.C % 8 || a.ldf % 8) return -2;
   for (int t = 0; t < a.T; ++t)
     if (a.ncls[t] <= 0 || a.C % a.ncls[t] || (a.C / a.ncls[t]) % 4) return -2;
-  if (a.my) {
-    if (a.mbn.C != a.C || a.ldmy % 8) return -2;
-    hipLaunchKernelGGL(mtl_head_kernel<true>, dim3(a.B, a.T), dim3(256), 0, st, a);
-  } else {
-    hipLaunchKernelGGL(mtl_head_kernel<false>, dim3(a.B, a.T), dim3(256), 0, st, a);
-  }
+  hipLaunchKernelGGL(mtl_head_kernel, dim3(a.B, a.T), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -190,12 +190,6 @@ struct HeadArgs {
   float* metrics;   // [T][4]: loss_sum, correct, count, abs_err_sum
   int* confusion;   // [T][16][16]
   const int64_t* nvalid;  // samples b >= *nvalid are padding: no metrics, no gradient (may be null)
-  // optional (my null = off): the features are the attention product sigmoid(BN(my)) * feat computed on load
-  // -- the last level's SIGMUL tail folded into the head (feat is then the shared feature, fgs 0; my the
-  // mask generator's pre-BN output per task, + t * mygs).  Block (0, t) updates that BN's running statistics
-  // and publishes its constants for the backward, as the tail's block 0 did.
-  const bf16_t* my; int64_t mygs; int ldmy;
-  BNArgs mbn;
 };
 
 struct ClsArgs {
@@ -282,8 +276,7 @@ constexpr int WGRAD_BIG_CFG0 = 32, WGRAD_BIG_NCFG = 4;  // wgrad cfgs 32-35: 32x
 int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8, int& R);
 int wgrad_ntiles(int cfg, const WgradArgs& a);  // tiles per group of a wgrad launch, < 0: cfg invalid for a
 // cap > 0: at most cap hardware blocks walk the nblocks virtual blocks (persistent grid)
-int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st, int64_t cap = 0,
-                         int xcd = 0);
+int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st, int64_t cap = 0);
 int launch_wgrad_finalize(const WgFinDesc* d_descs, int nd, int64_t nblocks, float scale, hipStream_t st);
 int launch_tail_fwd(int kind, const TailArgs& a, int G, int blocks, hipStream_t st);
 int launch_tail_fwd_batched(int kind, const TailJob* d_jobs, int nj, int nblocks, int maxC, hipStream_t st);

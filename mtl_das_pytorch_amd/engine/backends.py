@@ -22,7 +22,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..models import decode_joint, model_tasks
-from ..parallel.dist import DistContext, FlatGradAllReducer, average_, broadcast_module_state, sum_
+from ..parallel.dist import (DistContext, FlatGradAllReducer, average_, broadcast_module_state, calibrate_allreduce,
+                             sum_)
 
 N_DIST, N_EVENT = 16, 2
 
@@ -224,8 +225,14 @@ class EngineBackend(Backend):
                                 data_parallel=ctx.enabled)
         if hasattr(self.prog, "set_rng_stream"):
             self.prog.set_rng_stream(seed, ctx.rank)
-        self.prog.segment_backward(self.prog.dp_buckets(ctx.world, ctx.capturable_collectives))
+        nb = self.prog.dp_buckets(ctx.world, calibrate_allreduce(ctx, self.prog.flat.numel))
+        # captured collectives (a 1-rank RCCL group): the backward cut at the bucket boundaries; several ranks
+        # (eager RCCL behind the step graph's external bucket events): side-stream buckets, no cut
+        ext_form = ctx.enabled and not ctx.capturable_collectives and use_graph
+        self.prog.segment_backward(1 if ext_form else nb)
         autotune_program(self.prog, measure=tune)
+        if ext_form and nb > 1:
+            self.prog.stream_buckets(nb)
         f = self.prog.flat
         broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
         lab_eval = labels_eval if labels_eval is not None else labels

@@ -13,8 +13,11 @@ level branches over the same two (tools/timeline.py queue column).
 
 This module rebuilds the DAG a capture of engine phases produces (the capture semantics of
 ``Phase.run``: per-stream dependency sets, event records / waits, the phase-start fork and phase-end
-joins) and runs the executor's assignment on it, so that an issue order (Phase.ISSUE_ORDER) can be chosen
-on the CPU that makes the executor's streams coincide with the engine's logical streams."""
+joins) and runs the executor's assignment on it: an analysis tool (tools/graph_dot.py, profiles/
+r5_graph_streams.md).  Rewriting a captured graph's edge order so that the executor keeps every engine stream
+on a stream of its own was built in round 5 and measured SLOWER (A -1.7 %, C -7 %: more kernels compete for
+the CUs at once); it was removed, the measurement is in docs/PERF.md.  The engine instead runs with 2 executor
+streams (DEBUG_HIP_FORCE_GRAPH_QUEUES, set by the entry points: mtl_das_pytorch_amd.use_engine_graph_queues)."""
 from __future__ import annotations
 
 import re
@@ -25,8 +28,12 @@ from .program import Phase, stream_slots
 
 import os  # noqa: E402
 
-# the executor's stream count (DEBUG_HIP_FORCE_GRAPH_QUEUES: runtime default 4, the package sets 2)
-EXEC_STREAMS = int(os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES", "4"))
+
+def executor_streams() -> int:
+    """The executor's stream count as the environment requests it (DEBUG_HIP_FORCE_GRAPH_QUEUES, runtime default
+    4; the entry points set 2).  The runtime reads the variable once, at its initialisation: a value set after
+    the process's first HIP call is not the one in effect."""
+    return int(os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES", "4"))
 
 
 def launch_records(phases: Sequence[Phase]) -> List[dict]:
@@ -36,7 +43,7 @@ def launch_records(phases: Sequence[Phase]) -> List[dict]:
     out = []
     for pi, ph in enumerate(phases):
         slot = stream_slots(ph.launches)
-        for l in ph.issue_order():
+        for l in ph.launches:
             out.append({"phase": pi, "name": l.name, "stream": slot[l.stream], "logical": l.stream,
                         "waits": [f"{pi}:{ph.alias.get(t, t)}" for t in l.waits],
                         "record": None if l.record is None else f"{pi}:{l.record}", "kernel": l.fn is not None})
@@ -82,7 +89,7 @@ def capture_dag(records: List[dict]):
     return nodes, children
 
 
-def schedule(children: List[List[int]], n_streams: int = EXEC_STREAMS) -> List[int]:
+def schedule(children: List[List[int]], n_streams: int = 4) -> List[int]:
     """The executor's stream per node (see the module docstring)."""
     n = len(children)
     indeg = [0] * n
@@ -111,12 +118,12 @@ def schedule(children: List[List[int]], n_streams: int = EXEC_STREAMS) -> List[i
     return sid
 
 
-def mismatch(phases: Sequence[Phase], n_streams: int = EXEC_STREAMS) -> dict:
+def mismatch(phases: Sequence[Phase], n_streams: int = None) -> dict:
     """How far the executor's assignment is from the logical one: for every logical stream, the executor
     streams its kernels land on (count per stream), and the number of kernels not on the executor stream
     that holds most of their logical stream."""
     nodes, children = capture_dag(launch_records(phases))
-    sid = schedule(children, n_streams)
+    sid = schedule(children, executor_streams() if n_streams is None else n_streams)
     per: Dict[int, Dict[int, int]] = {}
     for r, s in zip(nodes, sid):
         per.setdefault(r["stream"], {}).setdefault(s, 0)
@@ -138,121 +145,3 @@ def parse_dot(path: str):
     for a, b in edges:
         children[a].append(b)
     return [nodes[i] for i in range(n)], children
-
-
-def plan_children(children: List[List[int]], target: List, n_streams: int = EXEC_STREAMS):
-    """New per-node child orders (with redundant filler edges) under which the executor's assignment
-    (``schedule``) puts every node whose ``target`` is known on exactly that executor stream.
-
-    Why it works: a node's first child inherits its stream, the child at edge position p gets stream + p.
-    * position 0 of every node is its same-target successor (the next node of its logical stream), so
-      the walk from the root first dives down the whole stream-0 chain, then each chain is followed down
-      from wherever it is first entered;
-    * a child on another non-zero target is placed at a position p = (its target - the node's) mod
-      n_streams, so that it is right whichever of its parents reaches it first;
-    * children that are already scheduled when the node's loop reaches them -- stream-0 nodes (scheduled by
-      the initial dive) and later nodes of the node's own chain (scheduled by its position-0 dive) -- fill
-      the gaps; when they run out, redundant edges to such nodes are added (the node already precedes
-      them, so no dependency changes).
-    Nodes with an unknown target (None) keep their child order.  Returns (new children, #filler edges)."""
-    n = len(children)
-    N = n_streams
-    parents = [[] for _ in range(n)]
-    for v, cs in enumerate(children):
-        for c in cs:
-            parents[c].append(v)
-
-    def succ(v):
-        if target[v] is None:
-            return None
-        return next((c for c in children[v] if target[c] == target[v]), None)
-
-    nxt = [succ(v) for v in range(n)]
-    new, fillers = [], 0
-    for v in range(n):
-        cs = children[v]
-        tv = target[v]
-        if tv is None or not cs:
-            new.append(list(cs))
-            continue
-        s = nxt[v]
-        constrained = {}
-        free = []
-        for c in cs:
-            if c == s:
-                continue
-            tc = target[c]
-            if tc is None or tc == 0 or tc == tv:
-                free.append(c)
-            else:
-                constrained.setdefault((tc - tv) % N, []).append(c)
-        # spare filler nodes: the node's own chain below its successor, then stream-0 descendants
-        have = set(cs)
-        spare = []
-
-        def more_spare():
-            if spare:
-                return spare.pop(0)
-            return None
-
-        chain, x = [], (nxt[s] if s is not None else None)
-        while x is not None and len(chain) < 3 * N:
-            if x not in have:
-                chain.append(x)
-            x = nxt[x]
-        spare.extend(chain)
-        out = [s] if s is not None else []
-        if s is None and constrained:  # position 0 must not take a constrained child
-            f = free.pop(0) if free else more_spare()
-            if f is None:
-                new.append(list(cs))
-                continue
-            if f not in have:
-                fillers += 1
-            out.append(f)
-        ok = True
-        while any(constrained.values()):
-            r = len(out) % N
-            if constrained.get(r):
-                out.append(constrained[r].pop(0))
-                continue
-            f = free.pop(0) if free else more_spare()
-            if f is None:
-                ok = False
-                break
-            if f not in have:
-                fillers += 1
-                have.add(f)
-            out.append(f)
-        if not ok:
-            new.append(list(cs))
-            continue
-        out += free
-        new.append(out)
-    return new, fillers
-
-
-def restream_check(children: List[List[int]], target: List, n_streams: int = EXEC_STREAMS):
-    """(#nodes with a known target, #of them the executor would put elsewhere) for a child order."""
-    sid = schedule(children, n_streams)
-    known = [i for i, t in enumerate(target) if t is not None]
-    return len(known), sum(1 for i in known if sid[i] != target[i])
-
-
-def restream(graph: int, tracker) -> dict:
-    """Rewrite the edge order of a captured (not yet instantiated) graph so that the executor runs every
-    tracked node on the executor stream of its engine stream (plan_children).  Applied only when the
-    emulated assignment is then exact; returns what was done."""
-    from ..ops.hip import lib
-    _, children = lib().graph_structure(graph)
-    # more engine streams than executor streams: stream 0 keeps an executor stream of its own, the side
-    # streams fold onto the others
-    targets = [None if t is None else min(t, EXEC_STREAMS - 1) for t in tracker.targets(graph)]
-    known, before = restream_check(children, targets)
-    new, fillers = plan_children(children, targets)
-    _, after = restream_check(new, targets)
-    applied = after < before
-    if applied:
-        lib().graph_set_children(graph, new)
-    return {"nodes": len(children), "tracked": known, "misplaced_before": before, "misplaced_after": after,
-            "fillers": fillers, "applied": applied}

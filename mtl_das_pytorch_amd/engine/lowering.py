@@ -12,7 +12,7 @@ from ..ops.functional import WGRAD_PATCH, WGRAD_TILES, wgrad_ktiles
 from ..ops.hip import lib
 from .core import (GRAD_DT, Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, optimizer_segments,
                    pad_to)
-from .program import (COMM_STREAM, SPILL_STREAM, Launch, Phase, k_adam, k_allreduce, k_conv, k_gather, k_tail_bwd, k_tail_fwd,
+from .program import (COMM_STREAM, SPILL_STREAM, Launch, Phase, k_adam, k_allreduce, k_ext_record, k_conv, k_gather, k_tail_bwd, k_tail_fwd,
                       k_tail_fwd_batched, k_wgfin, k_wgrad,
                       k_wgrad_batched)
 
@@ -74,20 +74,26 @@ class LoweredProgram:
     default_buckets = 1  # gradient buckets under data parallelism (segment_backward); MDA_BUCKETS overrides
     LOCAL_BUCKETS = 1    # the same segmentation of the backward in a single process (no collectives)
 
-    def dp_buckets(self, world: int, captured: bool = True) -> int:
-        """Gradient buckets of a data-parallel step.  Overlapped buckets only pay inside ONE captured graph
-        (backward_with_allreduce: the collectives are graph nodes on the communication stream).  When the
-        collectives run eagerly between graphs (``captured`` False: the multi-rank default) every bucket cuts
-        the backward into piece graphs whose boundaries join all streams -- measured on one MI355X with the
-        per-rank program of an 8-GPU run (bench.py --dp-shape 8, 1-rank RCCL): Model A 30.1 k (2 buckets)
-        vs 34.3 k samples/s (1), Model C 6.2 k (2) / 6.7 k (4) vs 8.3 k (1) -- more than the unoverlapped
-        all-reduce costs, so that path uses one bucket."""
+    # a measured all-reduce of the whole flat gradient shorter than this is not worth a bucket cut (each extra
+    # bucket costs a finalize launch and an event join on stream 0)
+    OVERLAP_MIN_MS = 0.02
+
+    def dp_buckets(self, world: int, allreduce_ms: Optional[float] = None) -> int:
+        """Gradient buckets of a data-parallel step of ``world`` ranks.  Every form of the step overlaps the
+        buckets' all-reduces with the rest of the backward inside ONE step graph: captured collectives on the
+        communication stream (backward_with_allreduce) or eager RCCL all-reduces ordered after the graph's
+        external bucket events (backward_with_ext_events, the multi-rank default).  ``allreduce_ms``: the
+        time of one all-reduce of the whole flat gradient measured on the live group at start-up
+        (parallel.dist.calibrate_allreduce); below OVERLAP_MIN_MS one bucket.  Otherwise the model's
+        default_buckets (A 2, C 4: SURVEY 5.8 sizes C's 83 MB in 2-4 buckets); MDA_BUCKETS overrides."""
         import os
         if world <= 1:
             return self.LOCAL_BUCKETS
-        if not captured:
-            return int(os.environ.get("MDA_BUCKETS", "1"))
-        return int(os.environ.get("MDA_BUCKETS", str(self.default_buckets)))
+        if "MDA_BUCKETS" in os.environ:
+            return int(os.environ["MDA_BUCKETS"])
+        if allreduce_ms is not None and allreduce_ms < self.OVERLAP_MIN_MS:
+            return 1
+        return self.default_buckets
 
     # -------------------------------------------------------------------------------------------
     def _tail_args(self, y: Act, bn: BNLayer, out: Act, training: bool, H=None, W=None) -> tuple:
@@ -419,6 +425,7 @@ class LoweredProgram:
         gradients).  Returns the buckets [(lo, hi)] in completion order."""
         f = self.flat
         self.buckets = [(0, f.numel)]
+        self.bucket_anchors = None
         if n_buckets <= 1 or any(l.name == "cut" for l in self.bwd.launches):
             return self.buckets
         ls = self.bwd.launches
@@ -493,6 +500,58 @@ class LoweredProgram:
         self.buckets = buckets
         return buckets
 
+    def stream_buckets(self, max_buckets: int) -> List[tuple]:
+        """Gradient buckets for the eager-collective data-parallel step (backward_with_ext_events) WITHOUT cutting
+        the backward: a bucket is a prefix range of the flat gradient whose every writer runs on ONE side stream
+        no later than that stream's own finalize (batch_wgrads' SIDE_FINALIZE), so it is complete when that
+        finalize is -- while stream 0 still runs its data-gradient chain -- and its all-reduce overlaps the rest
+        of the backward with no extra join of the streams (segment_backward's cut joins every stream at the
+        bucket boundary: A 30.0 k vs 33.3 k samples/s at 2 vs 1 buckets on the per-rank program of 8 GPUs).
+        The remainder is the last bucket, complete at the tail finalize.  Model A: the level parameters lead the
+        flat buffer and are written on stream 1 only.  Call after autotune_program (batched weight gradients)
+        on a backward that segment_backward left whole.  Returns the buckets [(lo, hi)] in completion order."""
+        f = self.flat
+        ls = self.bwd.launches
+        if any(l.name == "cut" for l in ls):
+            raise ValueError("stream_buckets needs an uncut backward (segment_backward(1))")
+        gbase = P(f.grads)
+        writers: Dict[int, set] = {}  # flat offset of a parameter's gradient -> {(stream, launch index)}
+        for i, l in enumerate(ls):
+            if l.name == "wgrad_finalize":
+                for c in (l.owner or self.convs):  # (no owner: the finalize covers every conv)
+                    for m in c.mods:
+                        writers.setdefault(f.off(m.weight), set()).add((l.stream, i))
+            elif l.fn is not None:
+                for off in _grad_offsets(l, gbase, f.numel):
+                    writers.setdefault(off, set()).add((l.stream, i))
+        side_fin = {l.stream: i for i, l in enumerate(ls) if l.name == "wgrad_finalize" and l.stream != 0}
+        buckets, anchors, k, lo = [], [], 0, 0
+        order = f.order
+        # (a parameter with no writer -- a conv bias feeding a BN, whose gradient is identically 0 -- is never
+        # written during the step: complete in any bucket)
+        while k < len(order) and len(buckets) < max_buckets - 1:
+            w = next((writers[f.off(q)] for q in order[k:] if f.off(q) in writers), None)
+            st = next(iter(w))[0] if w else None
+            if st not in side_fin:
+                break
+            j = k
+            while j < len(order):
+                w = writers.get(f.off(order[j]))
+                if w and any(s2 != st or i2 > side_fin[st] for s2, i2 in w):
+                    break
+                j += 1
+            hi = f.off(order[j]) if j < len(order) else f.numel
+            if hi <= lo:
+                break
+            buckets.append((lo, hi))
+            anchors.append(ls[side_fin[st]])
+            lo, k = hi, j
+        fins = [l for l in ls if l.name == "wgrad_finalize"]
+        buckets.append((lo, f.numel))
+        anchors.append(fins[-1])
+        self.buckets, self.bucket_anchors = buckets, anchors
+        return buckets
+
     def backward_with_allreduce(self, allreduce) -> Phase:
         """The backward with every gradient bucket's all-reduce embedded in it, so the whole
         data-parallel step -- forward, backward, collectives, optimizer -- is one HIP graph.  Each bucket's
@@ -526,12 +585,52 @@ class LoweredProgram:
             raise ValueError(f"finalize launches for buckets {sorted(done)}, expected {len(buckets)} buckets")
         return ph
 
+    def backward_with_ext_events(self, events) -> Phase:
+        """The backward with an EXTERNAL event recorded where each gradient bucket is complete: ``events[k]`` is
+        an ExtEvent (engine/program.py), so in the captured step graph it is an event-record node.  The
+        data-parallel step at world > 1 (engine/step.py "train_ext") replays forward + this backward as one
+        graph and then, on the host, makes the communication stream wait for ``events[k]`` and issues bucket
+        k's eager RCCL all-reduce there: bucket k's collective runs while the graph computes the rest of the
+        backward -- overlap without capturing multi-rank collectives.  Buckets from stream_buckets: the event
+        follows the bucket's side-stream finalize; from segment_backward: it follows the bucket's last finalize,
+        joined over the finalizes' streams."""
+        f = self.flat
+        buckets = getattr(self, "buckets", None) or [(0, f.numel)]
+        if len(events) != len(buckets):
+            raise ValueError(f"{len(events)} events for {len(buckets)} buckets")
+        ph = Phase("backward_ext")
+        ph.alias = dict(self.bwd.alias)
+        anchors = getattr(self, "bucket_anchors", None)
+        if anchors is not None and len(anchors) == len(buckets):
+            at = {id(a): k for k, a in enumerate(anchors)}
+            for l in self.bwd.launches:
+                ph.launches.append(l)
+                if id(l) in at:
+                    ph.launches.append(Launch("ext_record", k_ext_record, events[at[id(l)]], stream=l.stream))
+            return ph
+        fins = [l for l in self.bwd.launches if l.name == "wgrad_finalize"]
+        last = {l.bucket: l for l in fins}
+        done = {}
+        for l in self.bwd.launches:
+            if l.name == "cut":
+                continue
+            if l.name != "wgrad_finalize":
+                ph.launches.append(l)
+                continue
+            tag = l.record or f"bucket{l.bucket}_grads_{len(done.get(l.bucket, []))}"
+            ph.launches.append(Launch(l.name, l.fn, *l.args, owner=l.owner, stream=l.stream, waits=l.waits,
+                                      record=tag, bucket=l.bucket))
+            done.setdefault(l.bucket, []).append(tag)
+            if l is last[l.bucket]:
+                ph.launches.append(Launch("ext_record", k_ext_record, events[l.bucket], stream=l.stream,
+                                          waits=tuple(t for t in done[l.bucket] if t != tag), bucket=l.bucket))
+        if sorted(done) != list(range(len(buckets))):
+            raise ValueError(f"finalize launches for buckets {sorted(done)}, expected {len(buckets)} buckets")
+        return ph
+
     WGRAD_MAX_BATCHES = 3
     # the same cap for stream 0 only (its batches run serially after the data-gradient chain); None: as above
     WGRAD_MAX_BATCHES_S0 = None
-    # batched weight-gradient launches walk their virtual blocks in XCD-contiguous order (csrc/conv.hip
-    # wgrad_vblock): the tiles and neighbouring M splits that read the same rows share one L2
-    WGRAD_XCD = 0
     # hardware blocks of a side stream's batched weight-gradient launch (0: one per virtual block): a capped,
     # persistent grid leaves CU slots free for the critical chain's kernels (csrc/conv.hip WGRAD_FOR_VBLOCKS)
     SIDE_WGRAD_GRID = 0
@@ -617,9 +716,6 @@ class LoweredProgram:
     # C +0.6-7.5 % / A neutral, and A +0.3-0.6 % / C neutral (docs/PERF.md round 4); class switches for A/B runs
     SIDE_FINALIZE = True
     EARLY_ADAM = True
-    # stream 0's weight-gradient batches (after its last data gradient, the step's serial tail): the
-    # finalize + Adam of every batch but the last runs on a side stream while stream 0 computes the next batch
-    PIPELINE_S0 = False
 
     def batch_wgrads(self):
         """Replace the per-conv weight-gradient launches by batched launches, one per (stream, tile
@@ -682,14 +778,12 @@ class LoweredProgram:
                                           record=tag))
                     tags = [t for t in tags if t != batched[-2].record] + [tag]
             early_ok = self.EARLY_ADAM and not self.data_parallel and self._opt_hparams.get("grad_scale", 1.0) == 1.0
-            piped = self._pipeline_s0(inserts, keep, wg) if early_ok and self.PIPELINE_S0 else []
-            done = [c for v in side.values() for c in v] + [c for convs, _ in piped for c in convs]
+            done = [c for v in side.values() for c in v]
             rest = [c for c in self.convs if c not in done]
-            if (side or piped) and rest:
+            if side and rest:
                 ls[fin].owner = rest
                 ls[fin].args = self._wgfin_args(rest)
-            tags += [tag for _, tag in piped]
-            if (side or piped) and early_ok:
+            if side and early_ok:
                 # single process: the side convs' Adam + re-pack right after their finalize, on their stream
                 # (the optimizer phase then covers the rest); with gradient averaging (DP, set_optimizer's
                 # data_parallel) the update must wait for the all-reduce, so it stays in the optimizer phase
@@ -710,8 +804,6 @@ class LoweredProgram:
                     batched.append(Launch("adam_pack_early", k_adam, d, stream=st, record=tag))
                     tags = [t for t in tags if t != f"wgfin_s{st}"] + [tag]
                     self._early_adam = getattr(self, "_early_adam", []) + [d]
-                for convs, _ in piped:
-                    early |= {self.flat.off(m.weight) for c in convs for m in c.mods}
                 segs = [g for g in self.opt_segs if not (g["kind"] == 3 and g["off"] in early)]
                 table, ns, nb = build_optseg_table(segs, self.device)
                 self._opt_tables = getattr(self, "_opt_tables", []) + [table]
@@ -726,56 +818,12 @@ class LoweredProgram:
         self.bwd.launches = keep + ls[fin:]
         self.wgrads_batched = True
 
-    def _pipeline_s0(self, inserts, keep: List[Launch], wg: List[Launch]):
-        """PIPELINE_S0: after each of stream 0's weight-gradient batches but the last, a side stream reduces
-        that batch's split slabs (finalize) and runs the Adam + re-pack of its convs while stream 0 computes
-        the next batch, so the tail after stream 0's last batch only finalizes and updates the last batch's
-        convs.  A batch is pipelined only if none of its convs has a data gradient on another stream (its
-        weights must be dead once stream 0 reaches the batch).  Appends the launches to stream 0's insert
-        list; returns [(convs, event tag)] of the pipelined batches."""
-        s0 = next((b for _, b in inserts if b[0].stream == 0), None)
-        streams = {l.stream for l in keep}
-        if s0 is None or len(s0) < 2 or 1 not in streams:
-            return []
-        dgrad_streams = {}
-        for l in keep:
-            if l.name.startswith("conv_dgrad") and l.owner is not None:
-                dgrad_streams.setdefault(id(l.owner), set()).add(l.stream)
-        out, new = [], []
-        for i, b in enumerate(s0):
-            new.append(b)
-            if i == len(s0) - 1:
-                break
-            convs = list(dict.fromkeys(l.owner for l in wg if l.stream == 0 and l.args[0] == b.args[0]
-                                       and l.owner is not None))
-            if not convs or any(dgrad_streams.get(id(c), {0}) != {0} for c in convs):
-                continue
-            b.record = f"wgb0_{i}"
-            tag = f"adam_p{i}"
-            offs = {self.flat.off(m.weight) for c in convs for m in c.mods}
-            segs = [g for g in self.opt_segs if g["kind"] == 3 and g["off"] in offs]
-            table, ns, nb = build_optseg_table(segs, self.device)
-            self._opt_tables = getattr(self, "_opt_tables", []) + [table]
-            d = dict(self._opt_base, segs=P(table), nsegs=ns, nblocks=nb, update=1, inc_step=0, **self._opt_hparams)
-            self._early_adam = getattr(self, "_early_adam", []) + [d]
-            new += [Launch("wgrad_finalize", k_wgfin, *self._wgfin_args(convs), owner=convs, stream=1,
-                           waits=(b.record,)),
-                    Launch("adam_pack_early", k_adam, d, stream=1, record=tag)]
-            out.append((convs, tag))
-        s0[:] = new
-        return out
-
-    def wgrad_flags(self) -> int:
-        """Flag word of the batched weight-gradient launches (csrc/conv.hip wgrad_vblock)."""
-        return 1 if self.WGRAD_XCD else 0
-
     def _wgrad_batch_launch(self, cfg: int, group: List[Launch], st: int, bucket: int = 0) -> Launch:
         raw, nblocks = lib().wgrad_table(cfg, [l.args[2] for l in group], [l.args[1] for l in group])
         table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         self.wgrad_tables.append(table)
         cap = self.SIDE_WGRAD_GRID if st != 0 else 0
-        return Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, cap, self.wgrad_flags(), stream=st,
-                      bucket=bucket)
+        return Launch("wgrad_batched", k_wgrad_batched, cfg, table, len(group), nblocks, cap, stream=st, bucket=bucket)
 
     def _batch_wgrads_segmented(self):
         """batch_wgrads for a backward cut into gradient-bucket pieces (segment_backward): in every piece,

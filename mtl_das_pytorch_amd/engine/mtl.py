@@ -54,9 +54,6 @@ class MTLProgram(LoweredProgram):
     # (docs/PERF.md round 5); Model C keeps its own values (its weight gradients lose 0.9 % at 2048)
     NOL_MAX_PX = 60000
     WGRAD_MIN_SPLIT_PX_BIG = 2048
-    # the last level's attention product sigmoid(BN(y)) * F8 is computed on load by the head kernel
-    # (csrc/head.hip MASK): its SIGMUL tail launch leaves the end-of-forward critical path
-    HEAD_MASK = False
 
     def __init__(self, model: MTLNet, batch: int, device, in_hw=(100, 250), loss_weights: Optional[Sequence[float]] = None,
                  sync_world: int = 1):
@@ -264,9 +261,8 @@ class MTLProgram(LoweredProgram):
             else:
                 self._tail(ph, ACT_RELU, T, L["ym1"], L["bn0"], L["hm"], training)
                 self._conv_fwd(ph, L["c3"], src_dict(L["hm"]), L["ym2"], L["bn3"], training)
-            if "co" in L or not self.HEAD_MASK:
-                ph.pending_waits.append(f"F{2 * lvl + 2}")
-                self._tail(ph, SIGMUL, T, L["ym2"], L["bn3"], L["Aout"], training, r=L["Fb"])
+            ph.pending_waits.append(f"F{2 * lvl + 2}")
+            self._tail(ph, SIGMUL, T, L["ym2"], L["bn3"], L["Aout"], training, r=L["Fb"])
             if "co" in L:
                 self._conv_fwd(ph, L["co"], src_dict(L["Aout"]), L["yo"], L["bno"], training)
                 self._tail(ph, POOL_RELU, T, L["yo"], L["bno"], L["Bp"], training)
@@ -281,10 +277,6 @@ class MTLProgram(LoweredProgram):
               "metrics": P(self.metrics), "confusion": P(self.confusion), "nvalid": P(self.nvalid)}
         if T == 2:
             hd["lab_off"] = 0
-        if self.HEAD_MASK:  # (the head runs on stream 0 after F8's tail: the product's operands are ready)
-            L4 = self.levels[3]
-            hd.update({"feat": L4["Fb"].p, "fgs": L4["Fb"].gs, "ldf": L4["Fb"].ld, "my": L4["ym2"].p,
-                       "mygs": L4["ym2"].gs, "ldmy": L4["ym2"].ld, "mbn": L4["bn3"].args(training)})
         ph.add("mtl_head", k_head, hd)
         return ph
 

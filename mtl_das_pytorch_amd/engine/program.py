@@ -56,6 +56,10 @@ class Launch:
     def __call__(self, st: int, tstream=None):
         if self.fn is None:  # a pseudo-launch that only carries waits / a record (fork point)
             return
+        if self.fn is k_ext_record:  # an external event: a graph event-record node under capture
+            import torch
+            self.args[0].record(torch.cuda.current_stream() if tstream is None else tstream)
+            return
         if self.fn is k_allreduce:  # a host-issued collective: it runs with the launch's stream as current
             import torch
             if tstream is None or tstream == torch.cuda.current_stream():
@@ -107,6 +111,9 @@ class EngineStreams:
         n = MAX_STREAMS - 1 + 2
         self.handles = [lib().stream_create(0) for _ in range(n + 1)]
         self.streams = [torch.cuda.ExternalStream(h, device=device) for h in self.handles[:n]]
+        # the communication stream (slot MAX_STREAMS): captured bucket collectives run on it inside a phase,
+        # and the world > 1 step issues its eager bucket all-reduces on it (engine/step.py)
+        self.comm = self.streams[MAX_STREAMS - 1]
         # graph captures and their eager warm-up runs (StepRunner, capture_graph): never a pool stream, so a
         # communicator's pool stream can never be the stream a graph is captured on
         self.capture = torch.cuda.ExternalStream(self.handles[n], device=device)
@@ -121,7 +128,7 @@ class EngineStreams:
     def destroy(self):
         for h in self.handles:
             lib().stream_destroy(h)
-        self.handles, self.streams, self.capture = [], [], None
+        self.handles, self.streams, self.capture, self.comm = [], [], None, None
 
 
 def release_streams():
@@ -148,10 +155,8 @@ class EventKeeper:
 
     active = None  # the keeper of the capture in progress, if any
 
-    def __init__(self, track: bool = False):
+    def __init__(self):
         self.events = []
-        # tags every captured node with the executor stream its launch should run on (graphsched.restream)
-        self.tracker = lib().CaptureTracker() if track else None
 
     def __enter__(self):
         if EventKeeper.active is not None:
@@ -165,12 +170,6 @@ class EventKeeper:
 
 
 class Phase:
-    # issue order of the launches on the host (the order the capture sees them in): "program" as emitted,
-    # or "main_first": a stream-0 launch whose waits are satisfied is always issued before any side-stream
-    # launch, so that in the captured graph a stream-0 node's first successor edge is the next stream-0 node
-    # (the HIP graph executor walks first edges to build the chain it runs on the launch stream)
-    ISSUE_ORDER = "program"
-
     def __init__(self, name: str):
         self.name = name
         self.launches: List[Launch] = []
@@ -203,14 +202,11 @@ class Phase:
     def run(self, st=None):
         import torch
         keeper = EventKeeper.active
-        tracker = keeper.tracker if keeper is not None else None
         if not MULTI_STREAM or all(l.stream == 0 and not l.waits for l in self.launches):
             st = stream() if st is None else st
             for l in self.launches:
                 if l.fn is not None:
                     l(st)
-                    if tracker is not None:
-                        tracker.note(st, 0)
             return
         main = torch.cuda.current_stream()
         es = EngineStreams.get(main.device)
@@ -223,14 +219,11 @@ class Phase:
             if sid:
                 phys[sid].wait_event(start)
         events = {}
-        rank = {sid: i for i, sid in enumerate(sorted(phys))}  # executor stream of each slot (graphsched)
-        for l in self.issue_order():
+        for l in self.launches:
             s = phys[slot[l.stream]]
             for tag in l.waits:
                 s.wait_event(events[self.alias.get(tag, tag)])
             l(s.cuda_stream, s)
-            if tracker is not None and l.fn is not None:
-                tracker.note(s.cuda_stream, rank[slot[l.stream]])
             if l.record is not None:
                 events[l.record] = s.record_event()
         for sid in phys:
@@ -244,68 +237,12 @@ class Phase:
         else:
             self._live_events = (start, events)
 
-    def issue_order(self) -> List[Launch]:
-        """The launches in host issue order (see ISSUE_ORDER); every order returned keeps each stream's own
-        order and issues a wait only after the launch recording its event."""
-        if self.ISSUE_ORDER != "main_first":
-            return self.launches
-        recs = [l.record for l in self.launches if l.record is not None]
-        if len(recs) != len(set(recs)):  # a re-recorded tag: only the program order defines which record a wait sees
-            return self.launches
-        queues: dict = {}
-        for i, l in enumerate(self.launches):
-            queues.setdefault(l.stream, []).append(i)
-        heads = {s: 0 for s in queues}
-        recorded, out = set(), []
-        ready = lambda l: all(self.alias.get(t, t) in recorded for t in l.waits)  # noqa: E731
-        while len(out) < len(self.launches):
-            q0 = queues.get(0)
-            if q0 is not None and heads[0] < len(q0) and ready(self.launches[q0[heads[0]]]):
-                pick = 0
-            else:  # the earliest pending head in program order is always ready (all launches before it issued)
-                pick = min((queues[s][heads[s]], s) for s in queues if heads[s] < len(queues[s]))[1]
-            l = self.launches[queues[pick][heads[pick]]]
-            heads[pick] += 1
-            out.append(l)
-            if l.record is not None:
-                recorded.add(l.record)
-        return out
-
     def __len__(self):
         return len(self.launches)
 
     def release(self):
         """Drop the events of the last eager run (the caller has synchronized)."""
         self._live_events = None
-
-    def split(self) -> List["Phase"]:
-        """Cut the phase at its pseudo-launches named ``cut`` into consecutive phases.
-
-        Each piece is run (or captured) on its own: its side streams fork from stream 0 at its start and
-        are joined back at its end, so an event recorded in an earlier piece is already ordered before
-        the later one -- such waits are dropped.  Used to end the backward at gradient-bucket boundaries
-        (DP: a bucket's all-reduce is issued between two pieces and overlaps the next one)."""
-        pieces, cur = [], []
-        for l in self.launches:
-            if l.name == "cut":
-                pieces.append(cur)
-                cur = []
-            else:
-                cur.append(l)
-        pieces.append(cur)
-        out, recorded = [], set()
-        for i, ls in enumerate(pieces):
-            ph = Phase(f"{self.name}_{i}")
-            ph.alias = dict(self.alias)
-            for l in ls:
-                w = tuple(t for t in l.waits if self.alias.get(t, t) not in recorded)
-                ph.launches.append(Launch(l.name, l.fn, *l.args, owner=l.owner, stream=l.stream, waits=w,
-                                          record=l.record, bucket=l.bucket))
-            for l in ls:
-                if l.record is not None:
-                    recorded.add(l.record)
-            out.append(ph)
-        return out
 
 
 # thin adapters giving every launch the signature fn(*args, stream)
@@ -345,8 +282,8 @@ def k_pool(is_max, bwd, d, st):
     lib().pool3(is_max, bwd, st, d)
 
 
-def k_wgrad_batched(cfg, table, nj, nblocks, cap, xcd, st):
-    lib().wgrad_batched(cfg, table.data_ptr(), nj, nblocks, st, cap, xcd)
+def k_wgrad_batched(cfg, table, nj, nblocks, cap, st):
+    lib().wgrad_batched(cfg, table.data_ptr(), nj, nblocks, st, cap)
 
 
 def k_wgfin(table, nd, nblocks, st):
@@ -355,6 +292,34 @@ def k_wgfin(table, nd, nblocks, st):
 
 def k_adam(d, st):
     lib().adam_pack(st, d)
+
+
+class ExtEvent:
+    """A HIP event recorded with ``hipEventRecordExternal`` while its stream captures (an event-record node of
+    the graph, re-recorded at every replay), plainly otherwise; ``wait(stream)`` makes a torch stream wait for
+    its latest record.  (PyTorch refuses ``torch.cuda.Event(external=True)`` on ROCm.)  ``destroy`` after the
+    device has finished every graph that records it."""
+
+    def __init__(self):
+        self.handle = lib().event_create()
+
+    def record(self, stream):
+        lib().event_record_external(self.handle, stream.cuda_stream)
+
+    def wait(self, stream):
+        lib().stream_wait_event(stream.cuda_stream, self.handle)
+
+    def destroy(self):
+        if self.handle:
+            lib().event_destroy(self.handle)
+            self.handle = 0
+
+
+def k_ext_record(ev, st):
+    """Marker launch: record the EXTERNAL event ``ev`` (ExtEvent) on the launch's stream (Launch.__call__).  Captured, it is an event-record node of the graph: the host can order work
+    issued after the replay -- an eager RCCL all-reduce on another stream -- after that point of the graph
+    (engine/step.py, the data-parallel step at world > 1)."""
+    raise RuntimeError("k_ext_record is dispatched by Launch.__call__")
 
 
 def k_allreduce(fn, t, st):

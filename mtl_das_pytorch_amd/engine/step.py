@@ -6,18 +6,18 @@ A training step is
     gradient buckets)  ->  [fused Adam + bf16 re-pack] [step++]
 
 Single GPU: the whole step is ONE captured HIP graph (``torch.cuda.CUDAGraph`` is a hipGraph on ROCm),
-so a step costs one graph launch from the host.  Data parallel with capturable collectives (RCCL, see
-DistContext.capturable_collectives): still ONE graph -- the gradient buckets' all-reduces are captured
-on a communication stream inside it (LoweredProgram.backward_with_allreduce), each waiting only for its
-bucket's finalize.  Otherwise RCCL runs eagerly between graphs: with one bucket the compute graph is
-followed by one all-reduce and the optimizer graph; with several (LoweredProgram.segment_backward) the
-backward is captured as one graph per bucket piece; after replaying piece k the host issues bucket k's
-all-reduce asynchronously (RCCL's stream waits for piece k) and replays piece k+1, which then runs
-concurrently with the collective; the optimizer graph waits for every bucket.
+so a step costs one graph launch from the host.  Data parallel with capturable collectives (a 1-rank RCCL
+group, see DistContext.capturable_collectives): still ONE graph -- the gradient buckets' all-reduces are
+captured on a communication stream inside it (LoweredProgram.backward_with_allreduce), each waiting only for
+its bucket's finalize.  Otherwise (the multi-rank default: RCCL collectives stay eager) forward + backward
+are ONE graph that records an EXTERNAL event where each gradient bucket is complete
+(LoweredProgram.backward_with_ext_events); after enqueuing its replay the host makes the communication
+stream wait for bucket k's event and issues bucket k's asynchronous RCCL all-reduce there, so it runs while
+the graph computes the rest of the backward; the optimizer graph waits for every bucket (Work.wait).
 
-The batch indices live in a persistent device buffer that the host refreshes (device-to-device copy)
-before each replay; the learning rate is a device scalar, so the reference's LR schedule never forces
-a re-capture.
+The batch indices come from a device-resident schedule (set_index_schedule: the gather reads the next row,
+the optimizer kernel advances the cursor) or from a persistent device buffer the host refreshes before each
+replay; the learning rate is a device scalar, so the reference's LR schedule never forces a re-capture.
 """
 from __future__ import annotations
 
@@ -25,8 +25,7 @@ from typing import Callable, Dict, List, Optional
 
 import torch
 
-from .program import EngineStreams, EventKeeper, Phase
-from ..ops.hip import lib
+from .program import EngineStreams, EventKeeper, ExtEvent, Phase
 
 
 class StateSnapshot:
@@ -41,39 +40,22 @@ class StateSnapshot:
             t.copy_(s)
 
 
-def capture_graph(fns, restream: Optional[bool] = None, error_mode: str = "global"):
-    """Capture ``fns`` (phase runs) into one HIP graph.  Returns (graph, EventKeeper, restream info): the
-    keeper holds the events the capture recorded and must live as long as the graph; with ``restream``
-    (default StepRunner.RESTREAM) the graph's edge order is rewritten before instantiation so that the
-    executor keeps every engine stream on one stream of its own (engine/graphsched.py)."""
-    restream = StepRunner.RESTREAM if restream is None else restream
-    keeper = EventKeeper(track=restream)
-    g = torch.cuda.CUDAGraph(keep_graph=True) if restream else torch.cuda.CUDAGraph()
-    cap = EngineStreams.get(torch.cuda.current_stream().device).capture if StepRunner.ENGINE_CAPTURE_STREAM else None
+def capture_graph(fns, error_mode: str = "global"):
+    """Capture ``fns`` (phase runs) into one HIP graph on the engine's capture stream.  Returns (graph,
+    EventKeeper): the keeper holds the events the capture recorded and must live as long as the graph."""
+    keeper = EventKeeper()
+    g = torch.cuda.CUDAGraph()
+    cap = EngineStreams.get(torch.cuda.current_stream().device).capture
     with keeper, torch.cuda.graph(g, stream=cap, capture_error_mode=error_mode):
         for f in fns:
             f()
-    info = None
-    if restream:
-        from .graphsched import restream as _restream
-        info = _restream(g.raw_cuda_graph(), keeper.tracker)
-        g.instantiate()
-    return g, keeper, info
+    return g, keeper
 
 
 class StepRunner:
-    # stream the captured graphs are replayed on: None = the caller's current stream; an int = a dedicated
-    # stream of that HIP priority (-1 = high): the graph's first chain runs on the launch stream, its other
-    # branches on streams the HIP graph executor creates at normal priority
-    REPLAY_PRIORITY = None
-    # rewrite each captured graph's edge order so that the HIP graph executor runs every engine stream on a
-    # stream of its own (engine/graphsched.py: the executor otherwise re-derives streams from the DAG and
-    # mixes the critical chain with side work)
-    RESTREAM = False
-    # graphs are captured (and warmed up) on the engine's own capture stream, not on torch's pool streams:
-    # the world > 1 data-parallel step (per-bucket piece graphs + async RCCL) ran 2.7x slower with pool
-    # capture streams (bench.py --dp-shape 8 on Model A: 11.3 k -> 30.3 k samples/s, docs/PERF.md round 5)
-    ENGINE_CAPTURE_STREAM = True
+    # Graphs are captured (and warmed up) on the engine's own capture stream (EngineStreams.capture), never on
+    # torch's pool streams: the world > 1 data-parallel step ran 2.7x slower with pool capture streams (bench.py
+    # --dp-shape 8 on Model A: 11.3 k -> 30.3 k samples/s, docs/PERF.md round 5).
 
     def __init__(self, program, X: torch.Tensor, labels: torch.Tensor, use_graph: bool = True,
                  allreduce: Optional[Callable[[torch.Tensor], None]] = None, X_eval: torch.Tensor = None,
@@ -88,13 +70,15 @@ class StepRunner:
             self.sources["eval"] = (X_eval, labels_eval)
         self.graphs: Dict[str, torch.cuda.CUDAGraph] = {}
         self.keepers: Dict[str, EventKeeper] = {}  # events each graph was captured with (same lifetime)
-        self._replay = None  # (handle, ExternalStream) of the dedicated replay stream
-        self.restream_info: Dict[str, dict] = {}
         self._packed = False
-        self._bwd_pieces = None
         self._bwd_dp = None
+        self._bwd_ext = None
         # the DP step as one graph with the bucket collectives captured in it (FlatGradAllReducer.capturable)
         self.capture_dp = self.use_graph and allreduce is not None and getattr(allreduce, "capturable", False)
+        # otherwise forward + backward as one graph with an external event per gradient bucket, the bucket
+        # all-reduces issued eagerly on the communication stream after those events (train_step)
+        self.ext_dp = self.use_graph and allreduce is not None and not self.capture_dp
+        self.ext_events = None
         reducing = allreduce is not None and getattr(getattr(allreduce, "ctx", None), "enabled", False)
         if reducing and any(l.name == "adam_pack_early" for l in program.bwd.launches):
             # an update inside the backward would use local, un-reduced gradients
@@ -133,12 +117,6 @@ class StepRunner:
         self.p.opt["pack"].run()
         self._packed = True
 
-    def _pieces(self):
-        """The backward cut at its gradient-bucket boundaries (LoweredProgram.segment_backward)."""
-        if self._bwd_pieces is None:
-            self._bwd_pieces = self.p.bwd.split()
-        return self._bwd_pieces
-
     def _phases(self, kind: str) -> List[Callable[[], None]]:
         p = self.p
         X, lab = self.sources["train" if kind.startswith("train") else "eval"]
@@ -146,10 +124,11 @@ class StepRunner:
         sched = self.schedule is not None and kind.startswith("train")
         gather = p.gather_phase(X, lab, self.schedule if sched else self.idx, clear=kind.startswith("train"),
                                 cursor=self.cursor if sched else None)
-        if kind.startswith("train_piece"):
-            k = int(kind[len("train_piece"):])
-            pieces = self._pieces()
-            return ([gather.run, p.fwd_train.run] if k == 0 else []) + [pieces[k].run]
+        if kind == "train_ext":
+            if self._bwd_ext is None:
+                self.ext_events = [ExtEvent() for _ in self.buckets]
+                self._bwd_ext = p.backward_with_ext_events(self.ext_events)
+            return [gather.run, p.fwd_train.run, self._bwd_ext.run]
         if kind == "train_compute":
             return [gather.run, p.fwd_train.run, p.bwd.run]
         if kind == "train_opt":
@@ -170,17 +149,7 @@ class StepRunner:
                 f()
             return
         self._ensure_graph(kind)
-        if self.REPLAY_PRIORITY is None:
-            self.graphs[kind].replay()
-            return
-        if self._replay is None:
-            h = lib().stream_create(int(self.REPLAY_PRIORITY))
-            self._replay = (h, torch.cuda.ExternalStream(h, device=self.p.device))
-        rs, cur = self._replay[1], torch.cuda.current_stream()
-        rs.wait_stream(cur)
-        with torch.cuda.stream(rs):
-            self.graphs[kind].replay()
-        cur.wait_stream(rs)
+        self.graphs[kind].replay()
 
     def _drop_graph(self, kind: str):
         """Release one captured graph and the events it was captured with, after the device has finished
@@ -198,8 +167,7 @@ class StepRunner:
         if g is None:
             fns = self._phases(kind)
             snap = StateSnapshot(self._mutable_state())
-            s = (EngineStreams.get(torch.cuda.current_stream().device).capture if self.ENGINE_CAPTURE_STREAM
-                 else torch.cuda.Stream())
+            s = EngineStreams.get(torch.cuda.current_stream().device).capture
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):  # warm-up (loads code objects); side effects are rolled back
                 for f in fns:
@@ -211,9 +179,7 @@ class StepRunner:
             # Collectives captured here run on the capture-only RCCL communicator (DistContext.capture_group),
             # which never has eager work for the process-group watchdog to poll; the capture is thread-local
             # so that the watchdog's polls of the default communicator's eager work stay legal meanwhile.
-            g, keeper, info = capture_graph(fns, self.RESTREAM, "thread_local")
-            if info is not None:
-                self.restream_info[kind] = info
+            g, keeper = capture_graph(fns, "thread_local")
             torch.cuda.synchronize()
             self.graphs[kind] = g
             self.keepers[kind] = keeper
@@ -237,22 +203,24 @@ class StepRunner:
             self._run("train_full")
         elif self.capture_dp:
             self._run("train_full_dp")
-        elif len(self.buckets) == 1:
+        elif self.ext_dp:
+            # one graph for forward + backward; bucket k's all-reduce is issued on the communication stream
+            # behind the graph's external event k, so it overlaps the rest of the backward
+            if not self.graphs.get("train_ext") or not self.graphs.get("train_opt"):
+                self._ensure_graph("train_ext")  # both captured before any collective is in flight (the
+                self._ensure_graph("train_opt")  # capture's state snapshot/restore must not race an all-reduce)
+            self._run("train_ext")
+            comm = EngineStreams.get(self.p.device).comm
+            g = self.p.flat.grads
+            for ev, (lo, hi) in zip(self.ext_events, self.buckets):
+                ev.wait(comm)
+                with torch.cuda.stream(comm):
+                    self.allreduce.start(g[lo:hi])
+            self.allreduce.finish()
+            self._run("train_opt")
+        else:  # eager launches (no graphs): the whole gradient after the backward
             self._run("train_compute")
             self.allreduce(self.p.flat.grads)
-            self._run("train_opt")
-        else:
-            # piece k completes bucket k: its all-reduce is issued on the communication stream (after the
-            # piece, in stream order) while piece k+1 is replayed -- overlapped with the rest of the backward
-            g = self.p.flat.grads
-            if self.use_graph:  # capture every piece before any collective is in flight (the capture's
-                for k in range(len(self.buckets)):  # state snapshot/restore must not race an all-reduce)
-                    self._ensure_graph(f"train_piece{k}")
-                self._ensure_graph("train_opt")
-            for k, (lo, hi) in enumerate(self.buckets):
-                self._run(f"train_piece{k}")
-                self.allreduce.start(g[lo:hi])
-            self.allreduce.finish()
             self._run("train_opt")
 
     def set_eval_source(self, X: torch.Tensor, labels: torch.Tensor):
@@ -283,13 +251,12 @@ class StepRunner:
         for k in list(self.graphs):
             self._drop_graph(k)
         p = self.p
-        phases = [p.fwd_train, p.fwd_eval, p.bwd] + list(p.opt.values()) + list(self._bwd_pieces or [])
-        if self._bwd_dp is not None:
-            phases.append(self._bwd_dp)
+        phases = [p.fwd_train, p.fwd_eval, p.bwd] + list(p.opt.values())
+        phases += [ph for ph in (self._bwd_dp, self._bwd_ext) if ph is not None]
         for ph in phases:
             ph.release()
-        self._bwd_pieces = self._bwd_dp = None
-        if self._replay is not None:
-            lib().stream_destroy(self._replay[0])
-            self._replay = None
+        self._bwd_dp = self._bwd_ext = None
+        for ev in self.ext_events or []:
+            ev.destroy()
+        self.ext_events = None
         torch.cuda.synchronize()

@@ -268,8 +268,7 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
             t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(prog.device)
             tables.append(t)
             total += _time(lambda c=key[2], t=t, n=len(job), nb=nblocks:
-                           L.wgrad_batched(c, t.data_ptr(), n, nb, torch.cuda.current_stream().cuda_stream, 0,
-                                           prog.wgrad_flags()))
+                           L.wgrad_batched(c, t.data_ptr(), n, nb, torch.cuda.current_stream().cuda_stream, 0))
         for f in fin:
             total += _time(lambda f=f: f.fn(*f.args, torch.cuda.current_stream().cuda_stream))
         return total
@@ -416,7 +415,7 @@ def step_time_us(prog, X: torch.Tensor, labels: torch.Tensor, reps: int = 100, r
     for fn_ in fns:
         fn_()
     torch.cuda.synchronize()
-    g, keep, _ = capture_graph(fns)
+    g, keep = capture_graph(fns)
     for _ in range(10):
         g.replay()
     torch.cuda.synchronize()
@@ -511,7 +510,7 @@ def tune_in_context(prog, X: torch.Tensor, labels: torch.Tensor, cache: Dict[str
         for fn_ in fns:  # eager pass: code objects of a new config loaded before capture
             fn_()
         torch.cuda.synchronize()
-        g, events, _ = capture_graph(fns)
+        g, events = capture_graph(fns)
         g.replay()
         torch.cuda.synchronize()
         best = float("inf")

@@ -231,6 +231,30 @@ class FlatGradAllReducer:
             h.wait()
 
 
+def calibrate_allreduce(ctx: DistContext, numel: int, reps: int = 5) -> Optional[float]:
+    """Milliseconds of one all-reduce(SUM) of ``numel`` fp32 elements on the live process group (median of
+    ``reps`` after a warm-up, max over ranks so that every rank derives the same bucket count from it), or None
+    without a group.  bench.py reports it (``allreduce_ms``) and LoweredProgram.dp_buckets sizes the gradient
+    buckets from it: on xGMI the flat gradient's all-reduce is 10s of us (A, 4.3 MB) to ~0.5 ms (C, 83 MB)."""
+    if not ctx.enabled:
+        return None
+    import time
+    t = torch.zeros(numel, dtype=torch.float32, device=ctx.device)
+    sync = torch.cuda.synchronize if t.is_cuda else (lambda: None)
+    dist.all_reduce(t)
+    sync()
+    times = []
+    for _ in range(reps):
+        ctx.barrier()
+        sync()
+        t0 = time.perf_counter()
+        dist.all_reduce(t)
+        sync()
+        times.append(time.perf_counter() - t0)
+    del t
+    return ctx.max_scalar(1e3 * sorted(times)[len(times) // 2])
+
+
 def broadcast_module_state(ctx: DistContext, tensors: Iterable[torch.Tensor], src: int = 0):
     """C1: make every rank start from rank ``src``'s parameters and buffers."""
     if not ctx.enabled:

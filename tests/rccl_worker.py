@@ -9,10 +9,11 @@ line (bench.py's flagship step at per-GPU batch 32, tuned kernel configs):
              collectives -- bitwise equal after 3 steps (a 1-rank sum is exact), for 1 and 2 (A) / 4 (C) buckets:
              * captured (the 1-rank default, DistContext.capture_group): the buckets' all-reduces inside the
                step graph on the communication stream;
-             * pieces (the world > 1 default; ``FlatGradAllReducer.capturable = False`` here): the backward
-               cut into gradient-bucket piece graphs, each bucket's async all-reduce
-               (``FlatGradAllReducer.start``) issued on RCCL's stream while the next piece's graph runs,
-               ``finish`` making the compute stream wait (Work.wait), then the optimizer graph;
+             * ext (the world > 1 default; ``FlatGradAllReducer.capturable = False`` here): forward + backward
+               as ONE graph recording an external event per gradient bucket; after the replay is enqueued
+               the communication stream waits for bucket k's event and issues its async RCCL all-reduce
+               (``FlatGradAllReducer.start``), ``finish`` makes the compute stream wait (Work.wait), then
+               the optimizer graph;
   syncbn     ``enable_sync_bn``: every BN's replica sums all-reduced by RCCL inside the step, CAPTURED in the
              step's HIP graph (no eager fallback on RCCL): graph == eager bitwise; after one step the BN running
              statistics equal plain BN's bitwise and the gradients agree to summation order;
@@ -56,8 +57,8 @@ def run(ctx, model_type, X, labels, *, buckets=1, dp=False, sync_bn=False, graph
     autotune_program(prog, measure=False)
     ar = FlatGradAllReducer(ctx) if dp else None
     if ar is not None and not capture_dp:
-        # the multi-rank default (collectives not capturable): per-bucket piece graphs, each bucket's RCCL
-        # all-reduce issued asynchronously between them (FlatGradAllReducer.start / finish)
+        # the multi-rank default (collectives not capturable): one forward + backward graph with an external
+        # event per bucket, each bucket's RCCL all-reduce issued asynchronously behind its event
         ar.capturable = False
     runner = StepRunner(prog, X, labels, use_graph=graph, allreduce=ar)
     runner.set_lr(1e-3)
@@ -76,7 +77,7 @@ def run(ctx, model_type, X, labels, *, buckets=1, dp=False, sync_bn=False, graph
                                                 ("exp_avg_sq", f.exp_avg_sq), ("bn_mean", f.bn_mean),
                                                 ("bn_var", f.bn_var), ("step", f.step))}
     info = {"buckets": nb, "collectives_per_step": n_ar, "ms_per_step": ms, "graphs": sorted(runner.graphs),
-            "captured_dp": runner.capture_dp}
+            "captured_dp": runner.capture_dp, "ext_dp": runner.ext_dp}
     runner.close()
     return state, info
 
@@ -97,9 +98,9 @@ def main():
         ref, _ = run(ctx, model_type, X, labels, buckets=buckets, dp=False)
         got, info = run(ctx, model_type, X, labels, buckets=buckets, dp=True)
         out[f"dp{buckets}"] = dict(info, bitwise={k: bool(torch.equal(ref[k], got[k])) for k in ref})
-        # the world > 1 default path on RCCL: piece graphs + async bucket all-reduces + Work.wait
+        # the world > 1 default path on RCCL: one graph with external bucket events + async bucket all-reduces
         got, info = run(ctx, model_type, X, labels, buckets=buckets, dp=True, capture_dp=False)
-        out[f"dp{buckets}_pieces"] = dict(info, bitwise={k: bool(torch.equal(ref[k], got[k])) for k in ref})
+        out[f"dp{buckets}_ext"] = dict(info, bitwise={k: bool(torch.equal(ref[k], got[k])) for k in ref})
     # SyncBN: collectives inside the step's graph
     eager, _ = run(ctx, model_type, X, labels, sync_bn=True, graph=False, steps=2)
     graph, info = run(ctx, model_type, X, labels, sync_bn=True, graph=True, steps=2)

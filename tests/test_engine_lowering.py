@@ -362,45 +362,6 @@ def test_stream_slots_count_comm_and_spill_in_the_queue_budget():
     assert sorted(set(m.values())) == [0, 1, 2, MAX_STREAMS]
 
 
-def _issue_check(ph, order):
-    pos = {id(l): i for i, l in enumerate(order)}
-    assert sorted(pos.values()) == list(range(len(ph.launches)))
-    for s in {l.stream for l in ph.launches}:  # every stream keeps its own order
-        mine = [pos[id(l)] for l in ph.launches if l.stream == s]
-        assert mine == sorted(mine)
-    rec = {l.record: pos[id(l)] for l in ph.launches if l.record is not None}
-    for l in ph.launches:  # every wait is issued after its record
-        for t in l.waits:
-            assert rec[ph.alias.get(t, t)] < pos[id(l)]
-
-
-@pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
-def test_main_first_issue_order_is_a_valid_schedule(model):
-    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
-    from mtl_das_pytorch_amd.engine.program import Phase
-    from mtl_das_pytorch_amd.models import build_model
-    m = build_model(model)
-    p = InceptionProgram(m, 4, "cpu") if model == "multi_classifier" else MTLProgram(m, 4, "cpu")
-    try:
-        Phase.ISSUE_ORDER = "main_first"
-        for ph in (p.fwd_train, p.bwd, p.fwd_eval):
-            order = ph.issue_order()
-            _issue_check(ph, order)
-            # stream 0 is never behind: a side launch is issued only while stream 0's next launch waits
-            recorded = set()
-            q0 = [l for l in ph.launches if l.stream == 0]
-            k = 0
-            for l in order:
-                if l.stream == 0:
-                    k += 1
-                elif k < len(q0):
-                    assert not all(ph.alias.get(t, t) in recorded for t in q0[k].waits)
-                if l.record is not None:
-                    recorded.add(l.record)
-    finally:
-        Phase.ISSUE_ORDER = "program"
-
-
 def test_executor_schedule_rule_on_a_recorded_dot():
     """graphsched.schedule reproduces the HIP graph executor's StreamId of every node of a recorded
     DEBUG_HIP_GRAPH_DOT_PRINT dump (tools/hwq_repro.py --streams 3 --layers 2 on MI355X: 16 nodes; the
@@ -413,43 +374,6 @@ def test_executor_schedule_rule_on_a_recorded_dot():
     for a, b in edges:
         ch[a].append(b)
     assert gs.schedule(ch, 4) == truth  # recorded with the runtime's default 4 executor streams
-
-
-@pytest.mark.parametrize("model", ["MTL", "multi_classifier"])
-def test_restream_plan_puts_every_engine_stream_on_its_own_executor_stream(model):
-    """The child-order plan (graphsched.plan_children) makes the emulated executor assignment equal the
-    engine's streams on the captured step's DAG, only by reordering / adding redundant edges."""
-    from mtl_das_pytorch_amd.engine import graphsched as gs
-    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
-    from mtl_das_pytorch_amd.models import build_model
-    m = build_model(model)
-    p = InceptionProgram(m, 4, "cpu") if model == "multi_classifier" else MTLProgram(m, 4, "cpu")
-    recs = gs.launch_records([p.fwd_train, p.bwd, p.opt["adam"]])
-    nodes, ch = gs.capture_dag(recs)
-    ranks = {}
-    for r in recs:
-        ranks.setdefault(r["phase"], set()).add(r["stream"])
-    tgt = [sorted(ranks[r["phase"]]).index(r["stream"]) for r in nodes]
-    n, bad = gs.restream_check(ch, tgt, 4)
-    assert bad > 0  # the capture order alone leaves streams mixed (what the timelines showed)
-    new, _ = gs.plan_children(ch, tgt, 4)
-    assert gs.restream_check(new, tgt, 4) == (n, 0)
-    assert all(set(a) <= set(b) for a, b in zip(ch, new))  # every dependency kept
-    # the added edges are redundant: each new child was already a descendant
-    desc = [None] * len(ch)
-
-    def reach(v):
-        if desc[v] is None:
-            s = set()
-            for c in ch[v]:
-                s.add(c)
-                s |= reach(c)
-            desc[v] = s
-        return desc[v]
-    import sys
-    sys.setrecursionlimit(10000)
-    for v, (a, b) in enumerate(zip(ch, new)):
-        assert set(b) - set(a) <= reach(v)
 
 
 @pytest.mark.parametrize("model", ["A", "C"])
@@ -465,3 +389,36 @@ def test_executor_schedule_rule_on_recorded_step_dumps_at_two_streams(model):
     assert gs.schedule(d["children"], 2) == d["stream"]
     if model == "C":
         assert gs.schedule(d["children"], 4) != d["stream"]
+
+
+@pytest.mark.parametrize("model", ["MTL", "single_distance"])
+def test_stream_buckets_need_no_cut(model):
+    """The multi-rank DP step's buckets (LoweredProgram.stream_buckets): the first is a prefix of the flat
+    gradient written only on stream 1, complete at stream 1's own finalize (its external event follows that
+    launch, no stream join); the remainder completes at the tail finalize.  Model A: the level parameters."""
+    from mtl_das_pytorch_amd.engine.core import P
+    from mtl_das_pytorch_amd.engine.lowering import _grad_offsets
+    from mtl_das_pytorch_amd.models import build_model
+    m = build_model(model)
+    p = MTLProgram(m, 32, "cpu")
+    p.set_optimizer(weight_decay=1e-5, data_parallel=True)
+    p.segment_backward(1)
+    p.merge_wgrad_cfgs()
+    p.refresh_wgrad_finalize()
+    p.batch_wgrads()
+    b = p.stream_buckets(2)
+    f, ls = p.flat, p.bwd.launches
+    assert len(b) == 2 and b[0][0] == 0 and b[0][1] == b[1][0] and b[1][1] == f.numel and b[0][1] > f.numel // 5
+    a0, a1 = p.bucket_anchors
+    assert a0.name == a1.name == "wgrad_finalize" and a0.stream == 1 and a1 is ls[-1]
+    i0 = next(i for i, l in enumerate(ls) if l is a0)
+    gbase = P(f.grads)
+    for i, l in enumerate(ls):  # nothing writes bucket 0 after stream 1's finalize, or on another stream
+        offs = _grad_offsets(l, gbase, f.numel) if l.name != "wgrad_finalize" else \
+            [f.off(mm.weight) for c in (l.owner or p.convs) for mm in c.mods]
+        if any(o < b[0][1] for o in offs):
+            assert l.stream == 1 and i <= i0, (i, l.name, l.stream)
+    ph = p.backward_with_ext_events(["e0", "e1"])
+    recs = [(i, l.args[0]) for i, l in enumerate(ph.launches) if l.name == "ext_record"]
+    assert [e for _, e in recs] == ["e0", "e1"]
+    assert ph.launches[recs[0][0] - 1] is a0 and ph.launches[recs[0][0]].stream == 1

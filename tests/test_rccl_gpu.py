@@ -1,7 +1,8 @@
 """The RCCL collective path executed on one MI355X: a 1-rank RCCL process
 group (MDA_DIST_BACKEND=nccl, WORLD_SIZE=1) carries bench.py's DP step in both of its forms -- the bucket
-all-reduces captured inside the step graph (the 1-rank default) and the world > 1 default, per-bucket
-backward piece graphs with asynchronous RCCL all-reduces and Work.wait -- and graph-captured SyncBN.  Multi-rank correctness is covered by the gloo
+all-reduces captured inside the step graph (the 1-rank default) and the world > 1 default, one forward +
+backward graph with external bucket events behind which asynchronous RCCL all-reduces run (Work.wait) -- and
+graph-captured SyncBN.  Multi-rank correctness is covered by the gloo
 tests (tests/test_dp_engine_gpu.py, tests/test_dist.py); this one proves the RCCL-specific code: the
 communicator, stream-ordered collectives, Work.wait stream semantics, barrier(device_ids) and collective
 capture inside a HIP graph."""
@@ -35,13 +36,12 @@ def test_rccl_one_rank_dp_and_syncbn(model):
     assert res["enabled"] and res["backend"] == "nccl" and res["world"] == 1
     nbk = 4 if model == "multi_classifier" else 2
     for b in (1, nbk):
-        for form in ("", "_pieces"):
+        for form in ("", "_ext"):
             r = res[f"dp{b}{form}"]
             assert r["buckets"] == b
-            assert r["captured_dp"] == (form == ""), r
+            assert r["captured_dp"] == (form == "") and r["ext_dp"] == (form == "_ext"), r
             assert all(r["bitwise"].values()), r  # 1-rank RCCL sums are exact: same bits as no collective
-        if b > 1:  # the piece path really ran as per-bucket graphs
-            assert sum(k.startswith("train_piece") for k in res[f"dp{b}_pieces"]["graphs"]) == b
+        assert "train_ext" in res[f"dp{b}_ext"]["graphs"]  # the external-event path really ran
     s = res["syncbn"]
     assert s["collectives_per_step"] > 40  # one per BN forward + one per BN backward ...
     if model == "multi_classifier":  # ... except the Inception blocks' branch outputs: one per block and direction

@@ -54,8 +54,12 @@ case $mode in
       done
     done ;;
   dp)
+    # the per-rank program of an 8-GPU run on a 1-rank RCCL group (bench --dp-shape 8): the model's bucket count
+    # (A: 2 side-stream buckets behind external events) vs one bucket, next to the single-GPU benches
     bench_model A1 MTL && \
     TAILN=2 step A_w8 env MDA_DIST_BACKEND=nccl timeout -k 10 300 python bench.py --steps 300 --warmup 30 --dp-shape 8 && \
+    TAILN=2 step A_w8b1 env MDA_DIST_BACKEND=nccl timeout -k 10 300 python bench.py --steps 300 --warmup 30 --dp-shape 8 --buckets 1 && \
+    TAILN=2 step A_dpnogroup env timeout -k 10 300 python bench.py --steps 300 --warmup 30 --dp-shape 8 --buckets 1 && \
     bench_model C1 multi_classifier && \
     TAILN=2 step C_w8 env MDA_DIST_BACKEND=nccl timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --dp-shape 8 ;;
   prof)

@@ -60,7 +60,7 @@ def main():
         for fn in fns:
             fn()
         torch.cuda.synchronize()
-        g, keep, _ = capture_graph(fns)
+        g, keep = capture_graph(fns)
         g.replay()
         torch.cuda.synchronize()
         best = float("inf")

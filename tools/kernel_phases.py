@@ -121,7 +121,7 @@ def main():
     for fn in fns:
         fn()
     torch.cuda.synchronize()
-    g, keep, _ = capture_graph(fns, restream=False)
+    g, keep = capture_graph(fns)
     for _ in range(args.reps):
         g.replay()
     torch.cuda.synchronize()

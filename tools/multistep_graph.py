@@ -50,7 +50,7 @@ def main():
     res = {}
     for _ in range(2):  # two interleaved rounds
         for k in [int(v) for v in args.k.split(",")]:
-            g, keep, _ = capture_graph(step * k)
+            g, keep = capture_graph(step * k)
             for _ in range(3):
                 g.replay()
             torch.cuda.synchronize()

@@ -57,7 +57,7 @@ def main():
                 fn()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        g, keep, _ = capture_graph(fns)
+        g, keep = capture_graph(fns)
         for _ in range(20):
             g.replay()
         torch.cuda.synchronize()

@@ -83,16 +83,9 @@ def main():
     for fn in fns:
         fn()
     torch.cuda.synchronize()
-    g, keep, info = capture_graph(fns)  # noqa: F841 (the events live as long as the graph)
-    if info:
-        print("restream:", info)
-    rs = torch.cuda.current_stream()
-    if StepRunner.REPLAY_PRIORITY is not None:  # replay as StepRunner does (tools/variant.py)
-        rs = torch.cuda.ExternalStream(lib().stream_create(int(StepRunner.REPLAY_PRIORITY)))
-        rs.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(rs):
-        for _ in range(10):
-            g.replay()
+    g, keep = capture_graph(fns)  # noqa: F841 (the events live as long as the graph)
+    for _ in range(10):
+        g.replay()
     torch.cuda.synchronize()
     snap.restore()
     # clock calibration

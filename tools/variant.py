@@ -2,9 +2,9 @@
 """Run an entry script (default bench.py) with engine class switches or module constants overridden, for
 same-call A/B measurements without per-feature environment knobs:
 
-    python tools/variant.py engine.step.StepRunner.REPLAY_PRIORITY=-1 engine.program.Phase.ISSUE_ORDER=main_first \\
+    python tools/variant.py engine.mtl.MTLProgram.SIDE_WGRAD_GRID=0 engine.core.BN_PX_PER_REP=256 \\
         -- --steps 300 --warmup 30
-    python tools/variant.py --script tools/timeline.py engine.step.StepRunner.REPLAY_PRIORITY=-1 -- MTL
+    python tools/variant.py --script tools/timeline.py engine.mtl.MTLProgram.SIDE_WGRAD_GRID=0 -- MTL
 
 Each override is ``<module under mtl_das_pytorch_amd>.<Class>.<ATTR>=<python literal>`` (or
 ``<module>.<ATTR>=...`` for a module constant); values that are not Python literals are taken as strings.
