@@ -443,9 +443,11 @@ PYBIND11_MODULE(_mda_hip, m) {
     check(launch_philox_kat(reinterpret_cast<const uint32_t*>(static_cast<intptr_t>(ctr)), key,
                             reinterpret_cast<uint32_t*>(static_cast<intptr_t>(out)), n, S(stream)), "philox_kat");
   });
-  m.def("tick", [](int64_t buf, int i, int64_t stream) {
-    check(launch_tick(reinterpret_cast<uint64_t*>(static_cast<intptr_t>(buf)), i, S(stream)), "tick");
-  });
+  m.def("tick", [](int64_t buf, int i, int64_t stream, int64_t n, int64_t q) {
+    if (i < 0 || i >= n) throw std::runtime_error("tick: index outside the stamp buffer");
+    check(launch_tick(reinterpret_cast<uint64_t*>(static_cast<intptr_t>(buf)),
+                      reinterpret_cast<uint64_t*>(static_cast<intptr_t>(q)), i, S(stream)), "tick");
+  }, py::arg("buf"), py::arg("i"), py::arg("stream"), py::arg("n"), py::arg("q") = 0);
   m.def("adam_pack", &adam_pack);
   m.def("hip_device_sync", []() { return (int)hipDeviceSynchronize(); });
   // engine-owned streams (engine/program.py EngineStreams): created once per device, never drawn from

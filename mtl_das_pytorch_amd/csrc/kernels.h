@@ -306,7 +306,7 @@ struct SynthArgs {
 };
 int launch_synth_das(const SynthArgs& a, int n, hipStream_t st);
 int launch_philox_kat(const uint32_t* ctr, uint64_t key, uint32_t* out, int n, hipStream_t st);
-int launch_tick(uint64_t* buf, int i, hipStream_t st);
+int launch_tick(uint64_t* buf, uint64_t* q, int i, hipStream_t st);
 int launch_grad_sum(const GradSrcs& g, bf16_t* out, int ldo, int64_t M, int C, hipStream_t st);
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st);
 

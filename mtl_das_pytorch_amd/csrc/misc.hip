@@ -248,17 +248,17 @@ int launch_pool3(int is_max, int backward, const PoolArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// In-graph timeline stamp (tools/timeline.py): one thread stores the 100 MHz wall clock after the work
-// enqueued before it on its stream -- a profiler-free view of multi-stream graph replays.
-// timeline probe (tools/timeline.py): wall clock at index i, and for i < 4096 the HSA queue the packet was
-// dispatched from at 4096 + i (shows how the HIP graph executor mapped the captured streams onto queues)
-__global__ void tick_kernel(uint64_t* buf, int i) {
+// In-graph timeline stamp (tools/timeline.py): one thread stores the 100 MHz wall clock at buf[i] after the
+// work enqueued before it on its stream -- a profiler-free view of multi-stream graph replays -- and, when q is
+// given, the HSA queue the packet was dispatched from at q[i] (how the HIP graph executor mapped the captured
+// streams onto queues).  The caller sizes both buffers for every index it passes (the binding checks i < n).
+__global__ void tick_kernel(uint64_t* buf, uint64_t* q, int i) {
   buf[i] = wall_clock64();
-  if (i < 4096) buf[4096 + i] = reinterpret_cast<uint64_t>(__builtin_amdgcn_queue_ptr());
+  if (q) q[i] = reinterpret_cast<uint64_t>(__builtin_amdgcn_queue_ptr());
 }
 
-int launch_tick(uint64_t* buf, int i, hipStream_t st) {
-  hipLaunchKernelGGL(tick_kernel, dim3(1), dim3(1), 0, st, buf, i);
+int launch_tick(uint64_t* buf, uint64_t* q, int i, hipStream_t st) {
+  hipLaunchKernelGGL(tick_kernel, dim3(1), dim3(1), 0, st, buf, q, i);
   return (int)hipGetLastError();
 }
 

@@ -245,8 +245,21 @@ class EngineBackend(Backend):
     def set_lr(self, lr: float):
         self.runner.set_lr(lr)
 
-    def train_batch(self, idx: torch.Tensor):
+    def train_batch(self, idx: Optional[torch.Tensor]):
+        """One step on the batch ``idx`` -- or, after set_epoch_schedule and with ``idx`` None, on the schedule's
+        next row."""
         self.runner.train_step(idx)
+
+    def set_epoch_schedule(self, schedule: torch.Tensor):
+        """Train the coming steps from the device-resident [nbatches][B] index schedule (StepRunner.
+        set_index_schedule).  An epoch of the same shape reuses the schedule buffer the captured graph reads
+        (copy + cursor reset, no re-capture)."""
+        r = self.runner
+        if r.schedule is not None and r.schedule.shape == schedule.shape:
+            r.schedule.copy_(schedule)
+            r.cursor.zero_()
+        else:
+            r.set_index_schedule(schedule.to(torch.int64))
 
     def set_eval_data(self, X: torch.Tensor, labels: torch.Tensor):
         self.runner.set_eval_source(X, labels)

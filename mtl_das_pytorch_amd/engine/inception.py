@@ -476,6 +476,7 @@ class InceptionProgram(LoweredProgram):
             if sync:  # the block's partial sums all-reduced between the passes: one collective
                 mid = [Launch("allreduce_bn", k_allreduce, self._sync_allreduce, self._sync_part_groups[blk].t,
                               stream=0)]
+                self._sync_bwd_pending.discard(blk)
             inserts.append((fork_at[blk] + 1, [red] + mid + [app]))
             for t in tails:
                 if t.record is not None:
@@ -496,6 +497,15 @@ class InceptionProgram(LoweredProgram):
         self.bwd.launches = out
         self.n_tail_bwd_batched = n
         return n
+
+    def check_sync_bn(self):
+        """enable_sync_bn drops the per-BN backward collective of every coalesced block's branch-output
+        BNs and leaves ONE per block to batch_tails (autotune_program with batch_wgrads) -- raise if a step would
+        run without it (those BNs would silently train on per-rank statistics).  StepRunner calls this."""
+        pending = getattr(self, "_sync_bwd_pending", None)
+        if pending:
+            raise RuntimeError(f"SyncBN: the coalesced backward collective of {len(pending)} Inception blocks was never "
+                               "inserted -- run batch_tails (autotune_program(..., batch_wgrads=True)) before stepping")
 
     def _tail_bwd_groups(self):
         """The block-output BN-tail backward launches batch_tails batches, per block (keyed by the block's
@@ -525,8 +535,10 @@ class InceptionProgram(LoweredProgram):
         by_buf = {id(buf): (buf, bns) for buf, bns in self._part_groups.values()}
         for blk, tails in groups.items():
             bufs = {id(t.owner.bn.part) for t in tails}
-            if len(bufs) == 1 and len(by_buf[next(iter(bufs))][1]) == len(tails):
+            if self.tail_batch_enabled() and len(bufs) == 1 and len(by_buf[next(iter(bufs))][1]) == len(tails):
                 self._sync_part_groups[blk] = by_buf[next(iter(bufs))][0]
+        # the blocks whose backward collective batch_tails must still insert (check_sync_bn)
+        self._sync_bwd_pending = set(self._sync_part_groups)
         skip_bwd = {P(t.owner.bn.part, t.owner.bn.part_off) for blk in self._sync_part_groups for t in groups[blk]}
         n = super().enable_sync_bn(allreduce, skip_fwd=skip_fwd, skip_bwd=skip_bwd)
         self._sync_allreduce = allreduce

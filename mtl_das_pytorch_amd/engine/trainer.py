@@ -251,7 +251,15 @@ class Trainer:
         last = be.read_metrics()
         prof = self._maybe_profiler(epoch)
         t_log = time.perf_counter()
-        for bi, (idx, _) in enumerate(self.train_src.batches(batches)):
+        if hasattr(be, "set_epoch_schedule") and isinstance(self.train_src, ResidentSource) and batches:
+            # the engine trains from a device-resident schedule of the epoch's batch indices (one copy per epoch;
+            # the step's gather reads the next row, its optimizer kernel advances the cursor): the step bench.py
+            # times, with no host-issued index copy before each graph replay
+            be.set_epoch_schedule(torch.stack(batches).to(self.device))
+            steps = ((None, len(b)) for b in batches)
+        else:
+            steps = self.train_src.batches(batches)
+        for bi, (idx, _) in enumerate(steps):
             if self.fault is not None and self.global_step == self.fault:
                 print(f"fault injection: rank {self.ctx.rank} exits at global step {self.global_step}",
                       file=sys.stderr, flush=True)

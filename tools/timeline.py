@@ -26,8 +26,11 @@ from mtl_das_pytorch_amd.models import build_model, encode_joint  # noqa: E402
 from mtl_das_pytorch_amd.ops.hip import lib  # noqa: E402
 
 
-def k_tick(buf, i, st):
-    lib().tick(buf, i, st)
+NSTAMP = 4096  # launches a timeline can stamp (the queue-id buffer has one slot per stamp)
+
+
+def k_tick(buf, qbuf, i, st):
+    lib().tick(buf, i, st, NSTAMP + 2, qbuf)
 
 
 def shape_of(l):
@@ -60,7 +63,8 @@ def main():
     idx = torch.arange(32, device="cuda")
     p.flat.lr.fill_(1e-3)
     p.opt["pack"].run()
-    buf = torch.zeros(8192, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(NSTAMP + 2, dtype=torch.int64, device="cuda")  # + 2 clock-calibration stamps
+    qbuf = torch.zeros(NSTAMP, dtype=torch.int64, device="cuda")
     labels = []
 
     def instrument(ph, tag):
@@ -70,7 +74,9 @@ def main():
             if l.fn is None:
                 continue
             labels.append((tag, l.name, l.stream, shape_of(l)))
-            new.append(Launch("tick", k_tick, buf.data_ptr(), len(labels) - 1, stream=l.stream))
+            if len(labels) > NSTAMP:
+                raise SystemExit(f"timeline: more than {NSTAMP} launches to stamp")
+            new.append(Launch("tick", k_tick, buf.data_ptr(), qbuf.data_ptr(), len(labels) - 1, stream=l.stream))
         ph.launches = new
 
     gather = p.gather_phase(X, lab, idx)
@@ -90,15 +96,15 @@ def main():
     snap.restore()
     # clock calibration
     st = torch.cuda.current_stream().cuda_stream
-    lib().tick(buf.data_ptr(), 8190, st)
+    lib().tick(buf.data_ptr(), NSTAMP, st, NSTAMP + 2)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     time.sleep(0.2)
-    lib().tick(buf.data_ptr(), 8191, st)
+    lib().tick(buf.data_ptr(), NSTAMP + 1, st, NSTAMP + 2)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     t = buf.cpu().tolist()
-    mhz = (t[8191] - t[8190]) / dt / 1e6
+    mhz = (t[NSTAMP + 1] - t[NSTAMP]) / dt / 1e6
     n = len(labels)
     base = min(t[:n])
     us = [(t[i] - base) / mhz for i in range(n)]
@@ -106,7 +112,8 @@ def main():
     # the HSA queue each tick was dispatched from: how the graph executor mapped the captured (logical)
     # streams onto its own streams / hardware queues
     qids = {}
-    q = [qids.setdefault(t[4096 + i], len(qids)) if i < 4096 else -1 for i in range(n)]
+    tq = qbuf.cpu().tolist()
+    q = [qids.setdefault(tq[i], len(qids)) for i in range(n)]
     per = {}
     for i in range(n):
         per.setdefault(labels[i][2], {}).setdefault(q[i], 0)
