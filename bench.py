@@ -224,7 +224,10 @@ def main():
     # cannot measure N's all-reduce: it takes the model's default bucket count)
     # (--buckets K on one GPU runs the same bucketed graph with no-op collectives: measures the split's cost)
     shape = max(world, args.dp_shape)
-    captured = ctx.capturable_collectives and args.dp_shape <= 1  # the form the step's collectives take
+    # the form the step's collectives take: captured in the step graph (one-rank groups; SyncBN, whose in-step
+    # collectives are always captured where the group can -- the gradient buckets then share the capture
+    # communicator), else eager behind the graph's external bucket events (the multi-rank default)
+    captured = ctx.capturable_collectives and (sync or (ctx.capture_gradients and args.dp_shape <= 1))
     ar_ms = calibrate_allreduce(ctx, prog.flat.numel)
     nb = prog.dp_buckets(shape, ar_ms if world > 1 else None) if args.buckets is None else args.buckets
     # captured collectives: the backward cut at the bucket boundaries (segment_backward); eager RCCL behind the
@@ -239,9 +242,7 @@ def main():
     broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
     X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev, in_channels=args.in_channels)
     labels = encode_joint(d, e) if joint else torch.stack([d, e], 1)
-    reducer = FlatGradAllReducer(ctx) if (ctx.enabled or len(buckets) > 1) else None
-    if reducer is not None and args.dp_shape > 1:
-        reducer.capturable = False  # what a multi-rank group runs (DistContext.capturable_collectives)
+    reducer = FlatGradAllReducer(ctx, capture=captured) if (ctx.enabled or len(buckets) > 1) else None
     runner = StepRunner(prog, X, labels, use_graph=not args.no_graph and (not sync or captured), allreduce=reducer)
     runner.set_lr(1e-3 / 1.5)  # reference: lr/1.5 applied at the epoch-0 validation
     sampler = ShardedIndexSampler(args.dataset_size * world, args.batch, ctx, seed=7)

@@ -215,11 +215,11 @@ class EngineBackend(Backend):
         if sync:  # SyncBN: BN statistics all-reduced inside the step (captured into the HIP graph on RCCL)
             self.prog.enable_sync_bn(ctx.all_reduce_ordered_)
             if not ctx.capturable_collectives:
-                # gloo, or RCCL with several ranks (capture opt-in: MDA_CAPTURE_COLLECTIVES=1): the step runs
-                # its launches and collectives eagerly -- say so, this is several times slower
+                # gloo (or MDA_CAPTURE_COLLECTIVES=0): the step runs its launches and collectives eagerly -- say
+                # so, this is several times slower
                 if ctx.is_main:
                     print("SyncBN: collectives are not captured on this process group; the training step runs "
-                          "eagerly (set MDA_CAPTURE_COLLECTIVES=1 on RCCL to capture them)", flush=True)
+                          "eagerly", flush=True)
                 use_graph = False
         self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world,
                                 data_parallel=ctx.enabled)
@@ -228,7 +228,8 @@ class EngineBackend(Backend):
         nb = self.prog.dp_buckets(ctx.world, calibrate_allreduce(ctx, self.prog.flat.numel))
         # captured collectives (a 1-rank RCCL group): the backward cut at the bucket boundaries; several ranks
         # (eager RCCL behind the step graph's external bucket events): side-stream buckets, no cut
-        ext_form = ctx.enabled and not ctx.capturable_collectives and use_graph
+        captured = ctx.capturable_collectives and (sync or ctx.capture_gradients)
+        ext_form = ctx.enabled and not captured and use_graph
         self.prog.segment_backward(1 if ext_form else nb)
         autotune_program(self.prog, measure=tune)
         if ext_form and nb > 1:
@@ -237,7 +238,7 @@ class EngineBackend(Backend):
         broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
         lab_eval = labels_eval if labels_eval is not None else labels
         self.runner = StepRunner(self.prog, X, labels, use_graph=use_graph,
-                                 allreduce=FlatGradAllReducer(ctx) if ctx.enabled else None,
+                                 allreduce=FlatGradAllReducer(ctx, capture=captured) if ctx.enabled else None,
                                  X_eval=X_eval if X_eval is not None else X, labels_eval=lab_eval)
         self.runner.set_lr(lr)
         self.B = batch

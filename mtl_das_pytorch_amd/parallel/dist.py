@@ -50,11 +50,19 @@ class DistContext:
 
     @property
     def capturable_collectives(self) -> bool:
-        """Collectives can be captured into a HIP graph (RCCL: stream-ordered device collectives); gloo's
-        host round trip cannot, so a step with in-step collectives (SyncBN) then runs eagerly.  With more
-        than one rank the captured form is opt-in (``MDA_CAPTURE_COLLECTIVES=1``): it has been validated on
-        one-rank RCCL groups only, and the eager form is the known-good default there."""
+        """Collectives can be captured into a HIP graph (RCCL: stream-ordered device collectives, run on the
+        capture-only communicator ``capture_group``); gloo's host round trip cannot.  SyncBN's in-step
+        collectives are captured whenever this holds (the eager alternative is ~10x slower); the gradient
+        buckets only where ``capture_gradients`` says so.  MDA_CAPTURE_COLLECTIVES=0 disables capture."""
         return self.capture_group is not None
+
+    @property
+    def capture_gradients(self) -> bool:
+        """The gradient buckets' all-reduces are captured in the step graph: one-rank groups, or several ranks
+        with MDA_CAPTURE_COLLECTIVES=1.  The multi-rank default keeps them eager behind the graph's external
+        bucket events (engine/step.py "train_ext"): multi-rank RCCL graph capture could not be validated on
+        the one-GPU machines this was built on, the eager RCCL path is the known-good one."""
+        return self.capturable_collectives and (self.world == 1 or os.environ.get("MDA_CAPTURE_COLLECTIVES") == "1")
 
     @property
     def is_main(self) -> bool:
@@ -177,11 +185,10 @@ def _rccl_options():
 
 
 def _with_capture_group(ctx: DistContext) -> DistContext:
-    """Create the capture-only RCCL communicator (DistContext.capture_group) where captured collectives are
-    used: one-rank groups always, several ranks with MDA_CAPTURE_COLLECTIVES=1.  Every rank makes the same
-    call (new_group is collective); the default group is bound to the device, so the new communicator is
-    initialised eagerly here -- never lazily inside a capture."""
-    if ctx.backend == "nccl" and (ctx.world == 1 or os.environ.get("MDA_CAPTURE_COLLECTIVES") == "1"):
+    """Create the capture-only RCCL communicator (DistContext.capture_group) on RCCL groups (unless
+    MDA_CAPTURE_COLLECTIVES=0).  Every rank makes the same call (new_group is collective); the default group is
+    bound to the device, so the new communicator is initialised eagerly here -- never lazily inside a capture."""
+    if ctx.backend == "nccl" and os.environ.get("MDA_CAPTURE_COLLECTIVES") != "0":
         ctx.capture_group = dist.new_group(backend="nccl", pg_options=_rccl_options())
     return ctx
 
@@ -195,13 +202,16 @@ def shutdown(ctx: DistContext):
 class FlatGradAllReducer:
     """All-reduce(SUM) of a flat gradient buffer in ``bucket_mb`` chunks (0 = one bucket)."""
 
-    def __init__(self, ctx: DistContext, bucket_mb: float = 0.0):
+    def __init__(self, ctx: DistContext, bucket_mb: float = 0.0, capture: Optional[bool] = None):
         self.ctx = ctx
         self.bucket_elems = int(bucket_mb * 2 ** 20 / 4) if bucket_mb > 0 else 0
         self._pending = []
         # the bucket all-reduces may be embedded in the step's HIP graph (engine/step.py "train_full_dp"):
-        # ``ordered`` is then the stream-ordered form the captured launches call
-        self.capturable = ctx.capturable_collectives and os.environ.get("MDA_DP_CAPTURE", "1") == "1"
+        # ``ordered`` is then the stream-ordered form the captured launches call.  Default: where the group
+        # captures gradients (DistContext.capture_gradients); ``capture=True`` where every collective of the
+        # step must share the capture communicator (SyncBN's captured collectives), if the group can capture
+        want = ctx.capture_gradients if capture is None else (capture and ctx.capturable_collectives)
+        self.capturable = want and os.environ.get("MDA_DP_CAPTURE", "1") == "1"
         self.ordered = ctx.all_reduce_ordered_
 
     def start(self, t: torch.Tensor):

@@ -54,13 +54,18 @@ def gather_cpu(t):
 def main():
     model_type, nbuckets = sys.argv[1], int(sys.argv[2])
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    # "stream": the multi-rank production form (uncut backward, side-stream buckets: stream_buckets);
+    # "cut": segment_backward's cut backward
+    form = sys.argv[4] if len(sys.argv) > 4 else "stream"
     ctx = init_distributed()
     world, dev = ctx.world, ctx.device
     B = 32
     prog, joint = build(model_type, B, dev, nbuckets)
     prog.set_optimizer(betas=(B1, B2), eps=EPS, weight_decay=WD, grad_scale=1.0 / world, data_parallel=True)
-    buckets = prog.segment_backward(nbuckets)
+    buckets = prog.segment_backward(nbuckets if form == "cut" else 1)
     autotune_program(prog, measure=False)
+    if form == "stream" and nbuckets > 1:
+        buckets = prog.stream_buckets(nbuckets)
     f = prog.flat
     broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
     X, d, e = generate(4 * B, seed=100 + ctx.rank, device=dev)  # different data on every rank
@@ -105,7 +110,7 @@ def main():
             if not all(torch.equal(parts[0], q) for q in parts[1:]):
                 raise AssertionError(f"step {s}: ranks disagree on {name}")
     print(json.dumps({"rank": ctx.rank, "steps": steps, "max_grad_rel": worst_g, "max_adam_abs": worst_a,
-                      "buckets": [list(b) for b in buckets]}), flush=True)
+                      "buckets": [list(b) for b in buckets], "ext_dp": runner.ext_dp}), flush=True)
     shutdown(ctx)
 
 

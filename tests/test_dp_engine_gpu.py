@@ -1,7 +1,8 @@
 """Data parallelism through the HIP engine, rehearsed on ONE MI355X: two ranks on
 cuda:0 (MDA_SINGLE_DEVICE=1) with gloo carrying the collectives (RCCL refuses two ranks on one device).
-Everything else is the production DP path: per-bucket backward graphs, asynchronous bucket all-reduces
-overlapping the next piece, 1/world folded into the fused Adam, rank-0 I/O, BN-statistics averaging."""
+Everything else is the production DP path: one forward + backward graph with external bucket events,
+asynchronous bucket all-reduces behind them overlapping the rest of the backward, 1/world folded into the
+fused Adam, rank-0 I/O, BN-statistics averaging."""
 import glob
 import json
 import re
@@ -39,15 +40,18 @@ def _torchrun(args, cwd, timeout=240):
     return r.stdout
 
 
-@pytest.mark.parametrize("model,buckets", [("MTL", 2), ("MTL", 1), ("multi_classifier", 4)])
-def test_engine_dp_gradients_and_sync(model, buckets):
+@pytest.mark.parametrize("model,buckets,form", [("MTL", 2, "stream"), ("MTL", 2, "cut"), ("MTL", 1, "stream"),
+                                                ("multi_classifier", 4, "cut")])
+def test_engine_dp_gradients_and_sync(model, buckets, form):
     """3 DP steps: the reduced gradient is the sum of the ranks' single-process gradients, the fused Adam
-    applies exactly its mean, and both ranks end every step with bitwise-identical weights and moments."""
-    out = _torchrun([os.path.join(ROOT, "tests", "dp_engine_worker.py"), model, str(buckets), "3"], ROOT)
+    applies exactly its mean, and both ranks end every step with bitwise-identical weights and moments.  form
+    "stream": the multi-rank default (side-stream buckets, LoweredProgram.stream_buckets); "cut": the backward
+    cut at the bucket boundaries (segment_backward)."""
+    out = _torchrun([os.path.join(ROOT, "tests", "dp_engine_worker.py"), model, str(buckets), "3", form], ROOT)
     res = _json_rows(out)
     assert len(res) == 2, out
     for r in res:
-        assert len(r["buckets"]) == buckets
+        assert len(r["buckets"]) == buckets and r["ext_dp"]
         # different wgrad tile batching per bucket sums the split-M partials in another order: fp32 noise
         assert r["max_grad_rel"] < 1e-5, r
         assert r["max_adam_abs"] < 1e-6, r
@@ -123,3 +127,17 @@ def test_bench_contract_two_ranks(model):
     assert r["value"] > 0 and r["higher_is_better"] is True and r["scaling"] == "weak", r
     assert abs(r["value"] - 64 / (r["ms_per_step"] / 1e3)) / r["value"] < 0.02, r
     assert r["captured_collectives"] is False and r["dist_backend"] == "gloo", r
+    assert r["dp_overlap"] == "ext_events" and r["allreduce_ms"] is not None, r
+
+
+def test_bench_self_launch_two_ranks_on_the_gpu():
+    """``bench.py --gpus 2`` with no launcher starts its own two ranks (here both on cuda:0 over gloo, as a
+    1-GPU box allows): one JSON line, dp2."""
+    env = dict(os.environ, MDA_SINGLE_DEVICE="1", MDA_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2",
+                        "--heldout", "0"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["config"]["parallelism"] == "dp2", r.stdout

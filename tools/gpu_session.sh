@@ -59,9 +59,10 @@ case $mode in
     bench_model A1 MTL && \
     TAILN=2 step A_w8 env MDA_DIST_BACKEND=nccl timeout -k 10 300 python bench.py --steps 300 --warmup 30 --dp-shape 8 && \
     TAILN=2 step A_w8b1 env MDA_DIST_BACKEND=nccl timeout -k 10 300 python bench.py --steps 300 --warmup 30 --dp-shape 8 --buckets 1 && \
-    TAILN=2 step A_dpnogroup env timeout -k 10 300 python bench.py --steps 300 --warmup 30 --dp-shape 8 --buckets 1 && \
+    TAILN=2 step A_w8sbn env MDA_DIST_BACKEND=nccl timeout -k 10 300 python bench.py --steps 300 --warmup 30 --dp-shape 8 --sync_bn && \
     bench_model C1 multi_classifier && \
-    TAILN=2 step C_w8 env MDA_DIST_BACKEND=nccl timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --dp-shape 8 ;;
+    TAILN=2 step C_w8 env MDA_DIST_BACKEND=nccl timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --dp-shape 8 && \
+    TAILN=2 step C_w8sbn env MDA_DIST_BACKEND=nccl timeout -k 10 300 python bench.py --model multi_classifier --steps 100 --warmup 20 --dp-shape 8 --sync_bn ;;
   prof)
     source tools/profile_round.sh
     prof_model "${1:-MTL}" "${2:-A}" ;;
