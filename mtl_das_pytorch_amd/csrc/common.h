@@ -71,6 +71,21 @@ DEV int fdiv24(int n, int d, float inv) {
   return q;
 }
 
+// Transposed LDS read for the 16x16x32 MFMA operands (ds_read_b64_tr_b16): rows r..r+3 and r+HI..r+HI+3 (two
+// 4-row transposed reads), 16 columns col0..col0+15.  Lane 4q+p of each 16-lane group supplies &row[q][col0 + 4p];
+// lane i receives column col0+i.
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+template <int HI = 4>
+DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const bf16_t* a0 = lds_row0 + q * ld_elems + col0 + 4 * p;
+  const bf16_t* a1 = a0 + HI * ld_elems;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a1));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 // round-to-nearest-even; NaN-preserving via the hardware conversion
 DEV bf16_t f2bf(float f) {

@@ -410,21 +410,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
-
-template <int HI = 4>
-DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
-  // Rows r..r+3 and r+HI..r+HI+3 (two 4-row transposed reads), 16 columns col0..col0+15.
-  // Lane 4q+p of each 16-lane group supplies &row[q][col0 + 4p]; lane i receives column col0+i.
-  const int i = lane & 15, q = i >> 2, p = i & 3;
-  const bf16_t* a0 = lds_row0 + q * ld_elems + col0 + 4 * p;
-  const bf16_t* a1 = a0 + HI * ld_elems;
-  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
-  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a1));
-  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
-
 // Staging of one im2col weight-gradient chunk (MCH pixels): dy [MCH][TN] and the im2col rows [MCH][TK] of
 // the forward input, loaded by 16-byte units into registers (so that the next chunk's loads are in flight
 // while this chunk's MFMAs run) and stored into pixel-major LDS images, with the normalise-on-load
@@ -1088,6 +1073,7 @@ int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8, int& R) {
 }
 
 int wgrad_ntiles(int cfg, const WgradArgs& a) {
+  if (cfg >= WGRAD_LEAN_CFG0 && cfg < WGRAD_LEAN_CFG0 + WGRAD_LEAN_NCFG) return wgrad_lean_ntiles(cfg, a);
   int TN, TK, CB, W8, R;
   if (!wgrad_patch_shape(cfg, TN, CB, W8, R)) {
     const int Wo8 = (a.Wo + 7) & ~7;
@@ -1104,6 +1090,7 @@ int wgrad_ntiles(int cfg, const WgradArgs& a) {
 }
 
 int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st) {
+  if (cfg >= WGRAD_LEAN_CFG0 && cfg < WGRAD_LEAN_CFG0 + WGRAD_LEAN_NCFG) return launch_wgrad_lean(a, G, cfg, st);
   if (cfg >= WGRAD_BIG_CFG0) {
     const int nt = wgrad_ntiles(cfg, a);
     if (nt < 0) return nt;
@@ -1157,6 +1144,8 @@ int wgrad_tile_shape(int cfg, int& TN, int& TK) {
 int launch_wgrad_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, hipStream_t st, int64_t cap) {
   if (nblocks <= 0) return 0;
   dim3 grid((unsigned)(cap > 0 && cap < nblocks ? cap : nblocks));
+  if (cfg >= WGRAD_LEAN_CFG0 && cfg < WGRAD_LEAN_CFG0 + WGRAD_LEAN_NCFG)
+    return launch_wgrad_lean_batched(cfg, d_jobs, nj, nblocks, grid, st);
   if (cfg >= WGRAD_BIG_CFG0) {
 #define LAUNCH_WGBIGB(TN, TK)                                                                                 \
   hipLaunchKernelGGL((conv_wgrad_big_batched_kernel<TN, TK>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \

@@ -273,6 +273,11 @@ int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st);
 int wgrad_tile_shape(int cfg, int& TN, int& TK);
 constexpr int WGRAD_PATCH_CFG0 = 12, WGRAD_PATCH_NCFG = 8;  // wgrad cfgs 12-19: 3x3/s1 patch kernels (conv.hip)
 constexpr int WGRAD_BIG_CFG0 = 32, WGRAD_BIG_NCFG = 4;  // wgrad cfgs 32-35: 32x32x16 large-tile kernels
+constexpr int WGRAD_LEAN_CFG0 = 36, WGRAD_LEAN_NCFG = 8;  // wgrad cfgs 36-43: lean-staging im2col (wgrad_lean.hip)
+int wgrad_lean_shape(int cfg, int& TN, int& TK);
+int wgrad_lean_ntiles(int cfg, const WgradArgs& a);
+int launch_wgrad_lean(const WgradArgs& a, int G, int cfg, hipStream_t st);
+int launch_wgrad_lean_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, dim3 grid, hipStream_t st);
 int wgrad_patch_shape(int cfg, int& TN, int& CB, int& W8, int& R);
 int wgrad_ntiles(int cfg, const WgradArgs& a);  // tiles per group of a wgrad launch, < 0: cfg invalid for a
 // cap > 0: at most cap hardware blocks walk the nblocks virtual blocks (persistent grid)

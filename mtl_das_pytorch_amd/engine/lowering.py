@@ -74,9 +74,10 @@ class LoweredProgram:
     default_buckets = 1  # gradient buckets under data parallelism (segment_backward); MDA_BUCKETS overrides
     LOCAL_BUCKETS = 1    # the same segmentation of the backward in a single process (no collectives)
 
-    # a measured all-reduce of the whole flat gradient shorter than this is not worth a bucket cut (each extra
-    # bucket costs a finalize launch and an event join on stream 0)
-    OVERLAP_MIN_MS = 0.02
+    # a measured all-reduce of the whole flat gradient shorter than this stays one bucket: each further bucket
+    # adds an eager collective's event / stream hops (~20 us per step, profiles/r6_dp_rehearsal.md) and pays only
+    # when the overlapped share of the all-reduce (A: 40 %) exceeds that
+    OVERLAP_MIN_MS = 0.05
 
     def dp_buckets(self, world: int, allreduce_ms: Optional[float] = None) -> int:
         """Gradient buckets of a data-parallel step of ``world`` ranks.  Every form of the step overlaps the

@@ -229,8 +229,13 @@ WGRAD_TILES = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 
                8: (16, 192, 64), 9: (16, 128, 64), 10: (32, 192, 64), 11: (32, 320, 32),  # (TN, TK, MCH)
                # large tiles on the 32x32x16 MFMA (csrc/conv.hip wgrad_big_block); their last K tile may be
                # partial
-               32: (64, 64, 64), 33: (64, 128, 64), 34: (128, 64, 64), 35: (128, 128, 64)}
+               32: (64, 64, 64), 33: (64, 128, 64), 34: (128, 64, 64), 35: (128, 128, 64),
+               # lean-staging im2col tiles (csrc/wgrad_lean.hip: per-chunk pixel table in LDS, per-thread staging
+               # constants, branch-free loads); partial last K tile
+               36: (16, 64, 64), 37: (16, 144, 64), 38: (32, 64, 64), 39: (32, 144, 64), 40: (64, 64, 64),
+               41: (64, 128, 64), 42: (128, 64, 64), 43: (128, 128, 64)}
 WGRAD_BIG0 = 32
+WGRAD_LEAN0, WGRAD_LEAN_N = 36, 8
 
 
 def wgrad_ktiles(cfg: int, Kpad: int) -> int:

@@ -189,6 +189,53 @@ def test_conv_wgrad_big_two_segment(fn, cfg):
     assert rel(dw, wr.grad) < 5e-3
 
 
+@pytest.mark.parametrize("case", [(2, 33, 83, 16, 16, 3, 1, 1), (2, 17, 42, 32, 32, 3, 1, 1), (2, 33, 83, 16, 64, 3, 2, 1),
+                                  (2, 5, 11, 128, 128, 3, 1, 1), (2, 4, 13, 64, 96, (1, 7), 1, (0, 3)),
+                                  (2, 4, 13, 64, 48, (7, 1), 1, (3, 0)), (2, 23, 60, 80, 192, 3, 1, 0),
+                                  (2, 5, 11, 256, 64, 1, 1, 0), (2, 33, 83, 8, 16, 1, 1, 0), (3, 9, 21, 32, 24, 3, 2, 1)])
+@pytest.mark.parametrize("cfg", list(range(36, 44)))
+@pytest.mark.parametrize("nol", [False, True])
+def test_conv_wgrad_lean(fn, case, cfg, nol):
+    """Lean-staging weight gradients (configs 36-43, csrc/wgrad_lean.hip: per-chunk pixel table in LDS,
+    per-thread staging constants, branch-free loads): 16-128-row tiles with Cout below / not a multiple of the
+    tile, K tiles past the padded reduction (144-wide tiles over Kpad 192 / 320 ...), strided and rectangular
+    kernels, valid padding, 1x1 convs, pixel counts that end mid-chunk, and normalise-on-load of the input."""
+    B, H, W, C, Co, k, s, p = case
+    x, w, _, _, _ = _mk(case, seed=cfg + 21)
+    g = torch.Generator().manual_seed(cfg + 23)
+    ref_y = F.conv2d(x, w, stride=s, padding=p)
+    dy = torch.randn(ref_y.shape, generator=g).bfloat16().float().cuda()
+    if nol:
+        consts = torch.zeros(1, 4, C, device="cuda")
+        consts[0, 0] = torch.rand(C, generator=g).cuda() + 0.5
+        consts[0, 1] = torch.randn(C, generator=g).cuda() * 0.3
+        act = F.relu(x * consts[0, 0].view(1, -1, 1, 1) + consts[0, 1].view(1, -1, 1, 1)).bfloat16().float()
+    else:
+        act = x
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(act, wr, stride=s, padding=p).backward(dy)
+    kw = {"nol": (consts, 1)} if nol else {}
+    dw = fn.conv2d_wgrad(nhwc(x).bfloat16(), nhwc(dy).bfloat16(), w.shape, stride=s, padding=p, cfg=cfg, **kw)
+    assert rel(dw, wr.grad) < 5e-3
+    ref = fn.conv2d_wgrad(nhwc(x).bfloat16(), nhwc(dy).bfloat16(), w.shape, stride=s, padding=p, **kw)
+    assert rel(dw, ref) < 1e-5  # same bf16 operands, fp32 accumulation: only the summation order differs
+
+
+@pytest.mark.parametrize("cfg", [38, 43])
+def test_conv_wgrad_lean_two_segment(fn, cfg):
+    """Lean weight gradient of a conv reading two concatenated inputs (the Inception concat)."""
+    g = torch.Generator().manual_seed(6)
+    a = torch.randn(2, 96, 9, 21, generator=g).bfloat16().float().cuda()
+    bb = torch.randn(2, 64, 9, 21, generator=g).bfloat16().float().cuda()
+    w = (torch.randn(80, 160, 3, 3, generator=g) / 36).bfloat16().float().cuda()
+    ref = F.conv2d(torch.cat([a, bb], 1), w, padding=1)
+    dy = torch.randn(ref.shape, generator=g).bfloat16().float().cuda()
+    dw = fn.conv2d_wgrad(nhwc(a).bfloat16(), nhwc(dy).bfloat16(), w.shape, padding=1, x2=nhwc(bb).bfloat16(), cfg=cfg)
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(torch.cat([a, bb], 1), wr, padding=1).backward(dy)
+    assert rel(dw, wr.grad) < 5e-3
+
+
 # conv.hip default tile, and conv_lds.hip LDS-staged configs (tile, K chunk, K split) -- see test_conv_lds_gpu.py
 # heuristic, three LDS-staged configs, and two depth-4 register-pipelined tiles (conv.hip, cfg 128 + tile)
 LDS_SAMPLE = [None, 16 + 8 * 0 + 0 + 0, 16 + 8 * 1 + 4 + 2, 16 + 8 * 7 + 0 + 3, 128 + 8, 128 + 11]
