@@ -23,9 +23,10 @@
 namespace mda {
 
 // (TN, TK); keep in sync with ops/functional.py WGRAD_TILES (entries WGRAD_LEAN_CFG0..)
-#define WGRAD_LEAN_CASES(X)                                                                       \
-  case 36: X(16, 64) case 37: X(16, 144) case 38: X(32, 64) case 39: X(32, 144) case 40: X(64, 64) \
-  case 41: X(64, 128) case 42: X(128, 64) case 43: X(128, 128)
+// (TN, TK, MCH pixels per chunk)
+#define WGRAD_LEAN_CASES(X)                                                                                   \
+  case 36: X(16, 64, 256) case 37: X(16, 144, 128) case 38: X(32, 64, 256) case 39: X(32, 144, 128)           \
+  case 40: X(64, 64, 128) case 41: X(64, 128, 128) case 42: X(128, 64, 128) case 43: X(128, 128, 64)
 
 int wgrad_lean_shape(int cfg, int& TN, int& TK) {
   static const int tn[] = {16, 16, 32, 32, 64, 64, 128, 128}, tk[] = {64, 144, 64, 144, 64, 128, 64, 128};
@@ -45,12 +46,11 @@ DEV int lean_encode(int i, int Ktot, int Cs8, int KW, int C0) {
   return (seg ? c - C0 : c) | (kw << 14) | (kh << 21) | (seg << 28) | (1 << 29);
 }
 
-constexpr int LEAN_MCH = 64;
 constexpr int LEAN_BAD_ROW = -16384;  // first-tap row of a pixel past the split: every tap lands outside the image
 
-template <int TN, int TK>
+template <int TN, int TK, int MCH>
 DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, const int z) {
-  constexpr int MCH = LEAN_MCH;
+  static_assert(MCH % 64 == 0 && MCH <= 256, "chunk of 64..256 pixels (pixel table: one entry per thread)");
   // row pitches: 16 x odd elements, so the 8 rows a transposed read touches tile the 64 banks (wgrad_block)
   constexpr int LDY = (TN / 16) % 2 ? TN : TN + 16, LDX = (TK / 16) % 2 ? TK : TK + 16;
   constexpr int YG = TN / 8, KG = TK / 8;
@@ -107,7 +107,7 @@ DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, c
   __syncthreads();
 
   // per-thread constants of its 16-byte staging units, fixed for the block, two words per unit:
-  //   xk: pixel-in-chunk | kh << 6 | kw << 13 | segment << 20 | column valid << 21
+  //   xk: pixel-in-chunk | kh << 8 | kw << 15 | segment << 22 | column valid << 23
   //   xo: channel offset within the segment | LDS destination (element offset) << 14
   int xk[NX], xo[NX];
 #pragma unroll
@@ -115,17 +115,17 @@ DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, c
     const int v = tid + 256 * i;
     const int p = v / KG, g = v - p * KG;
     const int e = v < VX ? s_tab[g] : 0;
-    xk[i] = (v < VX ? p : 0) | (((e >> 21) & 127) << 6) | (((e >> 14) & 127) << 13) | (((e >> 28) & 1) << 20) |
-            (((e >> 29) & 1) << 21);
+    xk[i] = (v < VX ? p : 0) | (((e >> 21) & 127) << 8) | (((e >> 14) & 127) << 15) | (((e >> 28) & 1) << 22) |
+            (((e >> 29) & 1) << 23);
     xo[i] = (e & 16383) | ((p * LDX + g * 8) << 14);
   }
-  //   yk: pixel-in-chunk | channel valid << 6; yo: channel | LDS destination << 14
+  //   yk: pixel-in-chunk | channel valid << 8; yo: channel | LDS destination << 14
   int yk[NY], yo[NY];
 #pragma unroll
   for (int j = 0; j < NY; ++j) {
     const int v = tid + 256 * j;
     const int p = v / YG, cg = v - p * YG;
-    yk[j] = (v < VY ? p : 0) | ((v < VY && n0 + cg * 8 < a.Co) ? 64 : 0);
+    yk[j] = (v < VY ? p : 0) | ((v < VY && n0 + cg * 8 < a.Co) ? 256 : 0);
     yo[j] = (n0 + cg * 8) | ((p * LDY + cg * 8) << 14);
   }
   const int ld0 = a.src.ld[0], ld1 = a.src.ld[1];
@@ -136,10 +136,10 @@ DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, c
   do {                                                                                                         \
     rok = 0;                                                                                                   \
     _Pragma("unroll") for (int i = 0; i < NX; ++i) {                                                           \
-      const int k = xk[i], p = k & 63, kh = (k >> 6) & 127, kw = (k >> 13) & 127, seg = (k >> 20) & 1;         \
+      const int k = xk[i], p = k & 255, kh = (k >> 8) & 127, kw = (k >> 15) & 127, seg = (k >> 22) & 1;        \
       const int pix = s_pix[BUF][p], ihw = s_ihw[BUF][p];                                                      \
       const int ih = (ihw >> 16) + kh, iw = (int)(short)(ihw & 0xffff) + kw;                                   \
-      const bool ok = ((k >> 21) & 1) && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;       \
+      const bool ok = ((k >> 23) & 1) && (unsigned)ih < (unsigned)a.Hi && (unsigned)iw < (unsigned)a.Wi;       \
       const int off = ok ? (pix + kh * a.Wi + kw) * (seg ? ld1 : ld0) + (xo[i] & 16383) : 0;                  \
       const uint4 u = *reinterpret_cast<const uint4*>((seg ? base1 : base0) + off);                            \
       const uint32_t mk = ok ? 0xffffffffu : 0u; /* (a select of the uint4 went through scratch) */            \
@@ -147,8 +147,8 @@ DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, c
       rok |= (ok ? 1u : 0u) << i;                                                                              \
     }                                                                                                          \
     _Pragma("unroll") for (int j = 0; j < NY; ++j) {                                                           \
-      const int m = (MC) + (yk[j] & 63);                                                                       \
-      const bool ok = (yk[j] & 64) && m < mend;                                                                \
+      const int m = (MC) + (yk[j] & 255);                                                                      \
+      const bool ok = (yk[j] & 256) && m < mend;                                                               \
       const uint4 u = *reinterpret_cast<const uint4*>(dyz + (ok ? m * a.ldd + (yo[j] & 16383) : 0));           \
       const uint32_t mk = ok ? 0xffffffffu : 0u;                                                               \
       ry[j] = make_uint4(u.x & mk, u.y & mk, u.z & mk, u.w & mk);                                              \
@@ -225,12 +225,12 @@ DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, c
   }
 }
 
-template <int TN, int TK>
+template <int TN, int TK, int MCH>
 __global__ __launch_bounds__(256) void conv_wgrad_lean_kernel(WgradArgs a) {
-  wgrad_lean_block<TN, TK>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  wgrad_lean_block<TN, TK, MCH>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
-template <int TN, int TK>
+template <int TN, int TK, int MCH>
 __global__ __launch_bounds__(256) void conv_wgrad_lean_batched_kernel(const WgradJob* __restrict__ jobs, int nj,
                                                                        int64_t nvb) {
   for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_lean_batched_kernel(const Wgra
     const int local = (int)(vb - J.block0);
     const int per_z = J.ntiles * J.a.splits;
     const int z = local / per_z, r = local - z * per_z;
-    wgrad_lean_block<TN, TK>(J.a, r % J.ntiles, r / J.ntiles, z);
+    wgrad_lean_block<TN, TK, MCH>(J.a, r % J.ntiles, r / J.ntiles, z);
     __syncthreads();  // the next virtual block re-stages the LDS tables
   }
 }
@@ -267,8 +267,8 @@ int wgrad_lean_ntiles(int cfg, const WgradArgs& a) {
 int launch_wgrad_lean(const WgradArgs& a, int G, int cfg, hipStream_t st) {
   const int nt = wgrad_lean_ntiles(cfg, a);
   if (nt < 0) return nt;
-#define LAUNCH_WGL(TN, TK)                                                                              \
-  hipLaunchKernelGGL((conv_wgrad_lean_kernel<TN, TK>), dim3(nt, a.splits, G), dim3(256), 0, st, a);     \
+#define LAUNCH_WGL(TN, TK, MCH)                                                                            \
+  hipLaunchKernelGGL((conv_wgrad_lean_kernel<TN, TK, MCH>), dim3(nt, a.splits, G), dim3(256), 0, st, a);   \
   break;
   switch (cfg) {
     WGRAD_LEAN_CASES(LAUNCH_WGL)
@@ -279,8 +279,8 @@ int launch_wgrad_lean(const WgradArgs& a, int G, int cfg, hipStream_t st) {
 }
 
 int launch_wgrad_lean_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, dim3 grid, hipStream_t st) {
-#define LAUNCH_WGLB(TN, TK)                                                                                    \
-  hipLaunchKernelGGL((conv_wgrad_lean_batched_kernel<TN, TK>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \
+#define LAUNCH_WGLB(TN, TK, MCH)                                                                                    \
+  hipLaunchKernelGGL((conv_wgrad_lean_batched_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \
   break;
   switch (cfg) {
     WGRAD_LEAN_CASES(LAUNCH_WGLB)

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..ops.functional import (WGRAD_BIG0, WGRAD_PATCH, WGRAD_TILES, bnb_plan, patch_plan, patch_valid, wgrad_cfg,
+from ..ops.functional import (WGRAD_BIG0, WGRAD_LEAN0, WGRAD_LEAN_N, WGRAD_PATCH, WGRAD_TILES, bnb_plan, patch_plan, patch_valid, wgrad_cfg,
                               wgrad_ktiles)
 from ..ops.hip import lib, ptr
 from . import guard
@@ -492,6 +492,7 @@ class ConvLayer:
     # the large 32x32x16 tiles (configs 32-35) at 256 pixels per split: Model C's batches 624 -> 440 us but
     # the finalize's split slabs 102 -> 197 us; at 1024: 515 us and 103 us (tools/wgrad_assign.py)
     MIN_SPLIT_PX_BIG = 1024
+    LEAN_MIN_CHUNKS = 2
 
     def wgrad_valid(self, cfg: int) -> bool:
         """The K tiles of ``cfg`` cover this conv's padded reduction (exactly, except for the large-tile
@@ -512,6 +513,12 @@ class ConvLayer:
             return patch_plan(cfg, self.B, self.Ho, self.Npad, self.Cs, self.G, 512 if wide else 128)
         TN, TK, MCH = WGRAD_TILES[cfg]
         tiles = math.ceil(self.Npad / TN) * wgrad_ktiles(cfg, self.Kpad_w) * self.G
+        if WGRAD_LEAN0 <= cfg < WGRAD_LEAN0 + WGRAD_LEAN_N:
+            # lean staging (csrc/wgrad_lean.hip) is bound by the load latency of its serial chunks: ~1,024 blocks
+            # per job, at least LEAN_MIN_CHUNKS chunks each (fewer, longer blocks for the small-M layers)
+            splits = max(1, min(math.ceil(self.M_out / (self.LEAN_MIN_CHUNKS * MCH)), math.ceil(1024 / tiles)))
+            mps = pad_to(math.ceil(self.M_out / splits), MCH)
+            return math.ceil(self.M_out / mps), mps
         # whole-reduction tiles (TK >= 128) have one tile per channel block: shorter per-block pixel
         # ranges keep enough blocks in flight (the finalize sums the extra splits with several lanes)
         if cfg >= WGRAD_BIG0:

@@ -17,7 +17,8 @@ import torch
 
 from ..ops.functional import (CONV_DEEP_CFG0, CONV_DEEP_NCFG, CONV_GLDS_CFG0, CONV_GLDS_NCFG, CONV_LDS_CFG0,
                               CONV_LDS_NCFG, CONV_PATCH_CFG0, CONV_PATCH_NCFG, CONV_PATCHP_CFG0, CONV_PATCHP_NCFG,
-                              CONV_XCD, GDEEP_TILES, WGRAD_BIG0, WGRAD_PATCH, WGRAD_TILES, conv_workspace,
+                              CONV_XCD, GDEEP_TILES, WGRAD_BIG0, WGRAD_LEAN0, WGRAD_LEAN_N, WGRAD_PATCH, WGRAD_TILES,
+                              conv_workspace,
                               glds_cfg)
 from ..ops.hip import lib
 from .program import EventKeeper
@@ -230,7 +231,7 @@ def autotune_program(prog, out_path: Optional[str] = None, verbose: bool = False
 
 
 def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passes: int = 1,
-                       init_big: bool = False) -> Dict[str, int]:
+                       init_big: bool = False, init_lean=False) -> Dict[str, int]:
     """Choose the weight-gradient configs by the time of the BATCHED launches they end up in.
 
     A conv's weight gradient never runs alone: it is a job of one batched launch per (stream, config)
@@ -278,6 +279,22 @@ def tune_wgrad_batches(prog, cache: Dict[str, int], verbose: bool = False, passe
         return len(groups[sig]) * d["B"] * d["Ho"] * d["Wo"] * d["Npad"] * d["Kpad"]
 
     t0 = cost()
+    if init_lean:  # signatures on their fastest lean-staging config, timed alone (csrc/wgrad_lean.hip); a set of
+        # streams restricts it to the weight gradients batched on those streams
+        for sig, ls in groups.items():
+            l0 = ls[0]
+            if init_lean is not True and l0.stream not in init_lean:
+                continue
+            cand = []
+            for c in range(WGRAD_LEAN0, WGRAD_LEAN0 + WGRAD_LEAN_N):
+                if not all(l.owner.wgrad_valid(c) for l in ls):
+                    continue
+                l0.owner.set_wgrad_cfg(c)
+                cand.append((_time(lambda c=c: L.wgrad(c, l0.args[1], torch.cuda.current_stream().cuda_stream,
+                                                       l0.args[2])), c))
+            l0.owner.set_wgrad_cfg(assign[sig])
+            if cand:
+                assign[sig] = min(cand)[1]
     if init_big:
         for sig, ls in groups.items():
             conv = ls[0].owner

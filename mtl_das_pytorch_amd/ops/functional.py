@@ -232,8 +232,8 @@ WGRAD_TILES = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 
                32: (64, 64, 64), 33: (64, 128, 64), 34: (128, 64, 64), 35: (128, 128, 64),
                # lean-staging im2col tiles (csrc/wgrad_lean.hip: per-chunk pixel table in LDS, per-thread staging
                # constants, branch-free loads); partial last K tile
-               36: (16, 64, 64), 37: (16, 144, 64), 38: (32, 64, 64), 39: (32, 144, 64), 40: (64, 64, 64),
-               41: (64, 128, 64), 42: (128, 64, 64), 43: (128, 128, 64)}
+               36: (16, 64, 256), 37: (16, 144, 128), 38: (32, 64, 256), 39: (32, 144, 128), 40: (64, 64, 128),
+               41: (64, 128, 128), 42: (128, 64, 128), 43: (128, 128, 64)}
 WGRAD_BIG0 = 32
 WGRAD_LEAN0, WGRAD_LEAN_N = 36, 8
 

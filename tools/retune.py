@@ -68,6 +68,10 @@ def main():
     ap.add_argument("--drop", default="", help="with --keep: comma-separated key prefixes to re-measure (e.g. wgrad)")
     ap.add_argument("--wgrad-big-init", action="store_true",
                     help="--wgrad-batches starts from every im2col conv on its large tile")
+    ap.add_argument("--wgrad-lean-init", default="",
+                    help="--wgrad-batches starts from the convs of these streams (comma-separated, 'all': every "
+                         "stream) on their fastest lean-staging config (36-43)")
+    ap.add_argument("--wgrad-passes", type=int, default=2, help="--wgrad-batches: coordinate-descent passes")
     ap.add_argument("--wgrad-batches", action="store_true",
                     help="re-choose the weight-gradient configs by their batched launches' time (tune_wgrad_batches)")
     ap.add_argument("--wgrad-in-step", action="store_true",
@@ -92,7 +96,9 @@ def main():
         print(f"{name}: {len(cache) - n0} new entries in {time.time() - t0:.1f} s", flush=True)
         if args.wgrad_batches and name in ("MTL", "multi_classifier"):
             _warm_step(prog, name, args.batch)
-            tune_wgrad_batches(prog, cache, verbose=True, passes=2, init_big=args.wgrad_big_init)
+            tune_wgrad_batches(prog, cache, verbose=True, passes=args.wgrad_passes, init_big=args.wgrad_big_init,
+                               init_lean=(True if args.wgrad_lean_init == "all" else
+                                          {int(x) for x in args.wgrad_lean_init.split(",") if x}))
             print(f"{name}: weight-gradient batches tuned at {time.time() - t0:.1f} s", flush=True)
         if args.wgrad_in_step and name in ("MTL", "multi_classifier"):
             X, d, e = generate(4 * args.batch, seed=3, device="cuda")
