@@ -493,6 +493,8 @@ class ConvLayer:
     # the finalize's split slabs 102 -> 197 us; at 1024: 515 us and 103 us (tools/wgrad_assign.py)
     MIN_SPLIT_PX_BIG = 1024
     LEAN_MIN_CHUNKS = 2
+    LEAN_BLOCKS = 512
+    LEAN_MAX_SPLITS = 64
 
     def wgrad_valid(self, cfg: int) -> bool:
         """The K tiles of ``cfg`` cover this conv's padded reduction (exactly, except for the large-tile
@@ -514,9 +516,11 @@ class ConvLayer:
         TN, TK, MCH = WGRAD_TILES[cfg]
         tiles = math.ceil(self.Npad / TN) * wgrad_ktiles(cfg, self.Kpad_w) * self.G
         if WGRAD_LEAN0 <= cfg < WGRAD_LEAN0 + WGRAD_LEAN_N:
-            # lean staging (csrc/wgrad_lean.hip) is bound by the load latency of its serial chunks: ~1,024 blocks
-            # per job, at least LEAN_MIN_CHUNKS chunks each (fewer, longer blocks for the small-M layers)
-            splits = max(1, min(math.ceil(self.M_out / (self.LEAN_MIN_CHUNKS * MCH)), math.ceil(1024 / tiles)))
+            # lean staging (csrc/wgrad_lean.hip) is bound by the load latency of its serial chunks: ~LEAN_BLOCKS
+            # blocks per job, at least LEAN_MIN_CHUNKS chunks each, at most LEAN_MAX_SPLITS split slabs for the
+            # finalize to sum (it runs on the step's tail)
+            splits = max(1, min(math.ceil(self.M_out / (self.LEAN_MIN_CHUNKS * MCH)), math.ceil(self.LEAN_BLOCKS / tiles),
+                                self.LEAN_MAX_SPLITS))
             mps = pad_to(math.ceil(self.M_out / splits), MCH)
             return math.ceil(self.M_out / mps), mps
         # whole-reduction tiles (TK >= 128) have one tile per channel block: shorter per-block pixel
