@@ -212,13 +212,16 @@ class StepRunner:
                 self._ensure_graph("train_ext")  # both captured before any collective is in flight (the
                 self._ensure_graph("train_opt")  # capture's state snapshot/restore must not race an all-reduce)
             self._run("train_ext")
-            comm = EngineStreams.get(self.p.device).comm
             g = self.p.flat.grads
-            for ev, (lo, hi) in zip(self.ext_events, self.buckets):
-                ev.wait(comm)
-                with torch.cuda.stream(comm):
-                    self.allreduce.start(g[lo:hi])
-            self.allreduce.finish()
+            if hasattr(self.allreduce, "start"):
+                comm = EngineStreams.get(self.p.device).comm
+                for ev, (lo, hi) in zip(self.ext_events, self.buckets):
+                    ev.wait(comm)
+                    with torch.cuda.stream(comm):
+                        self.allreduce.start(g[lo:hi])
+                self.allreduce.finish()
+            else:  # a plain callable: the whole gradient, in stream order after the graph
+                self.allreduce(g)
             self._run("train_opt")
         else:  # eager launches (no graphs): the whole gradient after the backward
             self._run("train_compute")
