@@ -126,7 +126,7 @@ class Trainer:
         use_gpu = cfg.GPU_device and torch.cuda.is_available()
         self.device = self.ctx.device if use_gpu else torch.device("cpu")
         torch.manual_seed(cfg.seed)
-        self.model = build_model(cfg.model, in_channels=cfg.in_channels)
+        self.model = build_model(cfg.model, in_channels=cfg.in_channels, head=cfg.head)
         note = "model_type={} is_test={}".format(cfg.model, cfg.is_test)
         stamp = datetime.datetime.now().strftime("%m-%d-%H_%M_%S")
         if self.ctx.enabled:  # every rank must agree on the directory name
@@ -153,6 +153,10 @@ class Trainer:
 
     def _pick_backend(self) -> str:
         c = self.cfg
+        if c.head != "group_mean":  # the engine lowers the reference's parameter-free head only
+            if c.backend == "engine":
+                raise ValueError("--head fc runs on the plain-PyTorch backend (--backend torch / auto)")
+            return "torch"
         if c.backend == "torch" or self.device.type != "cuda":
             return "torch"
         return "engine"

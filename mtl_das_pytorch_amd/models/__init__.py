@@ -7,16 +7,19 @@ from .multi_classifier import (BasicConv2d, InceptionA, InceptionAux, InceptionB
 MODEL_TYPES = ("MTL", "single_distance", "single_event", "multi_classifier")
 
 
-def build_model(model_type: str, in_channels: int = 1):
-    """Model factory with the reference's ``--model`` names (reference utils.py:85-98)."""
-    if model_type == "MTL":
-        return MTL_Net(in_channels=in_channels)
-    if model_type == "single_distance":
-        return Single_Task_Net("distance", in_channels=in_channels)
-    if model_type == "single_event":
-        return Single_Task_Net("event", in_channels=in_channels)
+def build_model(model_type: str, in_channels: int = 1, head: str = "group_mean"):
+    """Model factory with the reference's ``--model`` names (reference utils.py:85-98).  ``head="fc"``
+    (Models A / B only) is the backbone-vs-head ablation of docs/ACCURACY.md, not a reference model."""
     if model_type == "multi_classifier":
+        if head != "group_mean":
+            raise ValueError("--head applies to the MTL / single-task models only")
         return Multi_Classifier(in_channels=in_channels)
+    if model_type == "MTL":
+        return MTL_Net(in_channels=in_channels, head=head)
+    if model_type == "single_distance":
+        return Single_Task_Net("distance", in_channels=in_channels, head=head)
+    if model_type == "single_event":
+        return Single_Task_Net("event", in_channels=in_channels, head=head)
     raise ValueError(f"unknown model type {model_type!r}; expected one of {MODEL_TYPES}")
 
 

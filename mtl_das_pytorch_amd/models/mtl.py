@@ -10,6 +10,8 @@ Reference: model/modelA_MTL.py:53-174 (``MTL_Net``) and model/modelB_singleTask.
       A_k     = mask_k * F_{2k}
       B_k     = maxpool2x2_ceil( relu(BN(conv3x3(A_k))) )     for k = 1..3
   head      GAP(A_4) -> mean over groups of 128/n_classes channels -> log_softmax
+            (``head="fc"``: GAP(A_4) -> Linear(128, n_classes) -> log_softmax -- NOT in the reference: the
+            backbone-vs-head ablation of docs/ACCURACY.md, trained on the plain-PyTorch backend only)
 
 ``MTLNet`` is generic in the task list; ``MTL_Net()`` and ``Single_Task_Net(task)`` are thin
 constructors that reproduce the reference class names, default arguments and the *exact*
@@ -36,11 +38,18 @@ class MTLNet(nn.Module):
         tasks: task names, subset/ordering of :data:`TASK_CLASSES` keys.
         in_channels: input channels (reference: 1; ``--in_channels 2`` changes conv1's weight shape).
         first_ch: channels of the first stage (reference: 16; doubles every two residual blocks).
+        head: ``"group_mean"`` (the reference's parameter-free head) or ``"fc"`` (ablation: a learned linear
+            layer per task on the pooled features, as Model C's classifier; adds ``task{1,2}fc`` keys).
     """
 
+    HEADS = ("group_mean", "fc")
+
     def __init__(self, tasks: Sequence[str] = ("distance", "event"), in_channels: int = 1, first_ch: int = 16,
-                 num_classes: Sequence[int] | None = None):
+                 num_classes: Sequence[int] | None = None, head: str = "group_mean"):
         super().__init__()
+        if head not in self.HEADS:
+            raise ValueError(f"unknown head {head!r}; expected one of {self.HEADS}")
+        self.head = head
         self.tasks = list(tasks)
         for t in self.tasks:
             if t not in TASK_CLASSES and num_classes is None:
@@ -83,6 +92,8 @@ class MTLNet(nn.Module):
             idx = 1 if t == "distance" else 2
             setattr(self, f"task{idx}pool", nn.AdaptiveAvgPool2d((1, 1)))
             setattr(self, f"task{idx}pool1d", nn.AvgPool1d(kernel_size=ch[-1] // ncls, stride=ch[-1] // ncls))
+            if head == "fc":
+                setattr(self, f"task{idx}fc", nn.Linear(ch[-1], ncls))
 
     # ---- structure accessors used by the engine -------------------------------------------------
     @property
@@ -124,7 +135,10 @@ class MTLNet(nn.Module):
                 else:
                     prev = a
             gap, grp = self.head_modules(t)
-            logits = grp(gap(prev).flatten(1).unsqueeze(1)).squeeze(1)
+            if self.head == "fc":
+                logits = getattr(self, f"task{1 if self.tasks[t] == 'distance' else 2}fc")(gap(prev).flatten(1))
+            else:
+                logits = grp(gap(prev).flatten(1).unsqueeze(1)).squeeze(1)
             outs.append(F.log_softmax(logits, dim=1))
         return tuple(outs) if len(outs) > 1 else outs[0]
 
@@ -132,14 +146,14 @@ class MTLNet(nn.Module):
 class MTL_Net(MTLNet):
     """Reference-compatible constructor: ``MTL_Net()`` (Model A, tasks distance+event)."""
 
-    def __init__(self, in_channels: int = 1):
-        super().__init__(tasks=("distance", "event"), in_channels=in_channels)
+    def __init__(self, in_channels: int = 1, head: str = "group_mean"):
+        super().__init__(tasks=("distance", "event"), in_channels=in_channels, head=head)
 
 
 class Single_Task_Net(MTLNet):
     """Reference-compatible constructor: ``Single_Task_Net(task)`` (Model B)."""
 
-    def __init__(self, task: str = "distance", in_channels: int = 1):
+    def __init__(self, task: str = "distance", in_channels: int = 1, head: str = "group_mean"):
         if task not in ("distance", "event"):
             raise ValueError(task)
-        super().__init__(tasks=(task,), in_channels=in_channels)
+        super().__init__(tasks=(task,), in_channels=in_channels, head=head)

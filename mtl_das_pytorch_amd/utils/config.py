@@ -50,6 +50,7 @@ class TrainConfig:
     save_threshold: Optional[float] = None  # 0.98 (A/B) / 0.95 (C), utils.py:329,716
     loss_weights: List[float] = field(default_factory=lambda: [1.0, 1.0])  # utils.py:367 (unweighted sum)
     in_channels: int = 1
+    head: str = "group_mean"              # group_mean (reference) | fc (ablation, plain-PyTorch backend only)
     backend: str = "auto"                 # auto | engine | torch
     synthetic: int = 0                    # >0: N synthetic samples per (distance, event) class, no dataset needed
     synthetic_seed: int = 0
@@ -105,6 +106,9 @@ def build_parser(is_test: bool) -> argparse.ArgumentParser:
     g.add_argument("--save_threshold", type=float, default=None)
     g.add_argument("--loss_weights", type=str, default="1,1", help="w_distance,w_event for the MTL loss")
     g.add_argument("--in_channels", type=int, default=1)
+    g.add_argument("--head", choices=["group_mean", "fc"], default="group_mean",
+                   help="A / B classifier head: the reference's group mean, or a learned linear layer per task "
+                        "(backbone-vs-head ablation; trains on the plain-PyTorch backend)")
     g.add_argument("--backend", choices=["auto", "engine", "torch"], default="auto",
                    help="engine = MI355X HIP engine (bf16), torch = plain PyTorch (fp32, CPU capable)")
     g.add_argument("--synthetic", type=int, default=0, help="synthetic samples per (distance, event) class")

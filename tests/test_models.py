@@ -100,3 +100,26 @@ def test_inception_init_is_truncated_normal():
     w = c.Mixed_6b.branch7x7_2.conv.weight
     assert w.abs().max() <= 0.2 + 1e-6 and 0.05 < w.std() < 0.1
     assert torch.all(c.Mixed_5b.branch1x1.bn.weight == 1)
+
+
+def test_fc_head_ablation():
+    """head="fc" (docs/ACCURACY.md backbone-vs-head ablation): a learned linear layer per task on the pooled
+    features; the reference head's key space is untouched, the trainer keeps it off the engine."""
+    from mtl_das_pytorch_amd.engine.trainer import Trainer
+    from mtl_das_pytorch_amd.utils.config import TrainConfig
+    m = build_model("MTL", head="fc")
+    sd = m.state_dict()
+    assert len(sd) == 268 + 4 and sd["task1fc.weight"].shape == (16, 128) and sd["task2fc.weight"].shape == (2, 128)
+    d, e = m.eval()(torch.randn(2, 1, 100, 250))
+    assert d.shape == (2, 16) and e.shape == (2, 2)
+    assert torch.allclose(d.exp().sum(1), torch.ones(2), atol=1e-5)
+    assert build_model("single_distance", head="fc")(torch.randn(1, 1, 100, 250)).shape == (1, 16)
+    with pytest.raises(ValueError):
+        build_model("multi_classifier", head="fc")
+    with pytest.raises(ValueError):
+        build_model("MTL", head="nope")
+    tr = Trainer(TrainConfig(model="MTL", head="fc", synthetic=1, output_savedir="/tmp/mda_fc_head_test"))
+    assert tr.backend_name == "torch"
+    with pytest.raises(ValueError):
+        Trainer(TrainConfig(model="MTL", head="fc", backend="engine", synthetic=1,
+                            output_savedir="/tmp/mda_fc_head_test"))._pick_backend()

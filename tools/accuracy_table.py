@@ -13,7 +13,9 @@ schedule -- batch 32, 40 epochs, Adam lr 1e-3 / wd 1e-5, LR / 1.5 at every 5th-e
   * ``snr=S``    clean test signals plus white Gaussian noise at S dB through the reference's
                  ``add_gaussian`` (dataset_preparation.py:83-105; the same fixed noise seed for every model).
 
-Rows: A on the engine (bf16 HIP) and A on plain fp32 PyTorch at the same seed, B_distance, B_event, C.
+Rows: A on the engine (bf16 HIP) and A on plain fp32 PyTorch at the same seed, B_distance, B_event, C, and the
+backbone-vs-head ablations A_fc / B_distance_fc (A's / B's backbone with a learned linear head per task in place
+of the reference's group-mean head, as Model C's classifier; fp32 PyTorch -- not reference models).
 
     python tools/accuracy_table.py [--per-class 200] [--epochs 40] [--out gpurun_out/accuracy]
 """
@@ -51,12 +53,12 @@ def make_test_sets(per_class: int, seed: int, snrs, device):
     return {k: v.to(device) for k, v in sets.items()}, lab2.to(device), joint.to(device), e.to(device)
 
 
-def run_one(name, model, backend, args, seed, test_sets, lab2, joint, ev, out_dir):
+def run_one(name, model, backend, args, seed, test_sets, lab2, joint, ev, out_dir, head="group_mean"):
     from mtl_das_pytorch_amd.engine.trainer import Trainer
     from mtl_das_pytorch_amd.utils.config import TrainConfig
     cfg = TrainConfig(model=model, synthetic=args.per_class, synthetic_seed=args.data_seed, batch_size=32,
                       epoch_num=args.epochs, output_savedir=os.path.join(out_dir, f"{name.replace(' ', '_')}_s{seed}"),
-                      backend=backend, seed=seed, save_threshold=2.0, log_every=100)
+                      backend=backend, seed=seed, save_threshold=2.0, log_every=100, head=head)
     t0 = time.time()
     tr = Trainer(cfg)
     tr.run()
@@ -194,14 +196,17 @@ def main():
     spec = {"A": ("A MTL_Net", "MTL", "engine"), "A_fp32": ("A MTL_Net (fp32 torch)", "MTL", "torch"),
             "B_distance": ("B Single_Task_Net distance", "single_distance", "engine"),
             "B_event": ("B Single_Task_Net event", "single_event", "engine"),
-            "C": ("C Multi_Classifier", "multi_classifier", "engine")}
+            "C": ("C Multi_Classifier", "multi_classifier", "engine"),
+            "A_fc": ("A backbone + fc head (ablation, fp32 torch)", "MTL", "torch", "fc"),
+            "B_distance_fc": ("B distance backbone + fc head (ablation, fp32 torch)", "single_distance", "torch", "fc")}
     rows = []
     for seed in [int(x) for x in args.seeds.split(",")]:
         for key in args.rows.split(","):
-            name, model, backend = spec[key]
+            name, model, backend = spec[key][:3]
+            head = spec[key][3] if len(spec[key]) > 3 else "group_mean"
             if dev.type != "cuda":
                 backend = "torch"
-            rows.append(run_one(name, model, backend, args, seed, test_sets, lab2, joint, ev, runs))
+            rows.append(run_one(name, model, backend, args, seed, test_sets, lab2, joint, ev, runs, head=head))
             with open(os.path.join(args.out, "accuracy.json"), "w") as f:
                 json.dump({"args": vars(args), "rows": rows}, f, indent=1)
     md = to_markdown(rows, args)
