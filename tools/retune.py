@@ -78,6 +78,8 @@ def main():
                     help="then re-choose the heaviest weight-gradient configs by the captured step's time "
                          "(tune_wgrad_in_step; A and C)")
     ap.add_argument("--wgrad-top", type=int, default=10, help="--wgrad-in-step: signatures to re-time")
+    ap.add_argument("--wgrad-topk", type=int, default=3,
+                    help="--wgrad-in-step: candidates per signature from its isolated ranking (+ its large tile)")
     ap.add_argument("--spill", action="store_true",
                     help="choose the weight-gradient spill fraction in the step (tune_spill)")
     ap.add_argument("--passes", default="cfg,xcd,tail", help="in-context passes: conv configs, tile order, BN tails")
@@ -103,7 +105,8 @@ def main():
         if args.wgrad_in_step and name in ("MTL", "multi_classifier"):
             X, d, e = generate(4 * args.batch, seed=3, device="cuda")
             labels = encode_joint(d, e) if name == "multi_classifier" else torch.stack([d, e], 1)
-            tune_wgrad_in_step(lambda: _make(name, args.batch), X, labels, cache, top=args.wgrad_top)
+            tune_wgrad_in_step(lambda: _make(name, args.batch), X, labels, cache, top=args.wgrad_top,
+                               topk=args.wgrad_topk)
             save_cache(cache, args.out)
             print(f"{name}: weight gradients tuned in the step at {time.time() - t0:.1f} s", flush=True)
         if args.spill and name in ("MTL", "multi_classifier"):
