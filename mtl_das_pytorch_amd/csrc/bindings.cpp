@@ -389,8 +389,15 @@ void adam_pack(int64_t stream, py::dict d) {
   a.wd = (float)F(d, "wd", 0.0); a.grad_scale = (float)F(d, "grad_scale", 1.0);
   a.update = (int)I(d, "update", 1);
   a.inc_step = (int)I(d, "inc_step", 1);
+  a.t_pre = (int)I(d, "t_pre", 0);
+  if (a.t_pre && a.inc_step && a.update) throw std::runtime_error("adam: t_pre with inc_step would advance the step twice");
   a.cursor = P<int64_t>(d, "cursor");
   check(launch_adam_pack(a, P<const OptSeg>(d, "segs"), (int)I(d, "nsegs"), I(d, "nblocks"), S(stream)), "adam_pack");
+}
+
+void step_inc(int64_t step, int64_t cursor, int64_t stream) {
+  if (!step) throw std::runtime_error("step_inc: null step counter");
+  check(launch_step_inc(reinterpret_cast<float*>(step), reinterpret_cast<int64_t*>(cursor), S(stream)), "step_inc");
 }
 
 }  // namespace
@@ -449,6 +456,7 @@ PYBIND11_MODULE(_mda_hip, m) {
                       reinterpret_cast<uint64_t*>(static_cast<intptr_t>(q)), i, S(stream)), "tick");
   }, py::arg("buf"), py::arg("i"), py::arg("stream"), py::arg("n"), py::arg("q") = 0);
   m.def("adam_pack", &adam_pack);
+  m.def("step_inc", &step_inc);
   m.def("hip_device_sync", []() { return (int)hipDeviceSynchronize(); });
   // engine-owned streams (engine/program.py EngineStreams): created once per device, never drawn from
   // torch's round-robin stream pool, so they cannot alias a capture stream or each other

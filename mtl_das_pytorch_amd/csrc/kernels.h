@@ -247,8 +247,13 @@ struct AdamArgs {
   float b1, b2, eps, wd, grad_scale;
   int update;  // 0: pack only
   int inc_step;  // advance the step counter after the update (0: a partial update -- another launch of the step does)
+  int t_pre;     // 1: this step already advanced the counter (launch_step_inc at the step's start): t = step, else
+                 // t = step + 1
   int64_t* cursor;  // optional: the batch-index schedule's cursor (gather_batch), advanced with the step counter
 };
+// the step counter (+ the schedule cursor) advanced by one thread: after the update (launch_adam_pack, inc_step)
+// or early in the step on a side stream (AdamArgs::t_pre)
+int launch_step_inc(float* step, int64_t* cursor, hipStream_t st);
 
 int launch_conv(int mode, const ConvArgs& a, int G, int cfg, hipStream_t st);
 // LDS-staged implicit GEMM (conv_lds.hip): cfg = CONV_LDS_CFG0 + 8 * tile + 4 * (KC == 128) + log2(splits)

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamArgs a, const OptSeg
   const int blk = (int)((int64_t)bx - S.block0);
   float c1 = 0.f, c2 = 0.f;
   if (a.update) {
-    const float t = a.step[0] + 1.f;
+    const float t = a.step[0] + (a.t_pre ? 0.f : 1.f);
     c1 = a.lr[0] / (1.f - powf(a.b1, t));
     c2 = 1.f / sqrtf(1.f - powf(a.b2, t));
   }
@@ -152,13 +152,17 @@ __global__ void step_inc_kernel(float* step, int64_t* cursor) {
   if (cursor) cursor[0] += 1;  // the next step gathers the next row of the batch-index schedule
 }
 
+int launch_step_inc(float* step, int64_t* cursor, hipStream_t st) {
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step, cursor);
+  return (int)hipGetLastError();
+}
+
 int launch_adam_pack(const AdamArgs& a, const OptSeg* d_segs, int ns, int64_t nblocks, hipStream_t st) {
   if (nblocks <= 0 || nblocks >= (1ll << 31)) return -2;
   hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)nblocks), dim3(256), 0, st, a, d_segs, ns);
   int rc = (int)hipGetLastError();
   if (rc || !a.update || !a.inc_step) return rc;
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, const_cast<float*>(a.step), a.cursor);
-  return (int)hipGetLastError();
+  return launch_step_inc(const_cast<float*>(a.step), a.cursor, st);
 }
 
 }  // namespace mda

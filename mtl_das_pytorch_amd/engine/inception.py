@@ -197,6 +197,9 @@ class InceptionProgram(LoweredProgram):
     # DP: 4 buckets of ~22 MB cut at Inception-block boundaries (fc+Mixed_7c, 7b, 7a-6c, the rest); the
     # first three all-reduces overlap the remaining blocks' backward
     default_buckets = 4
+    # the step counter stays after the last Adam launch here: on the forward's first side stream it cost Model C
+    # 0.7 % (9,567 / 9,566 vs 9,629 / 9,634 samples/s, interleaved; Model A +0.3 %, docs/PERF.md round 6)
+    EARLY_STEP_COUNTER = False
 
     def __init__(self, model: Multi_Classifier, batch: int, device, in_hw=(100, 250), p_drop: float = 0.5,
                  sync_world: int = 1):

@@ -12,7 +12,7 @@ from ..ops.functional import WGRAD_PATCH, WGRAD_TILES, wgrad_ktiles
 from ..ops.hip import lib
 from .core import (GRAD_DT, Act, BNLayer, ConvLayer, P, build_optseg_table, build_wgfin_table, optimizer_segments,
                    pad_to)
-from .program import (COMM_STREAM, SPILL_STREAM, Launch, Phase, k_adam, k_allreduce, k_ext_record, k_conv, k_gather, k_tail_bwd, k_tail_fwd,
+from .program import (COMM_STREAM, SPILL_STREAM, Launch, Phase, k_adam, k_step_inc, k_allreduce, k_ext_record, k_conv, k_gather, k_tail_bwd, k_tail_fwd,
                       k_tail_fwd_batched, k_wgfin, k_wgrad,
                       k_wgrad_batched)
 
@@ -800,7 +800,7 @@ class LoweredProgram:
                     table, ns, nb = build_optseg_table(segs, self.device)
                     self._opt_tables = getattr(self, "_opt_tables", []) + [table]
                     d = dict(self._opt_base, segs=P(table), nsegs=ns, nblocks=nb, update=1, inc_step=0,
-                             **self._opt_hparams)
+                             t_pre=int(self._step_early is not None), **self._opt_hparams)
                     tag = f"adam_s{st}"
                     batched.append(Launch("adam_pack_early", k_adam, d, stream=st, record=tag))
                     tags = [t for t in tags if t != f"wgfin_s{st}"] + [tag]
@@ -916,23 +916,54 @@ class LoweredProgram:
         for d in getattr(self, "_early_adam", []):  # the side streams' partial updates (batch_wgrads)
             d.update(self._opt_hparams)
         upd = Phase("adam")
-        upd.add("adam_pack", k_adam, dict(self._opt_base, update=1, **self._opt_hparams))
+        upd.add("adam_pack", k_adam, dict(self._opt_base, update=1, **self._opt_hparams, **self._step_mode()))
         self.opt["adam"] = upd
         self.set_step_cursor(getattr(self, "_step_cursor", None))
 
-    def set_step_cursor(self, cursor: Optional[torch.Tensor]):
-        """The device int64 cursor of a batch-index schedule (gather_phase ``cursor``): the optimizer's
-        step-counter kernel advances it together with the Adam step count (csrc/optim.hip step_inc_kernel),
-        at the end of the training step, after every gather block has read it.  None detaches it."""
-        self._step_cursor = cursor
-        for l in self.opt["adam"].launches:
-            if l.name == "adam_pack":
-                d = l.args[0]
-                if cursor is None:
-                    d.pop("cursor", None)
-                else:
-                    d["cursor"] = cursor.data_ptr()
+    _step_early = None  # the step-counter launch's args once use_early_step_counter moved it into the forward
+    EARLY_STEP_COUNTER = True  # class switch for A/B runs (tools/variant.py)
 
+    def _step_mode(self) -> dict:
+        return {"t_pre": 1, "inc_step": 0} if self._step_early is not None else {}
+
+    def use_early_step_counter(self) -> bool:
+        """Advance the Adam step counter (and a schedule cursor) at the START of the training step, by a one-
+        thread launch on the forward's first side stream, instead of after the last Adam launch, where it ended
+        the step's critical tail (rocprof, Model A: 4 us kernel + its dependency gap; profiles/r6_kernels_*).
+        Every Adam launch then uses t = step (AdamArgs::t_pre).  The launch waits for what the side stream's
+        first forward launch waits for (after the gather phase, which reads the cursor), and every Adam launch
+        follows it through the forward -> backward joins.  For the step runner (engine/step.py), which always
+        runs the forward before the update; phases run by hand keep the old form.  Idempotent; False (no
+        change) when the forward has no side stream."""
+        if self._step_early is not None:
+            return True
+        if not self.EARLY_STEP_COUNTER:
+            return False
+        ls = self.fwd_train.launches
+        i = next((i for i, l in enumerate(ls) if l.stream != 0), None)
+        if i is None:
+            return False
+        self._step_early = {"step": self.flat.step.data_ptr()}
+        ls.insert(i, Launch("step_inc", k_step_inc, self._step_early, stream=ls[i].stream, waits=tuple(ls[i].waits)))
+        for d in getattr(self, "_early_adam", []):
+            d.update(t_pre=1, inc_step=0)
+        self.set_optimizer(**self._opt_kwargs)
+        return True
+
+    def set_step_cursor(self, cursor: Optional[torch.Tensor]):
+        """The device int64 cursor of a batch-index schedule (gather_phase ``cursor``): the step-counter kernel
+        advances it together with the Adam step count (csrc/optim.hip step_inc_kernel) -- after the last Adam
+        launch, or early in the step (use_early_step_counter) -- after every gather block has read it.  None
+        detaches it."""
+        self._step_cursor = cursor
+        ds = [l.args[0] for l in self.opt["adam"].launches if l.name == "adam_pack"]
+        if self._step_early is not None:
+            ds = [self._step_early]
+        for d in ds:
+            if cursor is None:
+                d.pop("cursor", None)
+            else:
+                d["cursor"] = cursor.data_ptr()
     # -------------------------------------------------------------------------------------------
     def num_launches(self) -> dict:
         return {"forward_train": len(self.fwd_train), "backward": len(self.bwd), "adam": len(self.opt["adam"]) + 1}

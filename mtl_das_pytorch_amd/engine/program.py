@@ -294,6 +294,10 @@ def k_adam(d, st):
     lib().adam_pack(st, d)
 
 
+def k_step_inc(d, st):
+    lib().step_inc(d["step"], d.get("cursor", 0), st)
+
+
 class ExtEvent:
     """A HIP event recorded with ``hipEventRecordExternal`` while its stream captures (an event-record node of
     the graph, re-recorded at every replay), plainly otherwise; ``wait(stream)`` makes a torch stream wait for

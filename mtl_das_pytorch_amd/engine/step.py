@@ -84,6 +84,8 @@ class StepRunner:
             # an update inside the backward would use local, un-reduced gradients
             raise ValueError("data-parallel step with weight updates inside the backward: call "
                              "set_optimizer(data_parallel=True) before autotune_program")
+        if hasattr(program, "use_early_step_counter"):
+            program.use_early_step_counter()  # the step counter off the step's tail (every step runs the forward)
         if hasattr(program, "check_sync_bn"):
             program.check_sync_bn()  # every SyncBN collective the program promised is in its launch lists
         self.buckets = list(getattr(program, "buckets", None) or [(0, program.flat.numel)])
