@@ -370,6 +370,46 @@ def test_early_adam_matches_optimizer_phase(model_name, monkeypatch):
         assert torch.equal(a, b)
 
 
+def test_early_step_counter_matches_tail_counter():
+    """LoweredProgram.use_early_step_counter (the step runner's form for Model A): the Adam step counter advanced
+    by a launch on the forward's first side stream, every update using t = step, trains bitwise like the
+    phases run by hand with the counter advanced after the last Adam launch; the counter ends equal."""
+    from mtl_das_pytorch_amd.data.synthetic import generate
+    from mtl_das_pytorch_amd.engine.mtl import MTLProgram
+    from mtl_das_pytorch_amd.engine.step import StepRunner
+    from mtl_das_pytorch_amd.engine.tune import autotune_program
+    from mtl_das_pytorch_amd.models import build_model
+    X, d, e = generate(32, seed=6, device="cuda")
+    lab = torch.stack([d, e], 1)
+    out = []
+    for early in (False, True):
+        torch.manual_seed(0)
+        prog = MTLProgram(build_model("MTL"), 8, "cuda")
+        prog.set_optimizer(weight_decay=1e-5)
+        autotune_program(prog, measure=False)
+        prog.flat.lr.fill_(1e-3)
+        idx = [torch.arange(8, device="cuda") + 8 * (s % 4) for s in range(3)]
+        if early:
+            r = StepRunner(prog, X, lab, use_graph=False)
+            assert any(l.name == "step_inc" for l in prog.fwd_train.launches)
+            for i in idx:
+                r.train_step(i)
+        else:
+            assert not any(l.name == "step_inc" for l in prog.fwd_train.launches)
+            prog.opt["pack"].run()
+            for i in idx:
+                prog.gather_phase(X, lab, i, clear=True).run()
+                prog.fwd_train.run()
+                prog.bwd.run()
+                prog.opt["adam"].run()
+        torch.cuda.synchronize()
+        f = prog.flat
+        out.append([f.params.clone(), f.exp_avg.clone(), f.exp_avg_sq.clone(), f.step.clone()])
+    assert float(out[1][3][0]) == 3.0
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("model_name", ["MTL", "multi_classifier"])
 def test_index_schedule_matches_per_step_indices(model_name):
     """StepRunner.set_index_schedule: steps that gather the next row of a device-resident [nrows][B] index table
