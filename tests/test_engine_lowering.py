@@ -422,3 +422,29 @@ def test_stream_buckets_need_no_cut(model):
     recs = [(i, l.args[0]) for i, l in enumerate(ph.launches) if l.name == "ext_record"]
     assert [e for _, e in recs] == ["e0", "e1"]
     assert ph.launches[recs[0][0] - 1] is a0 and ph.launches[recs[0][0]].stream == 1
+
+
+def test_early_step_counter_placement():
+    """use_early_step_counter: the one-thread step-counter launch moves from after the last Adam launch to the
+    forward's first side-stream position (same stream and waits), every Adam launch then uses t = step and never
+    advances the counter itself, and a schedule cursor rides on the moved launch.  Off for Model C."""
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.models import Multi_Classifier
+    p = MTLProgram(MTL_Net(), 8, "cpu")
+    ls = p.fwd_train.launches
+    i = next(k for k, l in enumerate(ls) if l.stream != 0)
+    first = ls[i]
+    assert p.use_early_step_counter() and p.use_early_step_counter()  # idempotent
+    inc = [l for l in p.fwd_train.launches if l.name == "step_inc"]
+    assert len(inc) == 1 and p.fwd_train.launches[i] is inc[0] and p.fwd_train.launches[i + 1] is first
+    assert inc[0].stream == first.stream and inc[0].waits == first.waits
+    d = p.opt["adam"].launches[0].args[0]
+    assert d["t_pre"] == 1 and d["inc_step"] == 0
+    cur = torch.zeros(1, dtype=torch.int64)
+    p.set_step_cursor(cur)
+    assert inc[0].args[0]["cursor"] == cur.data_ptr() and "cursor" not in d
+    p.set_optimizer(weight_decay=1e-5)  # a rebuilt optimizer phase keeps the form
+    d = p.opt["adam"].launches[0].args[0]
+    assert d["t_pre"] == 1 and d["inc_step"] == 0 and "cursor" not in d
+    c = InceptionProgram(Multi_Classifier(init_weights=False), 4, "cpu")
+    assert not c.use_early_step_counter() and not any(l.name == "step_inc" for l in c.fwd_train.launches)
