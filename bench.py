@@ -187,6 +187,7 @@ def main():
     from mtl_das_pytorch_amd.data.synthetic import generate
     from mtl_das_pytorch_amd.engine.inception import InceptionProgram
     from mtl_das_pytorch_amd.engine.mtl import MTLProgram
+    from mtl_das_pytorch_amd.engine.lowering import build_for_stream_buckets
     from mtl_das_pytorch_amd.engine.step import StepRunner
     from mtl_das_pytorch_amd.engine.tune import autotune_program
     from mtl_das_pytorch_amd.models import build_model, encode_joint
@@ -211,14 +212,27 @@ def main():
     joint = args.model == "multi_classifier"
     sync = args.sync_bn and ctx.enabled
     sw = world if sync else 1
-    prog = (InceptionProgram(model, args.batch, dev, sync_world=sw) if joint
-            else MTLProgram(model, args.batch, dev, sync_world=sw))
-    if sync:  # the statistics collectives are captured into the step's HIP graph (RCCL)
-        n_sync = prog.enable_sync_bn(ctx.all_reduce_ordered_)
-    prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world,
-                       data_parallel=ctx.enabled or args.dp_shape > 1)
-    if hasattr(prog, "set_rng_stream"):  # Model C dropout: an independent mask stream per rank
-        prog.set_rng_stream(0, ctx.rank)
+    n_sync = 0
+
+    def make_prog(order=None):
+        nonlocal n_sync
+        p = (InceptionProgram(model, args.batch, dev, sync_world=sw, param_order=order) if joint
+             else MTLProgram(model, args.batch, dev, sync_world=sw))
+        if sync:  # the statistics collectives are captured into the step's HIP graph (RCCL)
+            n_sync = p.enable_sync_bn(ctx.all_reduce_ordered_)
+        p.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-5, grad_scale=1.0 / world,
+                        data_parallel=ctx.enabled or args.dp_shape > 1)
+        if hasattr(p, "set_rng_stream"):  # Model C dropout: an independent mask stream per rank
+            p.set_rng_stream(0, ctx.rank)
+        return p
+
+    def tuned(p, n_seg):
+        segs = p.segment_backward(n_seg)
+        autotune_program(p, out_path=os.path.join("gpurun_out", "tuned_cfgs.json") if ctx.is_main else None,
+                         measure=not args.no_tune)
+        return p, segs
+
+    prog = make_prog()
     # DP: gradient buckets whose all-reduces overlap the rest of the backward (engine/step.py), sized from the
     # all-reduce time of the whole flat gradient on the live group (a 1-rank rehearsal of N ranks, --dp-shape,
     # cannot measure N's all-reduce: it takes the model's default bucket count)
@@ -233,11 +247,14 @@ def main():
     # captured collectives: the backward cut at the bucket boundaries (segment_backward); eager RCCL behind the
     # graph's external events (the multi-rank default): buckets completed by side streams, no cut (stream_buckets)
     ext_form = not captured and (ctx.enabled or nb > 1)
-    buckets = prog.segment_backward(1 if ext_form else nb)
-    autotune_program(prog, out_path=os.path.join("gpurun_out", "tuned_cfgs.json") if ctx.is_main else None,
-                     measure=not args.no_tune)
     if ext_form and nb > 1:
-        buckets = prog.stream_buckets(nb)
+        # side-stream buckets; Model C is rebuilt with its side streams' parameters grouped (stream_param_order)
+        first = [prog]
+        del prog
+        prog, buckets = build_for_stream_buckets(lambda order: tuned(first.pop() if (order is None and first)
+                                                                     else make_prog(order), 1)[0], nb)
+    else:
+        prog, buckets = tuned(prog, 1 if ext_form else nb)
     f = prog.flat
     broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
     X, d, e = generate(args.dataset_size, seed=1000 + ctx.rank, device=dev, in_channels=args.in_channels)

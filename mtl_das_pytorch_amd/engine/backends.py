@@ -199,6 +199,7 @@ class EngineBackend(Backend):
                  weight_decay: float, loss_weights: Sequence[float] = (1.0, 1.0), use_graph: bool = True,
                  tune: bool = False, seed: int = 0, sync_bn: bool = False):
         from .inception import InceptionProgram
+        from .lowering import build_for_stream_buckets
         from .mtl import MTLProgram
         from .step import StepRunner
         from .tune import autotune_program
@@ -207,33 +208,50 @@ class EngineBackend(Backend):
         self.names, self.ncls = _report_tasks(model_type)
         sync = sync_bn and ctx.enabled
         sw = ctx.world if sync else 1
-        if model_type == "multi_classifier":
-            self.prog = InceptionProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), sync_world=sw)
-        else:
-            w = list(loss_weights) if model_type == "MTL" else [1.0]
-            self.prog = MTLProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), loss_weights=w, sync_world=sw)
-        if sync:  # SyncBN: BN statistics all-reduced inside the step (captured into the HIP graph on RCCL)
-            self.prog.enable_sync_bn(ctx.all_reduce_ordered_)
-            if not ctx.capturable_collectives:
-                # gloo (or MDA_CAPTURE_COLLECTIVES=0): the step runs its launches and collectives eagerly -- say
-                # so, this is several times slower
-                if ctx.is_main:
-                    print("SyncBN: collectives are not captured on this process group; the training step runs "
-                          "eagerly", flush=True)
-                use_graph = False
-        self.prog.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world,
-                                data_parallel=ctx.enabled)
-        if hasattr(self.prog, "set_rng_stream"):
-            self.prog.set_rng_stream(seed, ctx.rank)
+
+        def make(order=None):
+            if model_type == "multi_classifier":
+                p = InceptionProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), sync_world=sw,
+                                     param_order=order)
+            else:
+                w = list(loss_weights) if model_type == "MTL" else [1.0]
+                p = MTLProgram(model, batch, ctx.device, in_hw=tuple(X.shape[2:]), loss_weights=w, sync_world=sw)
+            if sync:  # SyncBN: BN statistics all-reduced inside the step (captured into the HIP graph on RCCL)
+                p.enable_sync_bn(ctx.all_reduce_ordered_)
+            p.set_optimizer(betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay, grad_scale=1.0 / ctx.world,
+                            data_parallel=ctx.enabled)
+            if hasattr(p, "set_rng_stream"):
+                p.set_rng_stream(seed, ctx.rank)
+            return p
+
+        self.prog = make()
+        if sync and not ctx.capturable_collectives:
+            # gloo (or MDA_CAPTURE_COLLECTIVES=0): the step runs its launches and collectives eagerly -- say so,
+            # this is several times slower
+            if ctx.is_main:
+                print("SyncBN: collectives are not captured on this process group; the training step runs "
+                      "eagerly", flush=True)
+            use_graph = False
         nb = self.prog.dp_buckets(ctx.world, calibrate_allreduce(ctx, self.prog.flat.numel))
         # captured collectives (a 1-rank RCCL group): the backward cut at the bucket boundaries; several ranks
-        # (eager RCCL behind the step graph's external bucket events): side-stream buckets, no cut
+        # (eager RCCL behind the step graph's external bucket events): side-stream buckets, no cut (Model C
+        # rebuilt with its side streams' parameters grouped, build_for_stream_buckets)
         captured = ctx.capturable_collectives and (sync or ctx.capture_gradients)
         ext_form = ctx.enabled and not captured and use_graph
-        self.prog.segment_backward(1 if ext_form else nb)
-        autotune_program(self.prog, measure=tune)
         if ext_form and nb > 1:
-            self.prog.stream_buckets(nb)
+            first = [self.prog]
+            self.prog = None
+
+            def tuned(order):
+                p = first.pop() if (order is None and first) else make(order)
+                p.segment_backward(1)
+                autotune_program(p, measure=tune)
+                return p
+
+            self.prog, _ = build_for_stream_buckets(tuned, nb)
+        else:
+            self.prog.segment_backward(1 if ext_form else nb)
+            autotune_program(self.prog, measure=tune)
         f = self.prog.flat
         broadcast_module_state(ctx, [f.params, f.bn_mean, f.bn_var, f.bn_nbt])
         lab_eval = labels_eval if labels_eval is not None else labels

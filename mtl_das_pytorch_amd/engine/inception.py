@@ -200,9 +200,13 @@ class InceptionProgram(LoweredProgram):
     # the step counter stays after the last Adam launch here: on the forward's first side stream it cost Model C
     # 0.7 % (9,567 / 9,566 vs 9,629 / 9,634 samples/s, interleaved; Model A +0.3 %, docs/PERF.md round 6)
     EARLY_STEP_COUNTER = False
+    # module order puts the stem (stream 0) first: build_for_stream_buckets rebuilds with stream_param_order
+    REORDER_FOR_STREAM_BUCKETS = True
 
     def __init__(self, model: Multi_Classifier, batch: int, device, in_hw=(100, 250), p_drop: float = 0.5,
-                 sync_world: int = 1):
+                 sync_world: int = 1, param_order=None):
+        """``param_order``: parameters laid out first in the flat buffers, in this order (LoweredProgram.
+        stream_param_order); the rest follow in module order."""
         if model.aux_logits:
             h6 = _mixed6_hw(in_hw)
             if min(h6) < 5:
@@ -226,7 +230,7 @@ class InceptionProgram(LoweredProgram):
             raise ValueError("in_channels > 8 not supported by the gather kernel")
         self.p_drop = float(p_drop)
         model.to(self.device)
-        self.flat = FlatState(model, self.device)
+        self.flat = FlatState(model, self.device, [list(param_order)] if param_order else ())
         self.flat.bn_world = sync_world  # SyncBN: global BN counts (enable_sync_bn adds the collectives)
         self.arena = Arena(self.device)
         self._alloc()

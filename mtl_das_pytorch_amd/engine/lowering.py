@@ -4,7 +4,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional
 
 import torch
 
@@ -515,17 +515,7 @@ class LoweredProgram:
         ls = self.bwd.launches
         if any(l.name == "cut" for l in ls):
             raise ValueError("stream_buckets needs an uncut backward (segment_backward(1))")
-        gbase = P(f.grads)
-        writers: Dict[int, set] = {}  # flat offset of a parameter's gradient -> {(stream, launch index)}
-        for i, l in enumerate(ls):
-            if l.name == "wgrad_finalize":
-                for c in (l.owner or self.convs):  # (no owner: the finalize covers every conv)
-                    for m in c.mods:
-                        writers.setdefault(f.off(m.weight), set()).add((l.stream, i))
-            elif l.fn is not None:
-                for off in _grad_offsets(l, gbase, f.numel):
-                    writers.setdefault(off, set()).add((l.stream, i))
-        side_fin = {l.stream: i for i, l in enumerate(ls) if l.name == "wgrad_finalize" and l.stream != 0}
+        writers, side_fin = self._grad_writers()
         buckets, anchors, k, lo = [], [], 0, 0
         order = f.order
         # (a parameter with no writer -- a conv bias feeding a BN, whose gradient is identically 0 -- is never
@@ -552,6 +542,49 @@ class LoweredProgram:
         anchors.append(fins[-1])
         self.buckets, self.bucket_anchors = buckets, anchors
         return buckets
+
+    def _grad_writers(self):
+        """(flat offset of a parameter's gradient -> {(stream, backward launch index)} of every launch writing
+        it, side stream -> index of its own weight-gradient finalize).  A batched launch (engine/inception.py
+        batch_tails: a device job table) writes what its ``owner`` launches would have."""
+        f = self.flat
+        gbase = P(f.grads)
+        writers: Dict[int, set] = {}
+        for i, l in enumerate(self.bwd.launches):
+            if l.name == "wgrad_finalize":
+                for c in (l.owner or self.convs):  # (no owner: the finalize covers every conv)
+                    for m in c.mods:
+                        writers.setdefault(f.off(m.weight), set()).add((l.stream, i))
+            elif l.fn is not None:
+                srcs = [l] + [o for o in (l.owner if isinstance(l.owner, (list, tuple)) else ())
+                              if isinstance(o, Launch)]
+                for src in srcs:
+                    for off in _grad_offsets(src, gbase, f.numel):
+                        writers.setdefault(off, set()).add((l.stream, i))
+        side_fin = {l.stream: i for i, l in enumerate(self.bwd.launches)
+                    if l.name == "wgrad_finalize" and l.stream != 0}
+        return writers, side_fin
+
+    def stream_param_order(self) -> Optional[list]:
+        """A parameter order for the flat buffers (FlatState ``param_groups``) under which stream_buckets finds
+        one bucket per side stream: first the parameters whose gradient only that side stream writes, no later
+        than its own finalize, side streams in finalize order; then the rest in module order.  A program built
+        with it (Model C: ``InceptionProgram(param_order=...)``, build_for_stream_buckets) all-reduces those
+        buckets while stream 0 still runs the rest of the backward.  Call on a program lowered like the one to
+        be built (autotuned, uncut).  None: no side stream finalizes a parameter of its own."""
+        f = self.flat
+        writers, side_fin = self._grad_writers()
+        cls = {}
+        for q in f.order:
+            w = writers.get(f.off(q))
+            sts = {s for s, _ in w} if w else set()
+            st = next(iter(sts)) if len(sts) == 1 else None
+            ok = st in side_fin and all(i <= side_fin[st] for _, i in w)
+            cls[id(q)] = st if ok else 0
+        sides = sorted((s for s in side_fin if any(c == s for c in cls.values())), key=lambda s: side_fin[s])
+        if not sides:
+            return None
+        return [q for s in sides for q in f.order if cls[id(q)] == s] + [q for q in f.order if cls[id(q)] == 0]
 
     def backward_with_allreduce(self, allreduce) -> Phase:
         """The backward with every gradient bucket's all-reduce embedded in it, so the whole
@@ -967,3 +1000,22 @@ class LoweredProgram:
     # -------------------------------------------------------------------------------------------
     def num_launches(self) -> dict:
         return {"forward_train": len(self.fwd_train), "backward": len(self.bwd), "adam": len(self.opt["adam"]) + 1}
+
+
+def build_for_stream_buckets(make: Callable, n_buckets: int):
+    """The eager-collective data-parallel program with up to ``n_buckets`` side-stream gradient buckets
+    (LoweredProgram.stream_buckets).  ``make(param_order)`` builds, configures and autotunes a program on an
+    uncut backward.  Where the parameter order the model's constructor gives has no side-stream prefix (Model C:
+    the stem comes first in module order, so its one bucket completed at the very end), the program is built a
+    second time with stream_param_order(), which groups each side stream's parameters.  Returns (program,
+    buckets)."""
+    prog = make(None)
+    if n_buckets > 1 and getattr(prog, "REORDER_FOR_STREAM_BUCKETS", False):
+        order = prog.stream_param_order()
+        if order is not None:
+            del prog
+            import gc
+            gc.collect()
+            torch.cuda.empty_cache()
+            prog = make(order)
+    return prog, prog.stream_buckets(n_buckets)

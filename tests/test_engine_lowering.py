@@ -448,3 +448,46 @@ def test_early_step_counter_placement():
     assert d["t_pre"] == 1 and d["inc_step"] == 0 and "cursor" not in d
     c = InceptionProgram(Multi_Classifier(init_weights=False), 4, "cpu")
     assert not c.use_early_step_counter() and not any(l.name == "step_inc" for l in c.fwd_train.launches)
+
+
+def test_stream_param_order_gives_model_c_side_stream_buckets():
+    """Model C's module order starts with the stem (stream 0), so stream_buckets finds no side-stream prefix;
+    rebuilt with stream_param_order (the parameters each side stream alone writes, grouped, in finalize order)
+    the multi-rank DP step gets one bucket per side stream, each complete at that stream's own finalize --
+    nothing writes it later or elsewhere, batched BN-tail launches (device job tables) included."""
+    from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.models import build_model
+
+    def make(order):
+        torch.manual_seed(0)
+        p = InceptionProgram(model, 8, "cpu", param_order=order)
+        p.set_optimizer(weight_decay=1e-5, data_parallel=True)
+        p.segment_backward(1)
+        p.merge_wgrad_cfgs()
+        p.refresh_wgrad_finalize()
+        p.batch_wgrads()
+        p.batch_tails()
+        return p
+
+    model = build_model("multi_classifier")
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    p0 = make(None)
+    assert len(p0.stream_buckets(4)) == 1  # module order: no side-stream prefix
+    order = p0.stream_param_order()
+    assert sorted(map(id, order)) == sorted(map(id, p0.flat.order))
+    del p0
+    p = make(order)
+    for k, v in model.state_dict().items():  # the rebuild keeps every value
+        assert torch.equal(v, sd[k]), k
+    b = p.stream_buckets(4)
+    f, ls = p.flat, p.bwd.launches
+    assert len(b) == 4 and b[0][0] == 0 and b[-1][1] == f.numel and all(b[i][1] == b[i + 1][0] for i in range(3))
+    assert sum(hi - lo for lo, hi in b[:3]) > f.numel // 2  # the Inception blocks' branch parameters
+    writers, side_fin = p._grad_writers()
+    anchors = p.bucket_anchors
+    assert [a.stream for a in anchors[:3]] == sorted(side_fin, key=side_fin.get) and anchors[3].stream == 0
+    for (lo, hi), a in zip(b[:3], anchors[:3]):
+        i0 = ls.index(a)
+        for q in f.order:
+            if lo <= f.off(q) < hi:
+                assert all(s == a.stream and i <= i0 for s, i in writers.get(f.off(q), ())), q.shape

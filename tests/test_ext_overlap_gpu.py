@@ -38,6 +38,7 @@ class _AddOne:
 def _run(model_type, buckets, graph, form, steps=3):
     from mtl_das_pytorch_amd.data.synthetic import generate
     from mtl_das_pytorch_amd.engine.inception import InceptionProgram
+    from mtl_das_pytorch_amd.engine.lowering import build_for_stream_buckets
     from mtl_das_pytorch_amd.engine.mtl import MTLProgram
     from mtl_das_pytorch_amd.engine.step import StepRunner
     from mtl_das_pytorch_amd.engine.tune import autotune_program
@@ -46,12 +47,20 @@ def _run(model_type, buckets, graph, form, steps=3):
     torch.manual_seed(1234)
     m = build_model(model_type)
     joint = model_type == "multi_classifier"
-    prog = InceptionProgram(m, B, "cuda") if joint else MTLProgram(m, B, "cuda")
-    prog.set_optimizer(weight_decay=1e-5, data_parallel=True)
-    nb = len(prog.segment_backward(buckets if form == "segmented" else 1))
-    autotune_program(prog, measure=False)
-    if form == "stream":
-        nb = len(prog.stream_buckets(buckets))
+
+    def make(order, nseg=1):
+        p = InceptionProgram(m, B, "cuda", param_order=order) if joint else MTLProgram(m, B, "cuda")
+        p.set_optimizer(weight_decay=1e-5, data_parallel=True)
+        p.segment_backward(nseg)
+        autotune_program(p, measure=False)
+        return p
+
+    if form == "stream":  # the multi-rank default (Model C rebuilt with stream_param_order)
+        prog, bl = build_for_stream_buckets(make, buckets)
+        nb = len(bl)
+    else:
+        prog = make(None, buckets)
+        nb = len(prog.buckets)
     X, d, e = generate(4 * B, seed=11, device="cuda")
     labels = encode_joint(d, e) if joint else torch.stack([d, e], 1)
     runner = StepRunner(prog, X, labels, use_graph=graph, allreduce=_AddOne())
@@ -67,7 +76,8 @@ def _run(model_type, buckets, graph, form, steps=3):
 
 
 @pytest.mark.parametrize("model_type,buckets,form", [("MTL", 2, "stream"), ("MTL", 2, "segmented"),
-                                                     ("multi_classifier", 4, "segmented")])
+                                                     ("multi_classifier", 4, "segmented"),
+                                                     ("multi_classifier", 4, "stream")])
 def test_external_bucket_events_order_the_collectives(model_type, buckets, form):
     """form "stream": LoweredProgram.stream_buckets (the multi-rank default: buckets completed by a side stream's
     finalize, no cut); "segmented": segment_backward's cut backward (bucket events after each bucket's finalize)."""
