@@ -539,7 +539,9 @@ class LoweredProgram:
             lo, k = hi, j
         fins = [l for l in ls if l.name == "wgrad_finalize"]
         buckets.append((lo, f.numel))
-        anchors.append(fins[-1])
+        # the remainder is complete once every stream has joined stream 0 after its finalize (batch_wgrads)
+        after = ls[ls.index(fins[-1]) + 1] if ls.index(fins[-1]) + 1 < len(ls) else None
+        anchors.append(after if after is not None and after.name == "join_side" else fins[-1])
         self.buckets, self.bucket_anchors = buckets, anchors
         return buckets
 
@@ -750,6 +752,8 @@ class LoweredProgram:
     # C +0.6-7.5 % / A neutral, and A +0.3-0.6 % / C neutral (docs/PERF.md round 4); class switches for A/B runs
     SIDE_FINALIZE = True
     EARLY_ADAM = True
+    # stream 0's tail finalize waits for every side stream's last launch (the round-5 form; class switch)
+    JOIN_AT_FINALIZE = False
 
     def batch_wgrads(self):
         """Replace the per-conv weight-gradient launches by batched launches, one per (stream, tile
@@ -848,8 +852,18 @@ class LoweredProgram:
         for l in keep:  # the per-conv "wgrads" event is gone
             if l.record == "wgrads":
                 l.record = None
-        ls[fin].waits = tuple(tags)
-        self.bwd.launches = keep + ls[fin:]
+        side_tags = tuple(t for t in tags if t != "wgrads_s0")
+        if self.SIDE_FINALIZE and side and not self.JOIN_AT_FINALIZE:
+            # stream 0's finalize reduces stream 0's convs only: it follows its own batches in stream order, and
+            # the side streams (their finalize, early Adam) join stream 0 after it -- a pseudo-launch, the last
+            # bucket's anchor (stream_buckets) -- instead of delaying it (A: the tail finalize waited ~20 us
+            # for stream 1's early Adam, profiles/r6_timeline_modelA_end.txt)
+            ls[fin].waits = ()
+            self.bwd.launches = keep + ls[fin:fin + 1] + [Launch("join_side", None, stream=0, waits=side_tags)] \
+                + ls[fin + 1:]
+        else:
+            ls[fin].waits = tuple(tags)
+            self.bwd.launches = keep + ls[fin:]
         self.wgrads_batched = True
 
     def _wgrad_batch_launch(self, cfg: int, group: List[Launch], st: int, bucket: int = 0) -> Launch:

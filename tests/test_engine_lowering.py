@@ -116,16 +116,17 @@ def test_wgrad_batching_structure():
     p.batch_wgrads()
     b = [l for l in p.bwd.launches if l.name == "wgrad_batched"]
     assert sum(l.args[2] for l in b) == n_wg
-    fin = p.bwd.launches[-1]
-    assert fin.name == "wgrad_finalize" and fin.stream == 0
+    fin, join = p.bwd.launches[-2:]
+    assert fin.name == "wgrad_finalize" and fin.stream == 0 and join.name == "join_side" and join.fn is None
     fins = [l for l in p.bwd.launches if l.name == "wgrad_finalize"]
     # side streams finalize their own convs right after their batches; the tail finalize keeps stream 0's
-    # and waits for stream 0's batches and every side finalize; every conv is finalized exactly once
+    # and follows stream 0's batches in stream order, then every side stream joins stream 0; every conv is
+    # finalized exactly once
     side = [l for l in fins if l.stream != 0]
     assert {l.stream for l in side} == {l.stream for l in b} - {0}
-    # (with EARLY_ADAM each side stream's last launch is its partial Adam update, which the tail waits for)
+    # (with EARLY_ADAM each side stream's last launch is its partial Adam update, which the join waits for)
     last = {st: [l for l in p.bwd.launches if l.stream == st][-1] for st in {l.stream for l in side}}
-    assert set(fin.waits) == {"wgrads_s0"} | {l.record for l in last.values()}
+    assert fin.waits == () and set(join.waits) == {l.record for l in last.values()}
     assert all(l.name == ("adam_pack_early" if p.EARLY_ADAM else "wgrad_finalize") for l in last.values())
     owners = [c for l in fins for c in l.owner]
     assert len(owners) == len(set(map(id, owners))) == len(p.convs)
@@ -410,7 +411,7 @@ def test_stream_buckets_need_no_cut(model):
     f, ls = p.flat, p.bwd.launches
     assert len(b) == 2 and b[0][0] == 0 and b[0][1] == b[1][0] and b[1][1] == f.numel and b[0][1] > f.numel // 5
     a0, a1 = p.bucket_anchors
-    assert a0.name == a1.name == "wgrad_finalize" and a0.stream == 1 and a1 is ls[-1]
+    assert a0.name == "wgrad_finalize" and a0.stream == 1 and a1.name == "join_side" and a1 is ls[-1]
     i0 = next(i for i, l in enumerate(ls) if l is a0)
     gbase = P(f.grads)
     for i, l in enumerate(ls):  # nothing writes bucket 0 after stream 1's finalize, or on another stream
