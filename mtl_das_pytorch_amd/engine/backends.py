@@ -273,12 +273,7 @@ class EngineBackend(Backend):
         """Train the coming steps from the device-resident [nbatches][B] index schedule (StepRunner.
         set_index_schedule).  An epoch of the same shape reuses the schedule buffer the captured graph reads
         (copy + cursor reset, no re-capture)."""
-        r = self.runner
-        if r.schedule is not None and r.schedule.shape == schedule.shape:
-            r.schedule.copy_(schedule)
-            r.cursor.zero_()
-        else:
-            r.set_index_schedule(schedule.to(torch.int64))
+        self.runner.restart_schedule(schedule.to(torch.int64))
 
     def set_eval_data(self, X: torch.Tensor, labels: torch.Tensor):
         self.runner.set_eval_source(X, labels)

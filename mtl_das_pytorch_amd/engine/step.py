@@ -109,6 +109,14 @@ class StepRunner:
         self.cursor = torch.zeros(1, dtype=torch.int64, device=self.p.device)
         self.p.set_step_cursor(self.cursor)
 
+    def restart_schedule(self, schedule: torch.Tensor):
+        """Start the schedule over with new rows of the same shape (the next epoch): copied into the buffer the
+        captured graphs read, cursor back to row 0, no re-capture."""
+        if self.schedule is None or self.schedule.shape != schedule.shape:
+            return self.set_index_schedule(schedule)
+        self.schedule.copy_(schedule)
+        self.cursor.zero_()
+
     # -------------------------------------------------------------------------------------------
     def _mutable_state(self) -> List[torch.Tensor]:
         f = self.p.flat
