@@ -86,6 +86,18 @@ DEV bf16x8 tr_read8(const bf16_t* lds_row0, int ld_elems, int col0, int lane) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// lane l receives column col0 + (l & 31) of rows 8 (l >> 5) .. 8 (l >> 5) + 7 of a pixel-major LDS image: the A
+// (row = l & 31) or B (column = l & 31) operand of a 32x32x16 MFMA whose k index is the row
+DEV bf16x8 tr_read32(const bf16_t* lds_row0, int ld, int col0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const bf16_t* a0 = lds_row0 + (8 * (g >> 1) + (i >> 2)) * ld + col0 + 16 * (g & 1) + 4 * (i & 3);
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + 4 * ld));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
 DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 // round-to-nearest-even; NaN-preserving via the hardware conversion
 DEV bf16_t f2bf(float f) {

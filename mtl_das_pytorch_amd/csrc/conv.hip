@@ -633,17 +633,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_batched_kernel(const WgradJob*
 // MFMAs of 16K MACs, and the operands are staged 2-4x less often.  Chunks of 64 pixels; the pitch of the
 // pixel-major LDS images (width + 32 elements) puts the 4 rows of a transposed read (32 columns each) on
 // disjoint bank quarters.  K tiles may run past Kpad (their columns stage zeros and are not stored).
-DEV bf16x8 tr_read32(const bf16_t* lds_row0, int ld, int col0, int lane) {
-  // lane l receives column col0 + (l & 31) of rows 8 (l >> 5) .. 8 (l >> 5) + 7: the A (row = l & 31) or
-  // B (column = l & 31) operand of a 32x32x16 MFMA whose k index is the row
-  const int i = lane & 15, g = lane >> 4;
-  const bf16_t* a0 = lds_row0 + (8 * (g >> 1) + (i >> 2)) * ld + col0 + 16 * (g & 1) + 4 * (i & 3);
-  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
-  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + 4 * ld));
-  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <int TN, int TK>
 DEV void wgrad_big_block(const WgradArgs& a, const int tile, const int split, const int z) {

@@ -278,7 +278,8 @@ int launch_wgrad(const WgradArgs& a, int G, int cfg, hipStream_t st);
 int wgrad_tile_shape(int cfg, int& TN, int& TK);
 constexpr int WGRAD_PATCH_CFG0 = 12, WGRAD_PATCH_NCFG = 8;  // wgrad cfgs 12-19: 3x3/s1 patch kernels (conv.hip)
 constexpr int WGRAD_BIG_CFG0 = 32, WGRAD_BIG_NCFG = 4;  // wgrad cfgs 32-35: 32x32x16 large-tile kernels
-constexpr int WGRAD_LEAN_CFG0 = 36, WGRAD_LEAN_NCFG = 8;  // wgrad cfgs 36-43: lean-staging im2col (wgrad_lean.hip)
+constexpr int WGRAD_LEAN_CFG0 = 36, WGRAD_LEAN_NCFG = 12;  // wgrad cfgs 36-47: lean-staging im2col (wgrad_lean.hip;
+                                                             // 44-47 on the 32x32x16 MFMA)
 int wgrad_lean_shape(int cfg, int& TN, int& TK);
 int wgrad_lean_ntiles(int cfg, const WgradArgs& a);
 int launch_wgrad_lean(const WgradArgs& a, int G, int cfg, hipStream_t st);

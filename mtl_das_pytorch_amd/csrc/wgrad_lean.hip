@@ -18,18 +18,28 @@
 //     zeroed by a select, so no exec-mask divergence splits the staging;
 //   * 32-bit offsets (every operand here is < 2^31 elements; checked on the host).
 // Normalise-on-load inputs (the forward conv read act(BN(y))) are rebuilt on the way into LDS, as in wgrad_block.
+//
+// Configs 44-47 (BIG) are the same staging under wgrad_big_block's compute: 64 x 64 .. 128 x 128 tiles on the
+// 32x32x16 MFMA, each wave a (TN/2) x (TK/2) quarter of 32x32 accumulators, 64-pixel chunks -- the throughput
+// form for batched launches of many jobs (Model C's Inception weight gradients: lean 16x16 tiles were 2x faster
+// per job alone but 45 % slower as batches, profiles/r6_wgrad_lean.md).  They split M like the large tiles
+// (engine/core.py wgrad_plan), not like the lean 16x16 configs.
 #include "kernels.h"
 
 namespace mda {
 
-// (TN, TK); keep in sync with ops/functional.py WGRAD_TILES (entries WGRAD_LEAN_CFG0..)
-// (TN, TK, MCH pixels per chunk)
+// (TN, TK, MCH pixels per chunk, 32x32x16 MFMA); keep in sync with ops/functional.py WGRAD_TILES (entries
+// WGRAD_LEAN_CFG0..)
 #define WGRAD_LEAN_CASES(X)                                                                                   \
-  case 36: X(16, 64, 256) case 37: X(16, 144, 128) case 38: X(32, 64, 256) case 39: X(32, 144, 128)           \
-  case 40: X(64, 64, 128) case 41: X(64, 128, 128) case 42: X(128, 64, 128) case 43: X(128, 128, 64)
+  case 36: X(16, 64, 256, false) case 37: X(16, 144, 128, false) case 38: X(32, 64, 256, false)               \
+  case 39: X(32, 144, 128, false) case 40: X(64, 64, 128, false) case 41: X(64, 128, 128, false)              \
+  case 42: X(128, 64, 128, false) case 43: X(128, 128, 64, false)                                             \
+  case 44: X(64, 64, 64, true) case 45: X(64, 128, 64, true) case 46: X(128, 64, 64, true)                    \
+  case 47: X(128, 128, 64, true)
 
 int wgrad_lean_shape(int cfg, int& TN, int& TK) {
-  static const int tn[] = {16, 16, 32, 32, 64, 64, 128, 128}, tk[] = {64, 144, 64, 144, 64, 128, 64, 128};
+  static const int tn[] = {16, 16, 32, 32, 64, 64, 128, 128, 64, 64, 128, 128};
+  static const int tk[] = {64, 144, 64, 144, 64, 128, 64, 128, 64, 128, 64, 128};
   if (cfg < WGRAD_LEAN_CFG0 || cfg >= WGRAD_LEAN_CFG0 + WGRAD_LEAN_NCFG) return -1;
   TN = tn[cfg - WGRAD_LEAN_CFG0];
   TK = tk[cfg - WGRAD_LEAN_CFG0];
@@ -48,15 +58,19 @@ DEV int lean_encode(int i, int Ktot, int Cs8, int KW, int C0) {
 
 constexpr int LEAN_BAD_ROW = -16384;  // first-tap row of a pixel past the split: every tap lands outside the image
 
-template <int TN, int TK, int MCH>
+template <int TN, int TK, int MCH, bool BIG>
 DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, const int z) {
   static_assert(MCH % 64 == 0 && MCH <= 256, "chunk of 64..256 pixels (pixel table: one entry per thread)");
-  // row pitches: 16 x odd elements, so the 8 rows a transposed read touches tile the 64 banks (wgrad_block)
-  constexpr int LDY = (TN / 16) % 2 ? TN : TN + 16, LDX = (TK / 16) % 2 ? TK : TK + 16;
+  static_assert(!BIG || (TN % 64 == 0 && TK % 64 == 0), "32x32 quarters per wave");
+  // row pitches: 16 x odd elements, so the 8 rows a transposed read touches tile the 64 banks (wgrad_block);
+  // BIG: width + 32, the 4 rows of a 32-column transposed read on disjoint bank quarters (wgrad_big_block)
+  constexpr int LDY = BIG ? TN + 32 : ((TN / 16) % 2 ? TN : TN + 16);
+  constexpr int LDX = BIG ? TK + 32 : ((TK / 16) % 2 ? TK : TK + 16);
   constexpr int YG = TN / 8, KG = TK / 8;
   constexpr int VY = MCH * YG, VX = MCH * KG;
   constexpr int NY = (VY + 255) / 256, NX = (VX + 255) / 256;
-  constexpr int FN = TN / 16, FK = TK / 16, NFR = FN * FK, FPW = (NFR + 3) / 4;
+  constexpr int FN = TN / 16, FK = TK / 16, NFR = FN * FK, FPW = BIG ? 1 : (NFR + 3) / 4;
+  constexpr int FA = BIG ? TN / 64 : 1, FB = BIG ? TK / 64 : 1;  // BIG: 32x32 accumulators of a wave
   __shared__ __attribute__((aligned(16))) bf16_t s_dy[MCH * LDY];
   __shared__ __attribute__((aligned(16))) bf16_t s_x[MCH * LDX];
   __shared__ int s_pix[2][MCH];  // (b * Hi + ih0) * Wi + iw0 of the chunk's pixels
@@ -158,6 +172,16 @@ DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, c
   f32x4 acc[FPW];
 #pragma unroll
   for (int j = 0; j < FPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x16 bacc[FA][FB];
+  const int wn = (wid & 1) * (TN / 2), wk = (wid >> 1) * (TK / 2);
+  if (BIG) {
+#pragma unroll
+    for (int i = 0; i < FA; ++i)
+#pragma unroll
+      for (int j = 0; j < FB; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bacc[i][j][r] = 0.f;
+  }
 
   if (mbeg < mend) LEAN_LOAD(0, mbeg);
   int buf = 0;
@@ -190,8 +214,23 @@ DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, c
     if (more) pix_table(buf ^ 1, mc + MCH);  // (last read by the load of chunk mc, before the previous barrier)
     __syncthreads();
     if (more) LEAN_LOAD(buf ^ 1, mc + MCH);  // in flight during this chunk's MFMAs
+    if (BIG) {
 #pragma unroll
-    for (int kk = 0; kk < MCH / 32; ++kk) {
+      for (int ks = 0; ks < MCH / 16; ++ks) {
+        bf16x8 av[FA], bv[FB];
+#pragma unroll
+        for (int i = 0; i < FA; ++i) av[i] = tr_read32(&s_dy[ks * 16 * LDY], LDY, wn + 32 * i, lane);
+#pragma unroll
+        for (int j = 0; j < FB; ++j) bv[j] = tr_read32(&s_x[ks * 16 * LDX], LDX, wk + 32 * j, lane);
+#pragma unroll
+        for (int i = 0; i < FA; ++i)
+#pragma unroll
+          for (int j = 0; j < FB; ++j)
+            bacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], bacc[i][j], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < (BIG ? 0 : MCH / 32); ++kk) {
       const int prow = kk * 32 + 16 * (lane >> 5) + 4 * ((lane >> 4) & 1);
 #pragma unroll
       for (int j = 0; j < FPW; ++j) {
@@ -209,6 +248,23 @@ DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, c
   }
 #undef LEAN_LOAD
   float* slab = a.slab + (((int64_t)z * a.splits + split) * a.Npad) * a.Kpad;
+  if (BIG) {
+#pragma unroll
+    for (int i = 0; i < FA; ++i)
+#pragma unroll
+      for (int j = 0; j < FB; ++j) {
+        const int col = k0 + wk + 32 * j + (lane & 31);
+        const int row0 = n0 + wn + 32 * i + 4 * (lane >> 5);
+        if (col < a.Kpad) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = row0 + (r & 3) + 8 * (r >> 2);
+            if (row < a.Npad) slab[(int64_t)row * a.Kpad + col] = bacc[i][j][r];
+          }
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < FPW; ++j) {
     const int fr = wid + 4 * j;
@@ -225,12 +281,12 @@ DEV void wgrad_lean_block(const WgradArgs& a, const int tile, const int split, c
   }
 }
 
-template <int TN, int TK, int MCH>
+template <int TN, int TK, int MCH, bool BIG>
 __global__ __launch_bounds__(256) void conv_wgrad_lean_kernel(WgradArgs a) {
-  wgrad_lean_block<TN, TK, MCH>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+  wgrad_lean_block<TN, TK, MCH, BIG>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
-template <int TN, int TK, int MCH>
+template <int TN, int TK, int MCH, bool BIG>
 __global__ __launch_bounds__(256) void conv_wgrad_lean_batched_kernel(const WgradJob* __restrict__ jobs, int nj,
                                                                        int64_t nvb) {
   for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
@@ -243,7 +299,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_lean_batched_kernel(const Wgra
     const int local = (int)(vb - J.block0);
     const int per_z = J.ntiles * J.a.splits;
     const int z = local / per_z, r = local - z * per_z;
-    wgrad_lean_block<TN, TK, MCH>(J.a, r % J.ntiles, r / J.ntiles, z);
+    wgrad_lean_block<TN, TK, MCH, BIG>(J.a, r % J.ntiles, r / J.ntiles, z);
     __syncthreads();  // the next virtual block re-stages the LDS tables
   }
 }
@@ -267,8 +323,8 @@ int wgrad_lean_ntiles(int cfg, const WgradArgs& a) {
 int launch_wgrad_lean(const WgradArgs& a, int G, int cfg, hipStream_t st) {
   const int nt = wgrad_lean_ntiles(cfg, a);
   if (nt < 0) return nt;
-#define LAUNCH_WGL(TN, TK, MCH)                                                                            \
-  hipLaunchKernelGGL((conv_wgrad_lean_kernel<TN, TK, MCH>), dim3(nt, a.splits, G), dim3(256), 0, st, a);   \
+#define LAUNCH_WGL(TN, TK, MCH, BIG)                                                                          \
+  hipLaunchKernelGGL((conv_wgrad_lean_kernel<TN, TK, MCH, BIG>), dim3(nt, a.splits, G), dim3(256), 0, st, a); \
   break;
   switch (cfg) {
     WGRAD_LEAN_CASES(LAUNCH_WGL)
@@ -279,8 +335,8 @@ int launch_wgrad_lean(const WgradArgs& a, int G, int cfg, hipStream_t st) {
 }
 
 int launch_wgrad_lean_batched(int cfg, const WgradJob* d_jobs, int nj, int64_t nblocks, dim3 grid, hipStream_t st) {
-#define LAUNCH_WGLB(TN, TK, MCH)                                                                                    \
-  hipLaunchKernelGGL((conv_wgrad_lean_batched_kernel<TN, TK, MCH>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \
+#define LAUNCH_WGLB(TN, TK, MCH, BIG)                                                                               \
+  hipLaunchKernelGGL((conv_wgrad_lean_batched_kernel<TN, TK, MCH, BIG>), grid, dim3(256), 0, st, d_jobs, nj, nblocks); \
   break;
   switch (cfg) {
     WGRAD_LEAN_CASES(LAUNCH_WGLB)

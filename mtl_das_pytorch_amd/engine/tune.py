@@ -17,7 +17,7 @@ import torch
 
 from ..ops.functional import (CONV_DEEP_CFG0, CONV_DEEP_NCFG, CONV_GLDS_CFG0, CONV_GLDS_NCFG, CONV_LDS_CFG0,
                               CONV_LDS_NCFG, CONV_PATCH_CFG0, CONV_PATCH_NCFG, CONV_PATCHP_CFG0, CONV_PATCHP_NCFG,
-                              CONV_XCD, GDEEP_TILES, WGRAD_BIG0, WGRAD_LEAN0, WGRAD_LEAN_N, WGRAD_PATCH, WGRAD_TILES,
+                              CONV_XCD, GDEEP_TILES, WGRAD_BIG0, WGRAD_LEAN0, WGRAD_LEAN_N, WGRAD_LEANBIG0, WGRAD_PATCH, WGRAD_TILES,
                               conv_workspace,
                               glds_cfg)
 from ..ops.hip import lib
@@ -364,8 +364,9 @@ def tune_wgrad_in_step(make_prog, X: torch.Tensor, labels: torch.Tensor, cache: 
         res.sort()
         big = WGRAD_BIG0 + 2 * (conv.Npad > 64) + (conv.Kpad_w > 64)
         cands = [c for _, c in res[:topk]]
-        if big in {c for _, c in res} and big not in cands:
-            cands.append(big)
+        for c in (big, big - WGRAD_BIG0 + WGRAD_LEANBIG0):  # the large tile and its lean-staging form
+            if c in {c2 for _, c2 in res} and c not in cands:
+                cands.append(c)
         ranked[sig] = cands
     del base
     torch.cuda.empty_cache()

@@ -233,9 +233,12 @@ WGRAD_TILES = {0: (16, 32, 128), 1: (32, 32, 128), 2: (32, 64, 64), 3: (64, 64, 
                # lean-staging im2col tiles (csrc/wgrad_lean.hip: per-chunk pixel table in LDS, per-thread staging
                # constants, branch-free loads); partial last K tile
                36: (16, 64, 256), 37: (16, 144, 128), 38: (32, 64, 256), 39: (32, 144, 128), 40: (64, 64, 128),
-               41: (64, 128, 128), 42: (128, 64, 128), 43: (128, 128, 64)}
+               41: (64, 128, 128), 42: (128, 64, 128), 43: (128, 128, 64),
+               # the same staging under the large tiles' 32x32x16 MFMA compute and M split (cfg 32-35 + 12)
+               44: (64, 64, 64), 45: (64, 128, 64), 46: (128, 64, 64), 47: (128, 128, 64)}
 WGRAD_BIG0 = 32
-WGRAD_LEAN0, WGRAD_LEAN_N = 36, 8
+WGRAD_LEAN0, WGRAD_LEAN_N = 36, 8   # lean 16x16x32 configs (their own M split: engine/core.py wgrad_plan)
+WGRAD_LEANBIG0 = 44                 # lean large tiles 44-47: WGRAD_BIG0 + i -> WGRAD_LEANBIG0 + i
 
 
 def wgrad_ktiles(cfg: int, Kpad: int) -> int:

@@ -193,13 +193,14 @@ def test_conv_wgrad_big_two_segment(fn, cfg):
                                   (2, 5, 11, 128, 128, 3, 1, 1), (2, 4, 13, 64, 96, (1, 7), 1, (0, 3)),
                                   (2, 4, 13, 64, 48, (7, 1), 1, (3, 0)), (2, 23, 60, 80, 192, 3, 1, 0),
                                   (2, 5, 11, 256, 64, 1, 1, 0), (2, 33, 83, 8, 16, 1, 1, 0), (3, 9, 21, 32, 24, 3, 2, 1)])
-@pytest.mark.parametrize("cfg", list(range(36, 44)))
+@pytest.mark.parametrize("cfg", list(range(36, 48)))
 @pytest.mark.parametrize("nol", [False, True])
 def test_conv_wgrad_lean(fn, case, cfg, nol):
-    """Lean-staging weight gradients (configs 36-43, csrc/wgrad_lean.hip: per-chunk pixel table in LDS,
-    per-thread staging constants, branch-free loads): 16-128-row tiles with Cout below / not a multiple of the
-    tile, K tiles past the padded reduction (144-wide tiles over Kpad 192 / 320 ...), strided and rectangular
-    kernels, valid padding, 1x1 convs, pixel counts that end mid-chunk, and normalise-on-load of the input."""
+    """Lean-staging weight gradients (configs 36-47, csrc/wgrad_lean.hip: per-chunk pixel table in LDS,
+    per-thread staging constants, branch-free loads; 44-47 on the 32x32x16 MFMA): 16-128-row tiles with Cout
+    below / not a multiple of the tile, K tiles past the padded reduction (144-wide tiles over Kpad 192 / 320
+    ...), strided and rectangular kernels, valid padding, 1x1 convs, pixel counts that end mid-chunk, and
+    normalise-on-load of the input."""
     B, H, W, C, Co, k, s, p = case
     x, w, _, _, _ = _mk(case, seed=cfg + 21)
     g = torch.Generator().manual_seed(cfg + 23)
@@ -221,7 +222,7 @@ def test_conv_wgrad_lean(fn, case, cfg, nol):
     assert rel(dw, ref) < 1e-5  # same bf16 operands, fp32 accumulation: only the summation order differs
 
 
-@pytest.mark.parametrize("cfg", [38, 43])
+@pytest.mark.parametrize("cfg", [38, 43, 47])
 def test_conv_wgrad_lean_two_segment(fn, cfg):
     """Lean weight gradient of a conv reading two concatenated inputs (the Inception concat)."""
     g = torch.Generator().manual_seed(6)

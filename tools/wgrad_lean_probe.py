@@ -1,6 +1,7 @@
 """Weight-gradient jobs of a model, one by one: the isolated time of the shipped tile config against every valid
-lean-staging config (csrc/wgrad_lean.hip, configs 36-43) at the split counts ConvLayer.wgrad_plan gives them,
-and the batched launches per stream with the shipped configs vs each job on its fastest lean config.
+lean-staging config (csrc/wgrad_lean.hip, configs 36-47) at the split counts ConvLayer.wgrad_plan gives them,
+and the batched launches per stream with the shipped configs vs each job on its fastest lean config vs the shipped
+table with its large tiles (32-35) on their lean-staging twins (44-47).
 
     python tools/wgrad_lean_probe.py [MTL|multi_classifier]
 """
@@ -13,10 +14,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mtl_das_pytorch_amd.data.synthetic import generate  # noqa: E402
 from mtl_das_pytorch_amd.engine.tune import _time, autotune_program  # noqa: E402
 from mtl_das_pytorch_amd.models import build_model, encode_joint  # noqa: E402
-from mtl_das_pytorch_amd.ops.functional import WGRAD_LEAN0, WGRAD_LEAN_N  # noqa: E402
+from mtl_das_pytorch_amd.ops.functional import WGRAD_BIG0, WGRAD_LEAN0, WGRAD_LEAN_N, WGRAD_LEANBIG0  # noqa: E402
 from mtl_das_pytorch_amd.ops.hip import lib  # noqa: E402
 
-LEAN = list(range(WGRAD_LEAN0, WGRAD_LEAN0 + WGRAD_LEAN_N))
+LEAN = list(range(WGRAD_LEAN0, WGRAD_LEAN0 + WGRAD_LEAN_N)) + list(range(WGRAD_LEANBIG0, WGRAD_LEANBIG0 + 4))
 
 
 def main():
@@ -66,7 +67,10 @@ def main():
               flush=True)
     # batched launches per stream: shipped configs vs every job on its best lean config (one batch per config)
     prog.wgrad_tables = []
-    for label, pick in (("shipped", shipped), ("lean", best)):
+    # the shipped table with every large-tile job (32-35) on its lean-staging twin (44-47): same tiles and M split,
+    # only the staging differs -- the throughput comparison of the two staging forms
+    twin = {k: (c - WGRAD_BIG0 + WGRAD_LEANBIG0 if WGRAD_BIG0 <= c < WGRAD_BIG0 + 4 else c) for k, c in shipped.items()}
+    for label, pick in (("shipped", shipped), ("lean", best), ("leanbig-twins", twin)):
         tot = 0.0
         for l in wg:
             l.owner.set_wgrad_cfg(pick[id(l)])
